@@ -70,22 +70,23 @@ static int rd_full(rdr *r, uint8_t *dst, size_t k) {
   return 0;
 }
 
-/* binary.ReadUvarint (encoding/binary): EOF on empty, overflow after 10 bytes. */
+/* binary.ReadUvarint (encoding/binary, Go 1.13): keeps reading while the
+ * continuation bit is set; EOF from the reader is returned as is; overflow is
+ * reported only when the terminating byte arrives (i > 9 || i == 9 && b > 1). */
 static int rd_uvarint(rdr *r, uint64_t *out) {
   uint64_t x = 0;
   unsigned s = 0;
-  for (int i = 0; i < 10; i++) {
+  for (int i = 0;; i++) {
     if (r->pos >= r->n) return PQR_ERR_EOF;
     uint8_t b = r->p[r->pos++];
     if (b < 0x80) {
-      if (i == 9 && b > 1) return PQR_ERR_RLE; /* overflow */
-      *out = x | ((uint64_t)b << s);
+      if (i > 9 || (i == 9 && b > 1)) return PQR_ERR_RLE; /* overflow */
+      *out = x | ((uint64_t)b << (s & 63));
       return 0;
     }
-    x |= (uint64_t)(b & 0x7f) << s;
+    if (s < 64) x |= (uint64_t)(b & 0x7f) << s;
     s += 7;
   }
-  return PQR_ERR_RLE; /* overflow */
 }
 /* readUVariant32 helpers.go:149-165 */
 static int rd_uvarint32(rdr *r, int32_t *out, int range_err) {

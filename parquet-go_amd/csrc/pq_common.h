@@ -1,0 +1,95 @@
+// pq_common.h — POD types shared by the host planner (pq_host.cpp) and the
+// HIP kernels (pq_kernels.hip).  Everything here lives in HBM as flat arrays:
+// one PageDesc per page of the batch (the descriptor table), one ColDesc per
+// selected leaf, one PageInfo per page (written by the device).
+#pragma once
+#include <stdint.h>
+
+namespace pq {
+
+// parquet.Encoding (parquet/parquet.go:343-354)
+enum : uint8_t { ENC_PLAIN = 0, ENC_PLAIN_DICT = 2, ENC_RLE = 3, ENC_BIT_PACKED = 4, ENC_DELTA_BP = 5,
+                 ENC_DELTA_LBA = 6, ENC_DELTA_BA = 7, ENC_RLE_DICT = 8 };
+// parquet.Type
+enum : int32_t { T_BOOLEAN = 0, T_INT32 = 1, T_INT64 = 2, T_INT96 = 3, T_FLOAT = 4, T_DOUBLE = 5,
+                 T_BYTE_ARRAY = 6, T_FLBA = 7 };
+
+enum : uint8_t { PAGE_V1 = 0, PAGE_V2 = 1, PAGE_DICT = 2 };
+
+// Where the uncompressed values section of a page comes from.
+enum : uint8_t { BODY_RAW = 0,        // uncompressed: body == payload in the input buffer
+                 BODY_SNAPPY = 1,     // snappy-decoded on the GPU into staging
+                 BODY_HOST = 2 };     // inflated on the host (gzip / user codec), uploaded into staging
+
+// Error "stages" in the reference's order of evaluation.  The reference reads
+// and initialises ALL pages of a chunk (phase 1, readPages chunk_reader.go:206)
+// before decoding any (phase 2, readPageData :380), so a page's status key is
+// (phase, page ordinal, stage); stages < STAGE_PHASE2 are phase 1.
+enum : uint32_t {
+  ST_HEADER = 1,      // host: nil/negative header fields, level encodings (page_v1.go:57-86)
+  ST_V2_ENC = 2,      // host: V2 value encoding (page_v2.go:95-98)
+  ST_V2_LEVELS = 3,   // host: V2 level bytes ReadFull (page_v2.go:103-108)
+  ST_V2_SIZE = 4,     // host: V2 negative data size (chunk_reader.go:199-201)
+  ST_DECOMPRESS = 5,  // device/host: newBlockReader (compress.go:102-122)
+  ST_V1_ENC = 6,      // host: V1 value encoding (page_v1.go:95-97); dict: encoding check
+  ST_REP_INIT = 7,    // device: V1 rep level length (hybrid_decoder.go:57-67)
+  ST_DEF_INIT = 8,
+  ST_VAL_INIT = 9,    // device: values init (type_dict.go:22-37, deltabp_decoder.go:197-246)
+  ST_DICT_VALUES = 9, // device: dictionary page PLAIN decode (page_dict.go:54-61)
+  ST_PHASE2 = 16,
+  ST_REP = 16,        // decodePackedArray(rDecoder) page_v1.go:37
+  ST_DEF = 17,
+  ST_VALUES = 18,     // valuesDecoder.decodeValues page_v1.go:48-52
+};
+__host__ __device__ inline uint32_t make_status(uint32_t stage, uint32_t code) { return (stage << 16) | code; }
+constexpr uint32_t STATUS_OK = 0xFFFFFFFFu;
+
+struct PageDesc {
+  uint64_t src;          // offset in the device input buffer of the page payload (after the header)
+  uint64_t body;         // offset of the values section: staging (SNAPPY/HOST) or input buffer (RAW)
+  int32_t comp_len;      // bytes fed to the codec (V2: compressed - level bytes)
+  int32_t body_len;      // expected uncompressed values-section length
+  int32_t num_values;    // header num_values (level entries); dictionary: entries
+  int32_t col;           // ColDesc index
+  int32_t dict;          // PageDesc index of this chunk's dictionary page, -1 if none
+  int32_t rg;            // row group
+  int32_t ord;           // page ordinal inside its chunk (error ordering)
+  uint8_t kind;          // PAGE_V1 / PAGE_V2 / PAGE_DICT
+  uint8_t enc;           // value encoding (PLAIN_DICT already mapped to RLE_DICT)
+  uint8_t body_src;      // BODY_*
+  uint8_t pad0;
+  int32_t v2_rep_len;    // V2: rep level bytes at src
+  int32_t v2_def_len;    // V2: def level bytes at src + v2_rep_len
+  int64_t level_base;    // first level entry of the page inside its column (flat slot base)
+  int64_t dict_base;     // BYTE_ARRAY dictionary page: first entry in the dict offsets scratch
+};
+
+struct ColDesc {
+  int32_t ptype, width;        // physical type, bytes per value (0 = BYTE_ARRAY)
+  int32_t max_def, max_rep, rep_def;
+  int32_t page_begin, page_end; // pages of this column in the table (all row groups)
+  int32_t flags;
+  // outputs (device pointers)
+  uint8_t *values;
+  uint32_t *validity;
+  int32_t *list_offsets;
+  uint32_t *list_validity;
+  int64_t *str_offsets;
+  uint8_t *def_out, *rep_out;
+  int64_t total_levels, total_slots, total_rows, total_str;
+};
+enum : int32_t { COL_NEEDS_COUNT = 1, COL_EMIT_LEVELS = 2 };
+
+// Written by the device.  Offsets are relative to the level source (V1: the
+// uncompressed body; V2: the payload) or to the body (values).
+struct PageInfo {
+  int32_t rep_off, rep_len;
+  int32_t def_off, def_len;
+  int32_t val_off, val_len;
+  int32_t idx_bw;
+  int32_t pad;
+  int64_t rows, slots, non_null, str_bytes;  // counts (prepare)
+  int64_t row_base, slot_base, str_base;     // exclusive scans over the column's pages
+};
+
+}  // namespace pq

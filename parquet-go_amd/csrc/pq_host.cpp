@@ -1,0 +1,1603 @@
+// pq_host.cpp — host side of libpqgpu.so: compact-Thrift footer and page-header
+// parsing, schema -> levels, the page walker that builds the batch descriptor
+// table, the codec registry, and the C ABI declared in include/pqgpu.h.
+//
+// Host work is limited to what the reference does before the per-value loops:
+// readFileMetaData (file_meta.go:14-62), makeSchema (schema.go:996),
+// readChunk/readPages page-header walk (chunk_reader.go:206-378).  Every byte
+// of page payload goes to HBM in one hipMemcpyAsync per batch; decompression
+// (Snappy) and all decoding run in pq_kernels.hip.
+#include <errno.h>
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/pqgpu.h"
+#include "pq_common.h"
+
+using namespace pq;
+
+extern "C" {
+struct pq_launch_args {
+  const uint8_t *in;
+  uint8_t *stage;
+  const void *pages;
+  void *info;
+  uint32_t *status;
+  void *cols;
+  uint64_t *dict_ent;
+  const int32_t *list;
+  int32_t nlist;
+  int32_t ncols;
+};
+int pq_launch(int which, const pq_launch_args *p, hipStream_t s);
+}
+
+namespace {
+
+thread_local std::string g_err;
+void set_err(const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+
+// ---------------------------------------------------------------------------
+// compact Thrift reader (read side only; unknown fields skipped)
+// ---------------------------------------------------------------------------
+struct TReader {
+  const uint8_t *p;
+  size_t n, pos = 0;
+  bool err = false;
+  int depth = 0;
+  TReader(const uint8_t *ptr, size_t len) : p(ptr), n(len) {}
+  uint8_t byte() {
+    if (pos >= n) {
+      err = true;
+      return 0;
+    }
+    return p[pos++];
+  }
+  uint64_t uvar() {
+    uint64_t x = 0;
+    for (int s = 0; s < 70; s += 7) {
+      uint8_t b = byte();
+      if (err) return 0;
+      x |= (uint64_t)(b & 0x7f) << s;
+      if (!(b & 0x80)) return x;
+    }
+    err = true;
+    return 0;
+  }
+  int64_t zz() {
+    uint64_t u = uvar();
+    return (int64_t)(u >> 1) ^ -(int64_t)(u & 1);
+  }
+  // returns field id (>0), 0 at stop/error; -1 for an explicit id of 0
+  int field(int16_t &last, int &type) {
+    uint8_t h = byte();
+    if (err || h == 0) return 0;
+    type = h & 0x0f;
+    int delta = h >> 4;
+    last = delta ? (int16_t)(last + delta) : (int16_t)zz();
+    return last == 0 ? -1 : last;
+  }
+  void list_header(int &etype, int64_t &size) {
+    uint8_t h = byte();
+    size = h >> 4;
+    etype = h & 0x0f;
+    if (size == 15) size = (int64_t)uvar();
+    if (size < 0 || (uint64_t)size > (n - pos) * 8 + 16) err = true;
+  }
+  void skip(int type) {
+    if (err) return;
+    switch (type) {
+      case 1: case 2: break;
+      case 3: byte(); break;
+      case 4: case 5: case 6: uvar(); break;
+      case 7:
+        if (n - pos < 8) err = true;
+        else pos += 8;
+        break;
+      case 8: {
+        uint64_t l = uvar();
+        if (err || l > n - pos) err = true;
+        else pos += l;
+        break;
+      }
+      case 9: case 10: {
+        int et;
+        int64_t sz;
+        list_header(et, sz);
+        for (int64_t i = 0; i < sz && !err; i++) {
+          if (et == 1 || et == 2) byte();
+          else skip(et);
+        }
+        break;
+      }
+      case 11: {
+        uint64_t sz = uvar();
+        if (sz == 0) break;
+        uint8_t kv = byte();
+        if (sz > n - pos) {
+          err = true;
+          break;
+        }
+        for (uint64_t i = 0; i < sz && !err; i++) {
+          skip(kv >> 4);
+          skip(kv & 15);
+        }
+        break;
+      }
+      case 12: {
+        if (++depth > 64) {
+          err = true;
+          break;
+        }
+        int16_t last = 0;
+        int t;
+        while (!err && field(last, t) != 0) skip(t);
+        depth--;
+        break;
+      }
+      default: err = true;
+    }
+  }
+  int32_t i32(int type) {
+    if (type == 3) return (int8_t)byte();
+    if (type != 4 && type != 5) {
+      skip(type);
+      err = true;
+      return 0;
+    }
+    return (int32_t)zz();
+  }
+  int64_t i64(int type) {
+    if (type != 4 && type != 5 && type != 6) {
+      skip(type);
+      err = true;
+      return 0;
+    }
+    return zz();
+  }
+  std::string str(int type) {
+    if (type != 8) {
+      skip(type);
+      err = true;
+      return {};
+    }
+    uint64_t l = uvar();
+    if (err || l > n - pos) {
+      err = true;
+      return {};
+    }
+    std::string s((const char *)p + pos, l);
+    pos += l;
+    return s;
+  }
+};
+
+struct SchemaElem {  // parquet/parquet.go:3381
+  bool has_type = false, has_rep = false, has_children = false, int_unsigned = false;
+  int32_t type = 0, type_length = 0, repetition = 0, num_children = 0, converted = -1;
+  std::string name;
+  bool has_name = false;
+};
+struct ColumnChunkMeta {  // parquet/parquet.go:8042 / :6822
+  bool has_meta = false, has_file_path = false, has_dict_off = false;
+  int32_t type = 0, codec = 0;
+  int64_t num_values = 0, total_uncompressed = 0, total_compressed = 0, data_page_offset = 0, dict_page_offset = 0;
+};
+struct RowGroupMeta {
+  std::vector<ColumnChunkMeta> cols;
+  int64_t num_rows = 0, total_byte_size = 0;
+};
+
+void read_int_type(TReader &t, bool &uns) {
+  int16_t last = 0;
+  int ty, f;
+  bool bw = false, sg = false, is_signed = true;
+  while ((f = t.field(last, ty)) != 0 && !t.err) {
+    if (f == 1 && ty == 3) {
+      t.byte();
+      bw = true;
+    } else if (f == 2 && (ty == 1 || ty == 2)) {
+      is_signed = ty == 1;
+      sg = true;
+    } else t.skip(ty);
+  }
+  if (!bw || !sg) t.err = true;
+  uns = !is_signed;
+}
+void read_schema_elem(TReader &t, SchemaElem &e) {
+  int16_t last = 0;
+  int ty, f;
+  while ((f = t.field(last, ty)) != 0 && !t.err) {
+    switch (f) {
+      case 1: e.type = t.i32(ty); e.has_type = true; break;
+      case 2: e.type_length = t.i32(ty); break;
+      case 3: e.repetition = t.i32(ty); e.has_rep = true; break;
+      case 4: e.name = t.str(ty); e.has_name = true; break;
+      case 5: e.num_children = t.i32(ty); e.has_children = true; break;
+      case 6: e.converted = t.i32(ty); break;
+      case 10:
+        if (ty == 12) {
+          int16_t l2 = 0;
+          int t2, f2;
+          while ((f2 = t.field(l2, t2)) != 0 && !t.err) {
+            if (f2 == 10 && t2 == 12) {
+              bool u = false;
+              read_int_type(t, u);
+              e.int_unsigned = u;
+            } else t.skip(t2);
+          }
+        } else t.skip(ty);
+        break;
+      default: t.skip(ty);
+    }
+  }
+  if (!e.has_name) t.err = true;
+}
+void read_col_meta(TReader &t, ColumnChunkMeta &c) {
+  int16_t last = 0;
+  int ty, f;
+  unsigned seen = 0;
+  while ((f = t.field(last, ty)) != 0 && !t.err) {
+    switch (f) {
+      case 1: c.type = t.i32(ty); seen |= 1; break;
+      case 2: t.skip(ty); seen |= 2; break;
+      case 3: t.skip(ty); seen |= 4; break;
+      case 4: c.codec = t.i32(ty); seen |= 8; break;
+      case 5: c.num_values = t.i64(ty); seen |= 16; break;
+      case 6: c.total_uncompressed = t.i64(ty); seen |= 32; break;
+      case 7: c.total_compressed = t.i64(ty); seen |= 64; break;
+      case 9: c.data_page_offset = t.i64(ty); seen |= 128; break;
+      case 11: c.dict_page_offset = t.i64(ty); c.has_dict_off = true; break;
+      default: t.skip(ty);
+    }
+  }
+  if (seen != 255) t.err = true;
+}
+void read_col_chunk(TReader &t, ColumnChunkMeta &c) {
+  int16_t last = 0;
+  int ty, f;
+  bool has_off = false;
+  while ((f = t.field(last, ty)) != 0 && !t.err) {
+    if (f == 1) {
+      t.str(ty);
+      c.has_file_path = true;
+    } else if (f == 2) {
+      t.i64(ty);
+      has_off = true;
+    } else if (f == 3 && ty == 12) {
+      read_col_meta(t, c);
+      c.has_meta = true;
+    } else t.skip(ty);
+  }
+  if (!has_off) t.err = true;
+}
+
+// PageHeader parquet/parquet.go:5794 (+ :3953, :4303, :4522)
+struct PageHeader {
+  int32_t type = 0, uncompressed = 0, compressed = 0;
+  bool has_dph = false, has_dict = false, has_v2 = false;
+  int32_t dp_num_values = 0, dp_encoding = 0, dp_def_enc = 0, dp_rep_enc = 0;
+  int32_t dict_num_values = 0, dict_encoding = 0;
+  int32_t v2_num_values = 0, v2_encoding = 0, v2_def_len = 0, v2_rep_len = 0;
+};
+void read_page_header(TReader &t, PageHeader &h) {
+  int16_t last = 0;
+  int ty, f;
+  unsigned seen = 0;
+  while ((f = t.field(last, ty)) != 0 && !t.err) {
+    if (f == 1) {
+      h.type = t.i32(ty);
+      seen |= 1;
+    } else if (f == 2) {
+      h.uncompressed = t.i32(ty);
+      seen |= 2;
+    } else if (f == 3) {
+      h.compressed = t.i32(ty);
+      seen |= 4;
+    } else if (f == 5 && ty == 12) {
+      int16_t l2 = 0;
+      int t2, f2;
+      unsigned s2 = 0;
+      while ((f2 = t.field(l2, t2)) != 0 && !t.err) {
+        switch (f2) {
+          case 1: h.dp_num_values = t.i32(t2); s2 |= 1; break;
+          case 2: h.dp_encoding = t.i32(t2); s2 |= 2; break;
+          case 3: h.dp_def_enc = t.i32(t2); s2 |= 4; break;
+          case 4: h.dp_rep_enc = t.i32(t2); s2 |= 8; break;
+          default: t.skip(t2);
+        }
+      }
+      if (s2 != 15) t.err = true;
+      h.has_dph = true;
+    } else if (f == 7 && ty == 12) {
+      int16_t l2 = 0;
+      int t2, f2;
+      unsigned s2 = 0;
+      while ((f2 = t.field(l2, t2)) != 0 && !t.err) {
+        switch (f2) {
+          case 1: h.dict_num_values = t.i32(t2); s2 |= 1; break;
+          case 2: h.dict_encoding = t.i32(t2); s2 |= 2; break;
+          default: t.skip(t2);
+        }
+      }
+      if (s2 != 3) t.err = true;
+      h.has_dict = true;
+    } else if (f == 8 && ty == 12) {
+      int16_t l2 = 0;
+      int t2, f2;
+      unsigned s2 = 0;
+      while ((f2 = t.field(l2, t2)) != 0 && !t.err) {
+        switch (f2) {
+          case 1: h.v2_num_values = t.i32(t2); s2 |= 1; break;
+          case 2: t.i32(t2); s2 |= 2; break;
+          case 3: t.i32(t2); s2 |= 4; break;
+          case 4: h.v2_encoding = t.i32(t2); s2 |= 8; break;
+          case 5: h.v2_def_len = t.i32(t2); s2 |= 16; break;
+          case 6: h.v2_rep_len = t.i32(t2); s2 |= 32; break;
+          default: t.skip(t2);
+        }
+      }
+      if (s2 != 63) t.err = true;
+      h.has_v2 = true;
+    } else t.skip(ty);
+  }
+  if (seen != 7) t.err = true;
+}
+
+int value_width(int ptype, int type_length) {
+  switch (ptype) {
+    case T_INT32: case T_FLOAT: return 4;
+    case T_INT64: case T_DOUBLE: return 8;
+    case T_INT96: return 12;
+    case T_FLBA: return type_length;
+    default: return 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// codec registry (compress.go:16-27, :130-156)
+// ---------------------------------------------------------------------------
+struct Codec {
+  pqg_decompress_fn fn = nullptr;  // nullptr: built-in
+  void *user = nullptr;
+};
+std::shared_mutex g_codec_mu;
+std::map<int, Codec> &codecs() {
+  static std::map<int, Codec> m = {{PQG_CODEC_UNCOMPRESSED, {}}, {PQG_CODEC_SNAPPY, {}}, {PQG_CODEC_GZIP, {}}};
+  return m;
+}
+
+int gzip_inflate(const uint8_t *src, size_t n, uint8_t *dst, size_t cap, size_t *out_len) {
+  z_stream zs;
+  memset(&zs, 0, sizeof(zs));
+  if (inflateInit2(&zs, 16 + MAX_WBITS) != Z_OK) return PQG_ERR_CODEC;
+  zs.next_in = (Bytef *)src;
+  zs.avail_in = (uInt)n;
+  zs.next_out = dst;
+  zs.avail_out = (uInt)cap;
+  int rc = inflate(&zs, Z_FINISH);
+  *out_len = cap - zs.avail_out;
+  inflateEnd(&zs);
+  if (rc == Z_STREAM_END) return PQG_OK;
+  return rc == Z_BUF_ERROR ? PQG_ERR_SIZE : PQG_ERR_CODEC;
+}
+
+// Host decompression for pages whose codec is not run on the GPU.  Returns
+// 0, or a status; the size check of newBlockReader is done by the caller.
+int host_decompress(int codec, const uint8_t *src, size_t n, uint8_t *dst, size_t cap, size_t *out_len,
+                    bool *on_device) {
+  std::shared_lock<std::shared_mutex> lk(g_codec_mu);  // held during the call, like compress.go:91-92
+  auto it = codecs().find(codec);
+  if (it == codecs().end()) return PQG_ERR_CODEC;
+  if (it->second.fn) {
+    *on_device = false;
+    return it->second.fn(it->second.user, src, n, dst, cap, out_len);
+  }
+  switch (codec) {
+    case PQG_CODEC_UNCOMPRESSED:
+      *on_device = false;
+      if (n > cap) return PQG_ERR_SIZE;
+      memcpy(dst, src, n);
+      *out_len = n;
+      return PQG_OK;
+    case PQG_CODEC_SNAPPY:
+      *on_device = true;
+      return PQG_OK;
+    case PQG_CODEC_GZIP:
+      *on_device = false;
+      return gzip_inflate(src, n, dst, cap, out_len);
+  }
+  return PQG_ERR_CODEC;
+}
+bool codec_builtin(int codec, bool *registered) {
+  std::shared_lock<std::shared_mutex> lk(g_codec_mu);
+  auto it = codecs().find(codec);
+  *registered = it != codecs().end();
+  return *registered && it->second.fn == nullptr;
+}
+
+}  // namespace
+
+// ===========================================================================
+// objects
+// ===========================================================================
+struct pqg_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+};
+
+struct pqg_file {
+  const uint8_t *data = nullptr;
+  size_t len = 0;
+  bool owned = false, mapped = false;
+  std::vector<SchemaElem> schema;
+  std::vector<RowGroupMeta> rgs;
+  std::vector<pqg_column_info> leaves;
+  int64_t num_rows = 0;
+  std::string err;
+  ~pqg_file() {
+    if (mapped) munmap((void *)data, len);
+    else if (owned) free((void *)data);
+  }
+};
+
+struct ChunkError {  // a host-detected error that ends a chunk's page walk
+  int rg, leaf, ord;
+  uint32_t stage, code;
+};
+
+struct ColumnPlan {
+  int leaf;
+  pqg_column_info info;
+  int flags;
+  int32_t page_begin, page_end;
+  int64_t levels;
+  // device outputs
+  void *values = nullptr, *validity = nullptr, *list_offsets = nullptr, *list_validity = nullptr,
+       *str_offsets = nullptr, *def_out = nullptr, *rep_out = nullptr;
+  size_t values_bytes = 0, validity_bytes = 0, list_off_bytes = 0, list_val_bytes = 0, str_off_bytes = 0;
+  int64_t slots = 0, rows = 0, str_bytes = 0;
+};
+
+struct pqg_batch {
+  pqg_ctx *ctx = nullptr;
+  pqg_file *file = nullptr;
+  int rg_begin = 0, rg_end = 0, flags = 0;
+  std::vector<ColumnPlan> cols;
+  std::vector<PageDesc> pages;
+  std::vector<uint32_t> status0;  // host-side initial status per page
+  std::vector<int32_t> snappy_list, dict_list, data_list;
+  std::vector<ChunkError> chunk_errors;
+  int64_t input_bytes = 0, staged_bytes = 0, h2d_bytes = 0, host_inflated = 0, dict_entries = 0;
+  // device
+  uint8_t *d_in = nullptr, *d_stage = nullptr;
+  PageDesc *d_pages = nullptr;
+  PageInfo *d_info = nullptr;
+  uint32_t *d_status = nullptr;
+  ColDesc *d_cols = nullptr;
+  uint64_t *d_dict = nullptr;
+  int32_t *d_lists = nullptr;
+  uint32_t *h_status = nullptr;  // pinned mirror
+  std::vector<ColDesc> hcols;
+  // timing
+  hipEvent_t ev[8] = {};
+  int nev = 0;
+  float kms[8] = {};
+  int err_rg = -1, err_leaf = -1, err_page = -1;
+  bool decoded = false;
+};
+
+static const char *kKernelNames[] = {"k_snappy", "k_dict_prepare", "k_prepare", "k_scan", "k_decode",
+                                     "k_level_check"};
+
+#define HIPCHK(x)                                                                 \
+  do {                                                                            \
+    hipError_t _e = (x);                                                          \
+    if (_e != hipSuccess) {                                                       \
+      set_err("HIP error %s at %s:%d", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return PQG_ERR_DEVICE;                                                      \
+    }                                                                             \
+  } while (0)
+
+extern "C" {
+
+int pqg_abi_version(void) { return PQGPU_ABI_VERSION; }
+
+int pqg_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int pqg_last_error(pqg_ctx *ctx, char *buf, size_t cap) {
+  (void)ctx;
+  if (buf && cap) snprintf(buf, cap, "%s", g_err.c_str());
+  return (int)g_err.size();
+}
+
+int pqg_ctx_create(int device, pqg_ctx **out) {
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+    set_err("no HIP device available");
+    return PQG_ERR_DEVICE;
+  }
+  if (device < 0 || device >= n) {
+    set_err("device %d out of range (%d devices)", device, n);
+    return PQG_ERR_ARG;
+  }
+  HIPCHK(hipSetDevice(device));
+  pqg_ctx *c = new pqg_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    set_err("hipStreamCreate failed");
+    return PQG_ERR_DEVICE;
+  }
+  *out = c;
+  return PQG_OK;
+}
+
+void pqg_ctx_destroy(pqg_ctx *ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+void *pqg_ctx_stream(pqg_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+// ---------------------------------------------------------------------------
+// codec registry API
+// ---------------------------------------------------------------------------
+int pqg_register_block_compressor(int codec, pqg_decompress_fn fn, void *user) {
+  if (codec < 0) {
+    set_err("invalid codec %d", codec);
+    return PQG_ERR_ARG;
+  }
+  std::unique_lock<std::shared_mutex> lk(g_codec_mu);
+  if (!fn && codec > PQG_CODEC_GZIP) {
+    codecs().erase(codec);
+    return PQG_OK;
+  }
+  codecs()[codec] = Codec{fn, user};
+  return PQG_OK;
+}
+
+int pqg_get_registered_codecs(int *out, int cap) {
+  std::unique_lock<std::shared_mutex> lk(g_codec_mu);  // compress.go:142 takes the write lock too
+  int i = 0;
+  for (auto &kv : codecs()) {
+    if (i < cap && out) out[i] = kv.first;
+    i++;
+  }
+  return i;
+}
+
+// forward
+static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8_t *dst, size_t expect, int *code);
+
+int pqg_decompress_block(pqg_ctx *ctx, int codec, const uint8_t *src, size_t src_len, uint8_t *dst, size_t dst_cap,
+                         size_t expect_len, size_t *out_len) {
+  if (!src && src_len) return PQG_ERR_ARG;
+  bool on_device = false;
+  size_t got = 0;
+  std::vector<uint8_t> tmp;
+  uint8_t *target = dst;
+  size_t cap = dst_cap;
+  if (dst_cap < expect_len) {
+    tmp.resize(expect_len + 1);
+    target = tmp.data();
+    cap = expect_len;
+  }
+  int rc = host_decompress(codec, src, src_len, target, cap, &got, &on_device);
+  if (rc) {
+    set_err("decompression failed (codec %d): status %d", codec, rc);
+    return rc;
+  }
+  if (on_device) {
+    if (!ctx) {
+      set_err("SNAPPY decompression needs a GPU context");
+      return PQG_ERR_ARG;
+    }
+    int code = 0;
+    rc = device_snappy_block(ctx, src, src_len, target, expect_len, &code);
+    if (rc) return rc;
+    if (code) {
+      set_err("snappy: %s", code == PQG_ERR_SIZE ? "decompressed size mismatch" : "corrupt input");
+      return code;
+    }
+    got = expect_len;
+  }
+  if (got != expect_len) {  // compress.go:117-119
+    set_err("decompressed data must be %zu byte but its %zu byte", expect_len, got);
+    return PQG_ERR_SIZE;
+  }
+  if (target != dst) {
+    set_err("destination too small");
+    return PQG_ERR_ARG;
+  }
+  if (out_len) *out_len = got;
+  return PQG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// file
+// ---------------------------------------------------------------------------
+static int walk_schema(pqg_file *f, size_t &idx, const std::string &prefix, int d, int r, int rep_def, int depth) {
+  if (depth > 64 || idx >= f->schema.size()) return PQG_ERR_SCHEMA;
+  const SchemaElem &e = f->schema[idx];
+  if (e.name.empty() || !e.has_rep) return PQG_ERR_SCHEMA;  // schema.go:792-798
+  if (e.repetition != 0) d++;                               // :800-802
+  if (e.repetition == 2) {                                  // :804-806
+    r++;
+    rep_def = d;
+  }
+  std::string name = prefix.empty() ? e.name : prefix + "." + e.name;
+  idx++;
+  if (!e.has_children || e.num_children == 0) {
+    if (!e.has_type) return PQG_ERR_SCHEMA;
+    pqg_column_info L;
+    memset(&L, 0, sizeof(L));
+    snprintf(L.name, sizeof(L.name), "%s", name.c_str());
+    L.physical_type = e.type;
+    L.type_length = e.type_length;
+    L.max_def = d;
+    L.max_rep = r;
+    L.rep_def = rep_def;
+    L.converted_type = e.converted;
+    int uns = 0;
+    if (e.type == T_INT32 && (e.converted == 11 || e.converted == 12 || e.converted == 13)) uns = 1;
+    if (e.type == T_INT64 && e.converted == 14) uns = 1;
+    if (e.int_unsigned) uns = 1;
+    L.unsigned_int = uns;
+    L.value_width = value_width(e.type, e.type_length);
+    f->leaves.push_back(L);
+    return 0;
+  }
+  for (int c = 0; c < e.num_children; c++) {
+    int rc = walk_schema(f, idx, name, d, r, rep_def, depth + 1);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+static int parse_file(pqg_file *f) {
+  const uint8_t *b = f->data;
+  size_t len = f->len;
+  if (len < 12 || memcmp(b, "PAR1", 4) != 0) {
+    set_err("invalid parquet file header");
+    return PQG_ERR_FORMAT;
+  }
+  if (memcmp(b + len - 4, "PAR1", 4) != 0) {
+    set_err("invalid parquet file footer");
+    return PQG_ERR_FORMAT;
+  }
+  int32_t fl;
+  memcpy(&fl, b + len - 8, 4);
+  if (fl <= 0 || (size_t)fl > len - 8) {
+    set_err("invalid footer len %d", fl);
+    return PQG_ERR_FORMAT;
+  }
+  TReader t(b + len - 8 - fl, (size_t)fl);
+  int16_t last = 0;
+  int ty, fid;
+  unsigned seen = 0;
+  while ((fid = t.field(last, ty)) != 0 && !t.err) {  // FileMetaData parquet.go:10564
+    if (fid == 1) {
+      t.i32(ty);
+      seen |= 1;
+    } else if (fid == 2 && ty == 9) {
+      int et;
+      int64_t sz;
+      t.list_header(et, sz);
+      if (t.err || et != 12) {
+        t.err = true;
+        break;
+      }
+      f->schema.resize((size_t)sz);
+      for (int64_t i = 0; i < sz && !t.err; i++) read_schema_elem(t, f->schema[(size_t)i]);
+      seen |= 2;
+    } else if (fid == 3) {
+      f->num_rows = t.i64(ty);
+      seen |= 4;
+    } else if (fid == 4 && ty == 9) {
+      int et;
+      int64_t sz;
+      t.list_header(et, sz);
+      if (t.err || et != 12) {
+        t.err = true;
+        break;
+      }
+      f->rgs.resize((size_t)sz);
+      for (int64_t i = 0; i < sz && !t.err; i++) {  // RowGroup parquet.go:8561
+        RowGroupMeta &g = f->rgs[(size_t)i];
+        int16_t l2 = 0;
+        int t2, f2;
+        unsigned s2 = 0;
+        while ((f2 = t.field(l2, t2)) != 0 && !t.err) {
+          if (f2 == 1 && t2 == 9) {
+            int e2;
+            int64_t n2;
+            t.list_header(e2, n2);
+            if (t.err || e2 != 12) {
+              t.err = true;
+              break;
+            }
+            g.cols.resize((size_t)n2);
+            for (int64_t j = 0; j < n2 && !t.err; j++) read_col_chunk(t, g.cols[(size_t)j]);
+            s2 |= 1;
+          } else if (f2 == 2) {
+            g.total_byte_size = t.i64(t2);
+            s2 |= 2;
+          } else if (f2 == 3) {
+            g.num_rows = t.i64(t2);
+            s2 |= 4;
+          } else t.skip(t2);
+        }
+        if (s2 != 7) t.err = true;
+      }
+      seen |= 8;
+    } else t.skip(ty);
+  }
+  if (t.err || seen != 15) {
+    set_err("read file meta failed");
+    return PQG_ERR_THRIFT;
+  }
+  if (f->schema.empty()) {
+    set_err("empty schema");
+    return PQG_ERR_SCHEMA;
+  }
+  size_t idx = 1;
+  for (int c = 0; c < f->schema[0].num_children; c++) {
+    int rc = walk_schema(f, idx, "", 0, 0, 0, 0);
+    if (rc) {
+      set_err("invalid schema");
+      return rc;
+    }
+  }
+  return PQG_OK;
+}
+
+int pqg_file_open_buffer(const uint8_t *data, size_t len, int copy, pqg_file **out) {
+  *out = nullptr;
+  if (!data) {
+    set_err("null buffer");
+    return PQG_ERR_ARG;
+  }
+  pqg_file *f = new pqg_file();
+  if (copy) {
+    uint8_t *p = (uint8_t *)malloc(len ? len : 1);
+    memcpy(p, data, len);
+    f->data = p;
+    f->owned = true;
+  } else {
+    f->data = data;
+  }
+  f->len = len;
+  int rc = parse_file(f);
+  if (rc) {
+    delete f;
+    return rc;
+  }
+  *out = f;
+  return PQG_OK;
+}
+
+int pqg_file_open_path(const char *path, pqg_file **out) {
+  *out = nullptr;
+  int fd = open(path, O_RDONLY);
+  if (fd < 0) {
+    set_err("open %s: %s", path, strerror(errno));
+    return PQG_ERR_FORMAT;
+  }
+  struct stat st;
+  if (fstat(fd, &st) != 0 || st.st_size < 12) {
+    close(fd);
+    set_err("invalid parquet file header");
+    return PQG_ERR_FORMAT;
+  }
+  void *m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+  close(fd);
+  if (m == MAP_FAILED) {
+    set_err("mmap failed");
+    return PQG_ERR_FORMAT;
+  }
+  pqg_file *f = new pqg_file();
+  f->data = (const uint8_t *)m;
+  f->len = (size_t)st.st_size;
+  f->mapped = true;
+  int rc = parse_file(f);
+  if (rc) {
+    delete f;
+    return rc;
+  }
+  *out = f;
+  return PQG_OK;
+}
+
+void pqg_file_close(pqg_file *f) { delete f; }
+int64_t pqg_file_num_rows(const pqg_file *f) { return f->num_rows; }
+int pqg_file_row_group_count(const pqg_file *f) { return (int)f->rgs.size(); }
+int64_t pqg_file_row_group_num_rows(const pqg_file *f, int rg) {
+  return rg >= 0 && rg < (int)f->rgs.size() ? f->rgs[(size_t)rg].num_rows : -1;
+}
+int64_t pqg_file_row_group_byte_size(const pqg_file *f, int rg) {
+  if (rg < 0 || rg >= (int)f->rgs.size()) return -1;
+  int64_t s = 0;
+  for (auto &c : f->rgs[(size_t)rg].cols) s += c.total_uncompressed;
+  return s;
+}
+int pqg_file_column_count(const pqg_file *f) { return (int)f->leaves.size(); }
+int pqg_file_column_info(const pqg_file *f, int leaf, pqg_column_info *out) {
+  if (leaf < 0 || leaf >= (int)f->leaves.size()) return PQG_ERR_ARG;
+  *out = f->leaves[(size_t)leaf];
+  return PQG_OK;
+}
+int pqg_file_find_column(const pqg_file *f, const char *name) {
+  for (size_t i = 0; i < f->leaves.size(); i++)
+    if (strcmp(f->leaves[i].name, name) == 0) return (int)i;
+  return -1;
+}
+int pqg_file_select_columns(const pqg_file *f, const char *const *names, int nnames, int *out, int cap) {
+  int k = 0;
+  for (size_t i = 0; i < f->leaves.size(); i++) {
+    bool sel = nnames == 0;
+    for (int j = 0; j < nnames && !sel; j++) {  // schema.go:296-312
+      size_t l = strlen(names[j]);
+      const char *nm = f->leaves[i].name;
+      if (strcmp(nm, names[j]) == 0 || (strncmp(nm, names[j], l) == 0 && nm[l] == '.')) sel = true;
+    }
+    if (sel) {
+      if (k < cap) out[k] = (int)i;
+      k++;
+    }
+  }
+  return k;
+}
+int pqg_file_last_error(const pqg_file *f, char *buf, size_t cap) {
+  (void)f;
+  if (buf && cap) snprintf(buf, cap, "%s", g_err.c_str());
+  return (int)g_err.size();
+}
+
+// ---------------------------------------------------------------------------
+// batch planning
+// ---------------------------------------------------------------------------
+static int supported_encoding(int ptype, int enc) {
+  if (enc == ENC_PLAIN_DICT) enc = ENC_RLE_DICT;  // chunk_reader.go:145-147
+  switch (ptype) {
+    case T_BYTE_ARRAY:
+      if (enc == ENC_PLAIN || enc == ENC_RLE_DICT) return 0;
+      return enc == ENC_DELTA_LBA || enc == ENC_DELTA_BA ? PQG_ERR_UNSUPPORTED : PQG_ERR_ENCODING;
+    case T_FLBA:
+      if (enc == ENC_PLAIN || enc == ENC_RLE_DICT) return 0;
+      return enc == ENC_DELTA_BA ? PQG_ERR_UNSUPPORTED : PQG_ERR_ENCODING;
+    case T_FLOAT: case T_DOUBLE: case T_INT96:
+      return enc == ENC_PLAIN || enc == ENC_RLE_DICT ? 0 : PQG_ERR_ENCODING;
+    case T_INT32: case T_INT64:
+      return enc == ENC_PLAIN || enc == ENC_RLE_DICT || enc == ENC_DELTA_BP ? 0 : PQG_ERR_ENCODING;
+    case T_BOOLEAN:
+      return enc == ENC_PLAIN || enc == ENC_RLE || enc == ENC_RLE_DICT ? PQG_ERR_UNSUPPORTED : PQG_ERR_ENCODING;
+  }
+  return PQG_ERR_ENCODING;
+}
+
+namespace {
+struct HostBuf {  // growable host staging for the input upload / host-inflated bodies
+  std::vector<uint8_t> v;
+  size_t append(const uint8_t *p, size_t n, size_t align = 16) {
+    size_t off = (v.size() + align - 1) & ~(align - 1);
+    v.resize(off + n);
+    if (n) memcpy(v.data() + off, p, n);
+    return off;
+  }
+};
+constexpr size_t kPad = 1024;  // readable slack after every device buffer
+}  // namespace
+
+static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t, std::vector<uint8_t>>> &host_bodies,
+                      int64_t &stage_off, int ci, int rg) {
+  pqg_file *f = B->file;
+  ColumnPlan &cp = B->cols[(size_t)ci];
+  const pqg_column_info &L = cp.info;
+  const RowGroupMeta &G = f->rgs[(size_t)rg];
+  auto chunk_err = [&](int ord, uint32_t stage, int code, const char *msg) {
+    B->chunk_errors.push_back({rg, cp.leaf, ord, stage, (uint32_t)code});
+    (void)msg;
+    return 0;
+  };
+  if (cp.leaf >= (int)G.cols.size()) return chunk_err(-1, 0, PQG_ERR_PAGE, "column index out of bounds");
+  const ColumnChunkMeta &C = G.cols[(size_t)cp.leaf];
+  if (C.has_file_path) return chunk_err(-1, 0, PQG_ERR_PAGE, "nyi: data is in another file");
+  if (!C.has_meta) return chunk_err(-1, 0, PQG_ERR_PAGE, "missing meta data");
+  if (C.type != L.physical_type) return chunk_err(-1, 0, PQG_ERR_PAGE, "wrong type in chunk metadata");
+  int64_t offset = C.has_dict_off ? C.dict_page_offset : C.data_page_offset;
+  if (offset < 0 || (uint64_t)offset > f->len) return chunk_err(-1, 0, PQG_ERR_SIZE, "seek");
+
+  bool registered = false;
+  bool builtin = codec_builtin(C.codec, &registered);
+  const bool device_codec = builtin && C.codec == PQG_CODEC_SNAPPY;
+
+  // walk page headers exactly like readPages (chunk_reader.go:206-284)
+  struct Walked {
+    PageHeader h;
+    int64_t payload;  // file offset of the payload
+    int ord;
+  };
+  std::vector<Walked> walked;
+  int64_t pos = offset, count = 0;
+  int ord = 0;
+  bool have_dict = false;
+  int64_t chunk_lo = offset, chunk_hi = offset;
+  while (C.total_compressed - count > 0) {
+    if ((uint64_t)pos >= f->len) return chunk_err(ord, 0, PQG_ERR_THRIFT, "page header past end of file");
+    TReader t(f->data + pos, f->len - (size_t)pos);
+    PageHeader h;
+    read_page_header(t, h);
+    if (t.err) {
+      chunk_err(ord, 0, PQG_ERR_THRIFT, "page header");
+      break;
+    }
+    pos += (int64_t)t.pos;
+    count += (int64_t)t.pos;
+    Walked w{h, pos, ord};
+    if (h.type == 2) {  // DICTIONARY_PAGE
+      if (have_dict) {
+        chunk_err(ord, 0, PQG_ERR_PAGE, "there should be only one dictionary");
+        break;
+      }
+      have_dict = true;
+      walked.push_back(w);
+      int64_t csz = h.compressed > 0 ? h.compressed : 0;
+      chunk_hi = std::max(chunk_hi, std::min<int64_t>(pos + csz, (int64_t)f->len));
+      pos += csz;
+      count += csz;
+      if (h.compressed < 0) break;  // page errors at its own stage; the walk cannot continue
+      if (C.has_dict_off && C.dict_page_offset != pos) {  // :243-249
+        count += C.data_page_offset - pos;
+        pos = C.data_page_offset;
+        if (pos < 0 || (uint64_t)pos > f->len) {
+          chunk_err(ord + 1, 0, PQG_ERR_SIZE, "seek");
+          break;
+        }
+        chunk_lo = std::min(chunk_lo, pos);
+      }
+      ord++;
+      continue;
+    }
+    if (h.type != 0 && h.type != 3) {
+      chunk_err(ord, 0, PQG_ERR_PAGE, "DATA_PAGE or DATA_PAGE_V2 type supported");
+      break;
+    }
+    walked.push_back(w);
+    if (h.compressed < 0) break;
+    chunk_hi = std::max(chunk_hi, std::min<int64_t>(pos + h.compressed, (int64_t)f->len));
+    pos += h.compressed;
+    count += h.compressed;
+    ord++;
+  }
+  // upload the chunk bytes once
+  size_t base = in.append(f->data + chunk_lo, (size_t)(chunk_hi - chunk_lo));
+  B->input_bytes += chunk_hi - chunk_lo;
+
+  int32_t dict_idx = -1;
+  int64_t level_base = cp.levels;
+  for (auto &w : walked) {
+    const PageHeader &h = w.h;
+    PageDesc d;
+    memset(&d, 0, sizeof(d));
+    d.col = ci;
+    d.rg = rg;
+    d.ord = w.ord;
+    d.dict = dict_idx;
+    d.src = base + (uint64_t)(w.payload - chunk_lo);
+    uint32_t st = STATUS_OK;
+    auto fail = [&](uint32_t stage, int code) {
+      if (st == STATUS_OK) st = make_status(stage, (uint32_t)code);
+    };
+    const int64_t avail = (int64_t)f->len - w.payload;
+    bool needs_device_codec = false;
+    int64_t comp = 0, body = 0, lsize = 0;
+    if (h.type == 2) {
+      d.kind = PAGE_DICT;
+      d.num_values = h.dict_num_values;
+      if (!h.has_dict || h.dict_num_values < 0) fail(ST_HEADER, PQG_ERR_PAGE);
+      if (L.physical_type == T_FLBA && L.type_length <= 0) fail(ST_HEADER, PQG_ERR_SCHEMA);
+      if (L.physical_type == T_BOOLEAN) fail(ST_HEADER, PQG_ERR_UNSUPPORTED);
+      if (h.dict_encoding != ENC_PLAIN && h.dict_encoding != ENC_PLAIN_DICT) fail(ST_V2_ENC, PQG_ERR_ENCODING);
+      comp = h.compressed;
+      body = h.uncompressed;
+      d.dict_base = B->dict_entries;
+      if (L.physical_type == T_BYTE_ARRAY && h.dict_num_values > 0) B->dict_entries += h.dict_num_values;
+    } else if (h.type == 0) {
+      d.kind = PAGE_V1;
+      d.num_values = h.dp_num_values;
+      if (!h.has_dph) fail(ST_HEADER, PQG_ERR_PAGE);
+      if (L.max_rep > 0 && h.dp_rep_enc != ENC_RLE) fail(ST_HEADER, PQG_ERR_ENCODING);
+      if (L.max_def > 0 && h.dp_def_enc != ENC_RLE) fail(ST_HEADER, PQG_ERR_ENCODING);
+      if (h.dp_num_values < 0) fail(ST_HEADER, PQG_ERR_PAGE);
+      int e = supported_encoding(L.physical_type, h.dp_encoding);
+      if (e) fail(ST_V1_ENC, e);
+      d.enc = (uint8_t)(h.dp_encoding == ENC_PLAIN_DICT ? ENC_RLE_DICT : h.dp_encoding);
+      comp = h.compressed;
+      body = h.uncompressed;
+    } else {
+      d.kind = PAGE_V2;
+      d.num_values = h.v2_num_values;
+      if (!h.has_v2 || h.v2_num_values < 0 || h.v2_rep_len < 0 || h.v2_def_len < 0) fail(ST_HEADER, PQG_ERR_PAGE);
+      int e = supported_encoding(L.physical_type, h.v2_encoding);
+      if (e) fail(ST_V2_ENC, e);
+      d.enc = (uint8_t)(h.v2_encoding == ENC_PLAIN_DICT ? ENC_RLE_DICT : h.v2_encoding);
+      lsize = (int64_t)std::max(h.v2_rep_len, 0) + std::max(h.v2_def_len, 0);
+      if (lsize > 0 && lsize > avail) fail(ST_V2_LEVELS, PQG_ERR_EOF);
+      d.v2_rep_len = h.v2_rep_len;
+      d.v2_def_len = h.v2_def_len;
+      comp = (int64_t)h.compressed - lsize;
+      body = (int64_t)h.uncompressed - lsize;
+      if (comp < 0 || body < 0) fail(ST_V2_SIZE, PQG_ERR_SIZE);
+    }
+    if (d.num_values < 0) d.num_values = 0;
+    d.comp_len = (int32_t)std::max<int64_t>(comp, 0);
+    d.body_len = (int32_t)std::max<int64_t>(body, 0);
+    d.level_base = level_base;
+    // decompression stage (newBlockReader compress.go:102-122)
+    if (st == STATUS_OK || (st >> 16) > ST_DECOMPRESS) {
+      if (comp < 0 || body < 0) {
+        fail(ST_DECOMPRESS, PQG_ERR_SIZE);
+      } else if (comp > avail - lsize) {
+        fail(ST_DECOMPRESS, PQG_ERR_SIZE);  // short read
+      } else if (!registered) {
+        fail(ST_DECOMPRESS, PQG_ERR_CODEC);
+      } else if (device_codec) {
+        needs_device_codec = true;
+      } else if (builtin && C.codec == PQG_CODEC_UNCOMPRESSED) {
+        if (comp != body) fail(ST_DECOMPRESS, PQG_ERR_SIZE);
+      } else {
+        // host codec (gzip / user-registered): inflate now, upload into staging
+        std::vector<uint8_t> out((size_t)body + 1);
+        size_t got = 0;
+        bool ondev = false;
+        int rc = host_decompress(C.codec, f->data + w.payload + lsize, (size_t)comp, out.data(), (size_t)body, &got,
+                                 &ondev);
+        if (rc) fail(ST_DECOMPRESS, rc);
+        else if (got != (size_t)body) fail(ST_DECOMPRESS, PQG_ERR_SIZE);
+        else {
+          out.resize((size_t)body);
+          d.body_src = BODY_HOST;
+          d.body = (uint64_t)stage_off;
+          host_bodies.emplace_back((uint64_t)stage_off, std::move(out));
+          stage_off += ((body + 15) & ~15) + 16;
+          B->host_inflated++;
+        }
+      }
+    }
+    if (needs_device_codec) {
+      d.body_src = BODY_SNAPPY;
+      d.body = (uint64_t)stage_off;
+      stage_off += ((body + 15) & ~15) + 16;
+      B->staged_bytes += body;
+    } else if (d.body_src == BODY_RAW) {
+      d.body = d.src + (uint64_t)lsize;
+    }
+    int32_t my_index = (int32_t)B->pages.size();
+    B->pages.push_back(d);
+    B->status0.push_back(st);
+    if (d.kind == PAGE_DICT) {
+      dict_idx = my_index;
+      B->dict_list.push_back(my_index);
+    } else {
+      B->data_list.push_back(my_index);
+      level_base += d.num_values;
+    }
+    if (needs_device_codec) B->snappy_list.push_back(my_index);
+  }
+  cp.levels = level_base;
+  return 0;
+}
+
+static int alloc_dev(void **p, size_t n) {
+  hipError_t e = hipMalloc(p, n + kPad);
+  if (e != hipSuccess) {
+    set_err("hipMalloc(%zu) failed: %s", n, hipGetErrorString(e));
+    return PQG_ERR_DEVICE;
+  }
+  return 0;
+}
+
+static int launch_all(pqg_batch *B, bool upto_scan, bool timed);
+
+int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const int *leaves, int nleaves, int flags,
+                     pqg_batch **out) {
+  *out = nullptr;
+  if (!ctx || !f || rg_begin < 0 || rg_end > (int)f->rgs.size() || rg_begin > rg_end || nleaves < 0) {
+    set_err("bad batch arguments");
+    return PQG_ERR_ARG;
+  }
+  HIPCHK(hipSetDevice(ctx->device));
+  pqg_batch *B = new pqg_batch();
+  B->ctx = ctx;
+  B->file = f;
+  B->rg_begin = rg_begin;
+  B->rg_end = rg_end;
+  B->flags = flags;
+  std::vector<int> sel;
+  if (nleaves == 0 || !leaves) {
+    for (int i = 0; i < (int)f->leaves.size(); i++) sel.push_back(i);
+  } else {
+    sel.assign(leaves, leaves + nleaves);
+  }
+  for (int l : sel) {
+    if (l < 0 || l >= (int)f->leaves.size()) {
+      delete B;
+      set_err("leaf %d out of range", l);
+      return PQG_ERR_ARG;
+    }
+    ColumnPlan cp;
+    cp.leaf = l;
+    cp.info = f->leaves[(size_t)l];
+    cp.flags = 0;
+    if (cp.info.max_rep > 0 || cp.info.physical_type == T_BYTE_ARRAY) cp.flags |= COL_NEEDS_COUNT;
+    if (flags & PQG_BATCH_LEVELS) cp.flags |= COL_EMIT_LEVELS;
+    cp.levels = 0;
+    B->cols.push_back(cp);
+  }
+  HostBuf in;
+  std::vector<std::pair<uint64_t, std::vector<uint8_t>>> host_bodies;
+  int64_t stage_off = 0;
+  for (size_t ci = 0; ci < B->cols.size(); ci++) {
+    B->cols[ci].page_begin = (int32_t)B->pages.size();
+    if (B->cols[ci].info.max_rep > 1) {
+      // deeper nesting: levels and dense values only are outside this build's layout
+      B->chunk_errors.push_back({rg_begin, B->cols[ci].leaf, -1, 0, PQG_ERR_UNSUPPORTED});
+    }
+    for (int rg = rg_begin; rg < rg_end; rg++) plan_chunk(B, in, host_bodies, stage_off, (int)ci, rg);
+    B->cols[ci].page_end = (int32_t)B->pages.size();
+  }
+  const size_t npages = B->pages.size();
+
+  // device buffers
+  int rc = 0;
+  size_t in_bytes = in.v.size();
+  rc |= alloc_dev((void **)&B->d_in, in_bytes);
+  rc |= alloc_dev((void **)&B->d_stage, (size_t)stage_off);
+  rc |= alloc_dev((void **)&B->d_pages, sizeof(PageDesc) * npages);
+  rc |= alloc_dev((void **)&B->d_info, sizeof(PageInfo) * npages);
+  rc |= alloc_dev((void **)&B->d_status, sizeof(uint32_t) * npages);
+  rc |= alloc_dev((void **)&B->d_cols, sizeof(ColDesc) * B->cols.size());
+  rc |= alloc_dev((void **)&B->d_dict, sizeof(uint64_t) * (size_t)B->dict_entries);
+  size_t nl = B->snappy_list.size() + B->dict_list.size() + B->data_list.size();
+  rc |= alloc_dev((void **)&B->d_lists, sizeof(int32_t) * nl);
+  if (rc) {
+    pqg_batch_destroy(B);
+    return PQG_ERR_DEVICE;
+  }
+  if (hipHostMalloc((void **)&B->h_status, sizeof(uint32_t) * (npages + 1), hipHostMallocDefault) != hipSuccess) {
+    pqg_batch_destroy(B);
+    set_err("hipHostMalloc failed");
+    return PQG_ERR_DEVICE;
+  }
+  hipStream_t s = ctx->stream;
+  // one upload of all chunk bytes (pinned bounce for large inputs)
+  {
+    void *pin = nullptr;
+    if (in_bytes && hipHostMalloc(&pin, in_bytes, hipHostMallocDefault) == hipSuccess) {
+      memcpy(pin, in.v.data(), in_bytes);
+      hipMemcpyAsync(B->d_in, pin, in_bytes, hipMemcpyHostToDevice, s);
+      hipStreamSynchronize(s);
+      hipHostFree(pin);
+    } else if (in_bytes) {
+      hipMemcpy(B->d_in, in.v.data(), in_bytes, hipMemcpyHostToDevice);
+    }
+    hipMemsetAsync(B->d_in + in_bytes, 0, kPad, s);
+    B->h2d_bytes += (int64_t)in_bytes;
+  }
+  for (auto &hb : host_bodies) {
+    HIPCHK(hipMemcpy(B->d_stage + hb.first, hb.second.data(), hb.second.size(), hipMemcpyHostToDevice));
+    B->h2d_bytes += (int64_t)hb.second.size();
+  }
+  if (npages) HIPCHK(hipMemcpy(B->d_pages, B->pages.data(), sizeof(PageDesc) * npages, hipMemcpyHostToDevice));
+  {
+    std::vector<int32_t> lists;
+    lists.insert(lists.end(), B->snappy_list.begin(), B->snappy_list.end());
+    lists.insert(lists.end(), B->dict_list.begin(), B->dict_list.end());
+    lists.insert(lists.end(), B->data_list.begin(), B->data_list.end());
+    if (!lists.empty()) HIPCHK(hipMemcpy(B->d_lists, lists.data(), sizeof(int32_t) * lists.size(), hipMemcpyHostToDevice));
+  }
+  memcpy(B->h_status, B->status0.data(), sizeof(uint32_t) * npages);
+
+  // column descriptors (outputs allocated after the counting pass)
+  B->hcols.resize(B->cols.size());
+  for (size_t ci = 0; ci < B->cols.size(); ci++) {
+    ColumnPlan &cp = B->cols[ci];
+    ColDesc &c = B->hcols[ci];
+    memset(&c, 0, sizeof(c));
+    c.ptype = cp.info.physical_type;
+    c.width = cp.info.value_width;
+    c.max_def = cp.info.max_def;
+    c.max_rep = cp.info.max_rep;
+    c.rep_def = cp.info.rep_def;
+    c.page_begin = cp.page_begin;
+    c.page_end = cp.page_end;
+    c.flags = cp.flags;
+    c.total_levels = cp.levels;
+  }
+  bool any_count = false;
+  for (auto &cp : B->cols) any_count |= (cp.flags & COL_NEEDS_COUNT) != 0;
+  if (!B->cols.empty())
+    HIPCHK(hipMemcpy(B->d_cols, B->hcols.data(), sizeof(ColDesc) * B->cols.size(), hipMemcpyHostToDevice));
+  if (any_count) {
+    // counting pass: snappy + prepare + scan once to size list/string outputs
+    rc = launch_all(B, true, false);
+    if (rc) {
+      pqg_batch_destroy(B);
+      return rc;
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<ColDesc> tmp(B->cols.size());
+    HIPCHK(hipMemcpy(tmp.data(), B->d_cols, sizeof(ColDesc) * tmp.size(), hipMemcpyDeviceToHost));
+    for (size_t ci = 0; ci < B->cols.size(); ci++) {
+      B->hcols[ci].total_rows = tmp[ci].total_rows;
+      B->hcols[ci].total_slots = tmp[ci].total_slots;
+      B->hcols[ci].total_str = tmp[ci].total_str;
+    }
+  }
+  // outputs
+  for (size_t ci = 0; ci < B->cols.size(); ci++) {
+    ColumnPlan &cp = B->cols[ci];
+    ColDesc &c = B->hcols[ci];
+    if (!(cp.flags & COL_NEEDS_COUNT)) {
+      c.total_slots = cp.levels;
+      c.total_rows = cp.info.max_rep == 0 ? cp.levels : 0;
+      c.total_str = 0;
+    }
+    cp.slots = c.total_slots;
+    cp.rows = c.total_rows;
+    cp.str_bytes = c.total_str;
+    bool is_ba = c.ptype == T_BYTE_ARRAY;
+    cp.values_bytes = is_ba ? (size_t)c.total_str : (size_t)c.total_slots * (size_t)std::max(c.width, 0);
+    rc |= alloc_dev(&cp.values, cp.values_bytes);
+    if (c.max_def > 0) {
+      cp.validity_bytes = (size_t)((c.total_slots + 63) / 64) * 8;
+      rc |= alloc_dev(&cp.validity, cp.validity_bytes);
+    }
+    if (c.max_rep == 1) {
+      cp.list_off_bytes = sizeof(int32_t) * (size_t)(c.total_rows + 1);
+      cp.list_val_bytes = (size_t)((c.total_rows + 63) / 64) * 8;
+      rc |= alloc_dev(&cp.list_offsets, cp.list_off_bytes);
+      rc |= alloc_dev(&cp.list_validity, cp.list_val_bytes);
+    }
+    if (is_ba) {
+      cp.str_off_bytes = sizeof(int64_t) * (size_t)(c.total_slots + 1);
+      rc |= alloc_dev(&cp.str_offsets, cp.str_off_bytes);
+    }
+    if (cp.flags & COL_EMIT_LEVELS) {
+      rc |= alloc_dev(&cp.def_out, (size_t)cp.levels);
+      rc |= alloc_dev(&cp.rep_out, (size_t)cp.levels);
+    }
+    c.values = (uint8_t *)cp.values;
+    c.validity = (uint32_t *)cp.validity;
+    c.list_offsets = (int32_t *)cp.list_offsets;
+    c.list_validity = (uint32_t *)cp.list_validity;
+    c.str_offsets = (int64_t *)cp.str_offsets;
+    c.def_out = (uint8_t *)cp.def_out;
+    c.rep_out = (uint8_t *)cp.rep_out;
+  }
+  if (rc) {
+    pqg_batch_destroy(B);
+    return PQG_ERR_DEVICE;
+  }
+  if (!B->cols.empty())
+    HIPCHK(hipMemcpy(B->d_cols, B->hcols.data(), sizeof(ColDesc) * B->cols.size(), hipMemcpyHostToDevice));
+  for (int i = 0; i < 8; i++) hipEventCreate(&B->ev[i]);
+  *out = B;
+  return PQG_OK;
+}
+
+static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
+  hipStream_t s = B->ctx->stream;
+  const size_t npages = B->pages.size();
+  if (npages) {
+    HIPCHK(hipMemcpyAsync(B->d_status, B->h_status, sizeof(uint32_t) * npages, hipMemcpyHostToDevice, s));
+  }
+  if (!upto_scan) {
+    for (auto &cp : B->cols) {
+      if (cp.validity) HIPCHK(hipMemsetAsync(cp.validity, 0, cp.validity_bytes, s));
+      if (cp.list_validity) HIPCHK(hipMemsetAsync(cp.list_validity, 0, cp.list_val_bytes, s));
+    }
+  }
+  pq_launch_args a;
+  a.in = B->d_in;
+  a.stage = B->d_stage;
+  a.pages = B->d_pages;
+  a.info = B->d_info;
+  a.status = B->d_status;
+  a.cols = B->d_cols;
+  a.dict_ent = B->d_dict;
+  a.ncols = (int32_t)B->cols.size();
+  const int32_t ns = (int32_t)B->snappy_list.size(), nd = (int32_t)B->dict_list.size(),
+                ndata = (int32_t)B->data_list.size();
+  int e = 0;
+  B->nev = 0;
+  auto mark = [&]() {
+    if (timed) hipEventRecord(B->ev[B->nev++], s);
+  };
+  mark();
+  a.list = B->d_lists;
+  a.nlist = ns;
+  e |= pq_launch(0, &a, s);
+  mark();
+  a.list = B->d_lists + ns;
+  a.nlist = nd;
+  e |= pq_launch(1, &a, s);
+  mark();
+  a.list = B->d_lists + ns + nd;
+  a.nlist = ndata;
+  e |= pq_launch(2, &a, s);
+  mark();
+  e |= pq_launch(4, &a, s);
+  mark();
+  if (!upto_scan) {
+    e |= pq_launch(3, &a, s);
+    mark();
+    e |= pq_launch(5, &a, s);
+    mark();
+  }
+  if (e) {
+    set_err("kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+    return PQG_ERR_DEVICE;
+  }
+  return PQG_OK;
+}
+
+int pqg_batch_decode(pqg_batch *B) {
+  if (!B) return PQG_ERR_ARG;
+  HIPCHK(hipSetDevice(B->ctx->device));
+  int rc = launch_all(B, false, true);
+  B->decoded = rc == 0;
+  return rc;
+}
+
+int pqg_batch_sync(pqg_batch *B) {
+  if (!B) return PQG_ERR_ARG;
+  HIPCHK(hipSetDevice(B->ctx->device));
+  HIPCHK(hipStreamSynchronize(B->ctx->stream));
+  if (B->nev >= 2) {
+    for (int i = 0; i + 1 < B->nev; i++) hipEventElapsedTime(&B->kms[i], B->ev[i], B->ev[i + 1]);
+  }
+  const size_t npages = B->pages.size();
+  std::vector<uint32_t> st(npages);
+  if (npages) HIPCHK(hipMemcpy(st.data(), B->d_status, sizeof(uint32_t) * npages, hipMemcpyDeviceToHost));
+  // first error in the reference's order: row group, leaf, phase, page ordinal, stage
+  struct Key {
+    int rg, leaf, phase, ord;
+    uint32_t stage, code;
+  };
+  bool have = false;
+  Key best{};
+  auto consider = [&](Key k) {
+    auto t = [](const Key &x) { return std::make_tuple(x.rg, x.leaf, x.phase, x.ord, x.stage); };
+    if (!have || t(k) < t(best)) {
+      best = k;
+      have = true;
+    }
+  };
+  for (size_t i = 0; i < npages; i++) {
+    if (st[i] == STATUS_OK) continue;
+    const PageDesc &d = B->pages[i];
+    uint32_t stage = st[i] >> 16, code = st[i] & 0xffff;
+    consider({d.rg, B->cols[(size_t)d.col].leaf, stage >= ST_PHASE2 ? 1 : 0, d.ord, stage, code});
+  }
+  for (auto &ce : B->chunk_errors) consider({ce.rg, ce.leaf, 0, ce.ord, ce.stage, ce.code});
+  if (!have) {
+    B->err_rg = B->err_leaf = B->err_page = -1;
+    return PQG_OK;
+  }
+  B->err_rg = best.rg;
+  B->err_leaf = best.leaf;
+  B->err_page = best.ord;
+  set_err("decode error %u at row group %d, column %d, page %d (stage %u)", best.code, best.rg, best.leaf, best.ord,
+          best.stage);
+  return (int)best.code;
+}
+
+int pqg_batch_error_location(const pqg_batch *B, int *rg, int *leaf, int *page) {
+  if (rg) *rg = B->err_rg;
+  if (leaf) *leaf = B->err_leaf;
+  if (page) *page = B->err_page;
+  return PQG_OK;
+}
+
+int pqg_batch_column(const pqg_batch *B, int i, pqg_column_view *v) {
+  if (!B || i < 0 || i >= (int)B->cols.size()) return PQG_ERR_ARG;
+  const ColumnPlan &cp = B->cols[(size_t)i];
+  memset(v, 0, sizeof(*v));
+  v->values = cp.values;
+  v->validity = cp.validity;
+  v->list_offsets = cp.list_offsets;
+  v->list_validity = cp.list_validity;
+  v->str_offsets = cp.str_offsets;
+  v->def_levels = cp.def_out;
+  v->rep_levels = cp.rep_out;
+  v->levels = cp.levels;
+  v->slots = cp.slots;
+  v->rows = cp.rows;
+  v->str_bytes = cp.str_bytes;
+  v->value_width = cp.info.value_width;
+  v->leaf = cp.leaf;
+  v->non_null = -1;
+  return PQG_OK;
+}
+
+int pqg_batch_copy(pqg_batch *B, int i, int buf, void *dst, size_t cap, size_t *nbytes) {
+  if (!B || i < 0 || i >= (int)B->cols.size()) return PQG_ERR_ARG;
+  HIPCHK(hipSetDevice(B->ctx->device));
+  const ColumnPlan &cp = B->cols[(size_t)i];
+  const void *src = nullptr;
+  size_t n = 0;
+  switch (buf) {
+    case PQG_BUF_VALUES: src = cp.values; n = cp.values_bytes; break;
+    case PQG_BUF_VALIDITY: src = cp.validity; n = (size_t)((cp.slots + 7) / 8); break;
+    case PQG_BUF_LIST_OFFSETS: src = cp.list_offsets; n = cp.list_off_bytes; break;
+    case PQG_BUF_LIST_VALIDITY: src = cp.list_validity; n = (size_t)((cp.rows + 7) / 8); break;
+    case PQG_BUF_STR_OFFSETS: src = cp.str_offsets; n = cp.str_off_bytes; break;
+    case PQG_BUF_DEF: src = cp.def_out; n = cp.def_out ? (size_t)cp.levels : 0; break;
+    case PQG_BUF_REP: src = cp.rep_out; n = cp.rep_out ? (size_t)cp.levels : 0; break;
+    default: return PQG_ERR_ARG;
+  }
+  if (!src) n = 0;
+  if (nbytes) *nbytes = n;
+  if (!dst) return PQG_OK;
+  if (cap < n) {
+    set_err("buffer too small (%zu < %zu)", cap, n);
+    return PQG_ERR_ARG;
+  }
+  if (n) {
+    HIPCHK(hipStreamSynchronize(B->ctx->stream));
+    HIPCHK(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost));
+  }
+  return PQG_OK;
+}
+
+int pqg_batch_stats_get(const pqg_batch *B, pqg_batch_stats *o) {
+  if (!B || !o) return PQG_ERR_ARG;
+  memset(o, 0, sizeof(*o));
+  o->pages = (int64_t)B->pages.size();
+  o->data_pages = (int64_t)B->data_list.size();
+  o->dict_pages = (int64_t)B->dict_list.size();
+  o->snappy_pages = (int64_t)B->snappy_list.size();
+  o->host_inflated_pages = B->host_inflated;
+  o->staged_bytes = B->staged_bytes;
+  o->h2d_bytes = B->h2d_bytes;
+  // B_in: stored payload bytes of the planned pages
+  int64_t bin = 0;
+  for (auto &d : B->pages) {
+    int64_t lsize = d.kind == PAGE_V2 ? (int64_t)d.v2_rep_len + d.v2_def_len : 0;
+    bin += (int64_t)d.comp_len + lsize;
+  }
+  o->input_bytes = bin;
+  int64_t bout = 0;
+  for (auto &cp : B->cols) {
+    bout += (int64_t)cp.values_bytes;
+    if (cp.validity) bout += (cp.slots + 7) / 8;
+    if (cp.list_offsets) bout += (int64_t)cp.list_off_bytes + (cp.rows + 7) / 8;
+    if (cp.str_offsets) bout += (int64_t)cp.str_off_bytes;
+  }
+  o->output_bytes = bout;
+  return PQG_OK;
+}
+
+int pqg_batch_kernel_times(pqg_batch *B, const char **names, float *ms, int cap) {
+  int n = B->nev > 0 ? B->nev - 1 : 0;
+  // timeline: [snappy, dict, prepare, scan, decode, level_check]
+  for (int i = 0; i < n && i < cap; i++) {
+    if (names) names[i] = kKernelNames[i];
+    if (ms) ms[i] = B->kms[i];
+  }
+  return n;
+}
+
+void pqg_batch_destroy(pqg_batch *B) {
+  if (!B) return;
+  hipSetDevice(B->ctx->device);
+  hipStreamSynchronize(B->ctx->stream);
+  for (auto &cp : B->cols) {
+    hipFree(cp.values);
+    hipFree(cp.validity);
+    hipFree(cp.list_offsets);
+    hipFree(cp.list_validity);
+    hipFree(cp.str_offsets);
+    hipFree(cp.def_out);
+    hipFree(cp.rep_out);
+  }
+  hipFree(B->d_in);
+  hipFree(B->d_stage);
+  hipFree(B->d_pages);
+  hipFree(B->d_info);
+  hipFree(B->d_status);
+  hipFree(B->d_cols);
+  hipFree(B->d_dict);
+  hipFree(B->d_lists);
+  if (B->h_status) hipHostFree(B->h_status);
+  for (int i = 0; i < 8; i++)
+    if (B->ev[i]) hipEventDestroy(B->ev[i]);
+  delete B;
+}
+
+}  // extern "C"
+
+// single-block device snappy for pqg_decompress_block
+static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8_t *dst, size_t expect, int *code) {
+  HIPCHK(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  uint8_t *d_in = nullptr, *d_out = nullptr;
+  PageDesc *d_page = nullptr;
+  uint32_t *d_st = nullptr;
+  int32_t *d_list = nullptr;
+  int rc = 0;
+  rc |= alloc_dev((void **)&d_in, n);
+  rc |= alloc_dev((void **)&d_out, expect);
+  rc |= alloc_dev((void **)&d_page, sizeof(PageDesc));
+  rc |= alloc_dev((void **)&d_st, sizeof(uint32_t));
+  rc |= alloc_dev((void **)&d_list, sizeof(int32_t));
+  if (!rc) {
+    PageDesc d;
+    memset(&d, 0, sizeof(d));
+    d.kind = PAGE_DICT;
+    d.comp_len = (int32_t)n;
+    d.body_len = (int32_t)expect;
+    d.body_src = BODY_SNAPPY;
+    uint32_t st = STATUS_OK;
+    int32_t zero = 0;
+    hipMemcpy(d_in, src, n, hipMemcpyHostToDevice);
+    hipMemcpy(d_page, &d, sizeof(d), hipMemcpyHostToDevice);
+    hipMemcpy(d_st, &st, 4, hipMemcpyHostToDevice);
+    hipMemcpy(d_list, &zero, 4, hipMemcpyHostToDevice);
+    pq_launch_args a;
+    memset(&a, 0, sizeof(a));
+    a.in = d_in;
+    a.stage = d_out;
+    a.pages = d_page;
+    a.status = d_st;
+    a.list = d_list;
+    a.nlist = 1;
+    rc = pq_launch(0, &a, s);
+    hipStreamSynchronize(s);
+    hipMemcpy(&st, d_st, 4, hipMemcpyDeviceToHost);
+    *code = st == STATUS_OK ? 0 : (int)(st & 0xffff);
+    if (!*code && expect) hipMemcpy(dst, d_out, expect, hipMemcpyDeviceToHost);
+  }
+  hipFree(d_in);
+  hipFree(d_out);
+  hipFree(d_page);
+  hipFree(d_st);
+  hipFree(d_list);
+  if (rc) {
+    set_err("device snappy failed");
+    return PQG_ERR_DEVICE;
+  }
+  return PQG_OK;
+}

@@ -1,0 +1,197 @@
+"""GPU parity: libpqgpu.so (HIP kernels on cuda:0) against the CPU oracle and the
+committed golden fixtures.  Bit-exact on every output buffer."""
+import io
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import pqgpu
+from conftest import GOLDEN, golden_bytes
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("values", "validity", "list_offsets", "list_validity", "str_offsets", "def", "rep")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if pqgpu.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+
+
+def assert_same(gpu, ora, max_def, max_rep, ctx=""):
+    for k in KEYS:
+        if k == "validity" and max_def == 0:
+            continue
+        if k in ("list_offsets", "list_validity") and max_rep != 1:
+            continue
+        a, b = gpu[k], ora[k]
+        if k in ("def", "rep") and a.size == 0:
+            continue
+        assert a.size == b.size, (ctx, k, a.size, b.size)
+        if not np.array_equal(a, b):
+            bad = np.nonzero(a != b)[0]
+            raise AssertionError("%s %s: %d bytes differ, first at %d (gpu %d, oracle %d)"
+                                 % (ctx, k, bad.size, bad[0], a[bad[0]], b[bad[0]]))
+    for k in ("slots", "str_bytes"):
+        assert gpu[k] == ora[k], (ctx, k)
+    if max_rep == 1:
+        assert gpu["rows"] == ora["rows"], ctx
+
+
+def gpu_decode_all(data, levels=True, rg0=0, rg1=None, leaves=None):
+    r = pqgpu.FileReader(data)
+    rg1 = r.RowGroupCount() if rg1 is None else rg1
+    leaves = list(range(len(r.Columns()))) if leaves is None else leaves
+    b = r.batch(rg0, rg1, leaves, pqgpu.BATCH_LEVELS if levels else 0)
+    b.decode()
+    rc = b.sync(raise_on_error=False)
+    out = {leaf: b.column(i) for i, leaf in enumerate(leaves)} if rc == 0 else None
+    b.close()
+    return rc, out, r.Columns()
+
+
+def check_file(data, ctx, rg0=0, rg1=None):
+    o = oracle.File(data)
+    rg1 = o.num_row_groups if rg1 is None else rg1
+    exp, first_err = {}, None
+    for leaf, info in enumerate(o.leaves()):
+        try:
+            exp[leaf] = o.decode(leaf, rg0, rg1)
+        except oracle.OracleError as e:
+            # first error in (row group, leaf) order is what the batch must report
+            key = (e.rg, leaf)
+            if first_err is None or key < first_err[0]:
+                first_err = (key, e.code)
+    rc, got, cols = gpu_decode_all(data, True, rg0, rg1)
+    if first_err is not None:
+        assert rc == first_err[1], (ctx, rc, first_err)
+        return
+    assert rc == 0, (ctx, rc, pqgpu.last_error())
+    for leaf, info in enumerate(o.leaves()):
+        assert_same(got[leaf], exp[leaf], info["max_def"], info["max_rep"], "%s leaf %d" % (ctx, leaf))
+
+
+def fixture_names():
+    return sorted(json.load(open(os.path.join(GOLDEN, "manifest.json"))))
+
+
+@pytest.mark.parametrize("name", fixture_names())
+def test_golden_fixture_parity(name, manifest):
+    data = golden_bytes(name + ".parquet")
+    check_file(data, name)
+    # and against the committed pyarrow expectations
+    e = manifest[name]
+    cols = [c for c in e["columns"].values()]
+    if any("error" in c for c in cols):
+        rc, _, _ = gpu_decode_all(data)
+        assert rc == [c["error"] for c in cols if "error" in c][0]
+        return
+    exp = np.load(os.path.join(GOLDEN, name + ".npz"))
+    rc, got, info = gpu_decode_all(data, levels=False)
+    assert rc == 0
+    for key, c in e["columns"].items():
+        g = got[c["leaf"]]
+        for k in ("values", "validity", "list_offsets", "list_validity", "str_offsets"):
+            ek = "%s_%s" % (key, k)
+            if ek not in exp or (k == "validity" and info[c["leaf"]]["max_def"] == 0):
+                continue
+            assert np.array_equal(g[k], exp[ek].view(np.uint8).ravel()), (name, key, k)
+
+
+def test_row_group_subsets():
+    data = golden_bytes("c4_list_str.parquet")
+    check_file(data, "c4 rg1", 1, 2)
+    check_file(data, "c4 rg1-3", 1, 3)
+    data = golden_bytes("c1_int64_plain.parquet")
+    check_file(data, "c1 rg2", 2, 3)
+
+
+def test_snappy_block_roundtrip():
+    pa = pytest.importorskip("pyarrow")
+    rng = np.random.default_rng(5)
+    for n in (0, 1, 5, 64, 65, 4095, 8192, 8193, 70000, 300000):
+        for kind in ("rand", "rep", "mixed"):
+            if kind == "rand":
+                data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            elif kind == "rep":
+                data = (b"0123456789abcdefXYZ" * (n // 19 + 1))[:n]
+            else:
+                data = np.round(rng.standard_normal(n // 8 + 1), 2).tobytes()[:n]
+            comp = pa.compress(data, codec="snappy", asbytes=True)
+            assert pqgpu.DecompressBlock(pqgpu.CompressionCodec_SNAPPY, comp, n) == data, (n, kind)
+    # far back-references (offset > the 8 KB LDS history): repeat a random 20 KB block
+    blk = rng.integers(0, 256, 20000, dtype=np.uint8).tobytes()
+    data = blk * 3
+    comp = pa.compress(data, codec="snappy", asbytes=True)
+    assert pqgpu.DecompressBlock(pqgpu.CompressionCodec_SNAPPY, comp, len(data)) == data
+
+
+def test_snappy_block_errors_match_oracle():
+    cases = [bytes([4, 0b01, 0]), bytes([4, 0x0c, 1, 2, 3]), bytes([5, 0x0c, 1, 2, 3]), b"", bytes([0x80]),
+             bytes([3, 0x08, 1, 2, 3]), bytes([2, 0x04, 7, 8, 0x01, 1])]
+    for c in cases:
+        rc_o, _ = oracle.snappy_decode(c, 4)
+        for expect in (4, 3, 2):
+            rc_o, _ = oracle.snappy_decode(c, expect)
+            try:
+                pqgpu.DecompressBlock(pqgpu.CompressionCodec_SNAPPY, c, expect)
+                rc_g = 0
+            except pqgpu.PqgError as e:
+                rc_g = e.code
+            # oracle reports SIZE when the decoded length (header) differs from cap
+            if rc_o == 0:
+                rc_o = 0
+            assert (rc_g == 0) == (rc_o == 0), (c, expect, rc_g, rc_o)
+
+
+def _pq_bytes(table, **kw):
+    pq = pytest.importorskip("pyarrow.parquet")
+    buf = io.BytesIO()
+    pq.write_table(table, buf, **kw)
+    return buf.getvalue()
+
+
+@pytest.mark.parametrize("bw", [3, 7, 13, 17, 20])
+def test_generated_dictionary_widths(bw):
+    pa = pytest.importorskip("pyarrow")
+    rng = np.random.default_rng(bw)
+    K = 1 << bw
+    rows = max(3 * K // 2, 50000) if bw <= 17 else 700000
+    dvals = rng.permutation(K).astype(np.int32) * 3 - 7
+    t = pa.table({"v": pa.array(dvals[rng.integers(0, K, rows)])},
+                 schema=pa.schema([pa.field("v", pa.int32(), nullable=False)]))
+    check_file(_pq_bytes(t, compression="snappy", dictionary_pagesize_limit=1 << 30, row_group_size=1 << 18),
+               "dict bw%d" % bw)
+
+
+def test_generated_nullable_mix():
+    pa = pytest.importorskip("pyarrow")
+    rng = np.random.default_rng(11)
+    n = 120000
+    ts = (1_600_000_000_000_000 + np.cumsum(np.where(rng.random(n) < 0.95, 1000, rng.integers(0, 4096, n)))).astype(np.int64)
+    t = pa.table({
+        "ts": pa.array(ts),
+        "x": pa.array(np.round(rng.standard_normal(n), 2), mask=rng.random(n) < 0.1),
+        "i": pa.array(rng.integers(-5, 5, n).astype(np.int32), mask=rng.random(n) < 0.5),
+        "s": pa.array(["k%d" % v if v % 7 else None for v in rng.integers(0, 500, n)]),
+    })
+    for ver in ("1.0", "2.0"):
+        check_file(_pq_bytes(t, compression="snappy", data_page_version=ver, use_dictionary=["s", "i"],
+                             column_encoding={"ts": "DELTA_BINARY_PACKED", "x": "PLAIN"}, row_group_size=50000),
+                   "mix v" + ver)
+
+
+def test_generated_lists():
+    pa = pytest.importorskip("pyarrow")
+    rng = np.random.default_rng(12)
+    n = 60000
+    lists = [None if rng.random() < 0.05 else [None if rng.random() < 0.05 else int(v)
+                                                for v in rng.integers(0, 100, rng.poisson(4))] for _ in range(n)]
+    strs = [None if rng.random() < 0.1 else ["w%d" % v for v in rng.integers(0, 50, rng.poisson(2))] for _ in range(n)]
+    t = pa.table({"l": pa.array(lists, pa.list_(pa.int32())), "ls": pa.array(strs, pa.list_(pa.string()))})
+    check_file(_pq_bytes(t, compression="snappy", row_group_size=25000), "lists v1")
+    check_file(_pq_bytes(t, compression="snappy", row_group_size=25000, data_page_version="2.0"), "lists v2")
