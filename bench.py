@@ -1,0 +1,187 @@
+"""bench.py — decoded GB/s of the MI355X Parquet decoder (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], the single-GPU headline config): one
+required INT32 column, 100M rows, RLE_DICTIONARY pages whose index bit width
+sweeps 1..20 across row groups (row group i uses a dictionary of 2^(1 + i % 20)
+entries), Snappy, data page V1, ~1M-row row groups, 20k-row pages.  Synthetic
+data (seeded), written with pyarrow on the box, then planned on the host and
+uploaded to HBM once; the timed region is the whole GPU decode pipeline
+(snappy -> prepare -> scan -> decode) with every page already resident.
+
+A "step" decodes every page of the file once.  For N > 1 each rank decodes its
+own identical 100M-row shard on its own GPU (weak scaling, no collective on the
+data path); value = decoded bytes of all ranks / max-over-ranks time.
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "parquet-go_amd"))
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def make_file(path, rows, rg_rows, seed=2):
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    rng = np.random.default_rng(seed)
+    schema = pa.schema([pa.field("v", pa.int32(), nullable=False)])
+    tmp = path + ".tmp%d" % os.getpid()
+    with pq.ParquetWriter(tmp, schema, compression="snappy", use_dictionary=True, data_page_version="1.0",
+                          dictionary_pagesize_limit=1 << 30) as w:
+        done, i = 0, 0
+        while done < rows:
+            n = min(rg_rows, rows - done)
+            bw = 1 + (i % 20)
+            K = 1 << bw
+            dvals = (rng.permutation(K).astype(np.int64) * 2654435761 % (1 << 32) - (1 << 31)).astype(np.int32)
+            idx = rng.integers(0, K, n)
+            w.write_table(pa.table({"v": pa.array(dvals[idx])}, schema=schema), row_group_size=n)
+            done += n
+            i += 1
+    os.replace(tmp, path)
+
+
+def cpu_baseline(path, budget_s=10.0):
+    """The CPU oracle (a serial C port of the reference read path) on a bounded
+    sample of the same file: whole row groups until ~budget_s of CPU time."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    data = open(path, "rb").read()
+    f = oracle.File(data)
+    L = oracle.lib()
+    t_total, out_bytes, rows, rgs = 0.0, 0, 0, 0
+    for rg in range(f.num_row_groups):
+        r = ctypes.c_void_p()
+        t0 = time.perf_counter()
+        st = L.pqref_decode(f._h, 0, rg, rg + 1, ctypes.byref(r))
+        t_total += time.perf_counter() - t0
+        if st != 0:
+            raise RuntimeError("oracle failed on the bench file: %d" % st)
+        out_bytes += L.pqref_result_count(r, oracle.CNT_SLOTS) * 4
+        rows += L.pqref_result_count(r, oracle.CNT_SLOTS)
+        L.pqref_result_free(r)
+        rgs += 1
+        if t_total >= budget_s:
+            break
+    return {"value": out_bytes / t_total / 1e9, "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": "oracle/pqref.c single-thread on %d of %d row groups (%d rows) of the bench file, %.1f s"
+                      % (rgs, f.num_row_groups, rows, t_total)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows", type=int, default=100_000_000)
+    ap.add_argument("--rg-rows", type=int, default=1 << 20)
+    ap.add_argument("--file", default=None)
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    import pqgpu
+    path = args.file or os.path.join(os.environ.get("TMPDIR", "/tmp"),
+                                     "pqgpu_bench_c2_%d_%d.parquet" % (args.rows, args.rg_rows))
+    if local == 0 and not os.path.exists(path):
+        make_file(path, args.rows, args.rg_rows)
+    barrier()
+
+    ctx = pqgpu.Context(local if world > 1 else 0)
+    reader = pqgpu.FileReader(path, ctx=ctx)
+    batch = reader.batch()
+    stats = batch.stats()
+
+    def step():
+        batch.decode()
+
+    for _ in range(args.warmup):
+        step()
+    batch.sync()
+    batch.kernel_times()  # drop warmup events
+    barrier()
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipDeviceSynchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    hip.hipDeviceSynchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    batch.sync()  # raises if any page failed to decode
+    # per-kernel HIP-event times recorded on the decode stream during the timed steps
+    kern = {k: [v] for k, v in batch.kernel_times().items()}
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    out_b, in_b = stats["output_bytes"], stats["input_bytes"]
+    per_step = dt / args.steps
+    value = out_b * world * args.steps / dt / 1e9
+    avg = {k: float(np.mean(v)) for k, v in kern.items()}
+    dom = max(avg, key=avg.get)
+    # algorithmic bytes per launch of each kernel
+    alg = {
+        "k_snappy": stats["input_bytes"] + stats["staged_bytes"],     # compressed in + uncompressed out
+        "k_decode": stats["staged_bytes"] + out_b,                    # encoded indices in + decoded values out
+    }
+    ach = alg.get(dom, in_b + out_b) / (avg[dom] * 1e-3) / 1e9
+    line = {
+        "metric": "decoded GB/s (uncompressed output) per GPU + node at 1/2/4/8 MI355X, % HBM peak",
+        "value": round(value, 3),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(per_step * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (seeded pyarrow writer: dictionary INT32, bit widths 1-20 across row groups, snappy, V1)",
+        "config": {"workload": "C2: INT32 RLE_DICTIONARY bw 1-20, Snappy, V1, %d rows, %d-row row groups"
+                               % (args.rows, args.rg_rows),
+                   "rows_per_gpu": args.rows, "pages": stats["data_pages"], "dict_pages": stats["dict_pages"],
+                   "B_in": in_b, "B_out": out_b, "staged": stats["staged_bytes"],
+                   "pipeline_hbm_frac": round((in_b + out_b) / per_step / 1e9 / HBM_PEAK_GBPS, 4),
+                   "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
+                   "parallelism": "row-group shards, one process per GPU, no data-path collective"},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None},
+    }
+    if rank == 0 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(path, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    batch.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -141,7 +141,7 @@ def snappy_decode(src: bytes, cap: int):
     dst = ctypes.create_string_buffer(max(cap, 1))
     n = ctypes.c_size_t()
     rc = lib().pqref_snappy_decode(src, len(src), dst, cap, ctypes.byref(n))
-    return rc, dst.raw[:min(n.value, cap)]
+    return rc, dst.raw[:min(n.value, cap)], n.value
 
 
 def unpack8_32(data: bytes, width: int):

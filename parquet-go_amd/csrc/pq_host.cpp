@@ -502,10 +502,13 @@ struct pqg_batch {
   int32_t *d_lists = nullptr;
   uint32_t *h_status = nullptr;  // pinned mirror
   std::vector<ColDesc> hcols;
-  // timing
-  hipEvent_t ev[8] = {};
+  // timing: a ring of event sets, one per decode, harvested by pqg_batch_kernel_times
+  static constexpr int kRing = 64;
+  hipEvent_t ev[kRing][8] = {};
   int nev = 0;
-  float kms[8] = {};
+  int ring_head = 0, ring_count = 0;
+  double kms_sum[8] = {};
+  int kms_n = 0;
   int err_rg = -1, err_leaf = -1, err_page = -1;
   bool decoded = false;
 };
@@ -1220,6 +1223,8 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
     B->h2d_bytes += (int64_t)hb.second.size();
   }
   if (npages) HIPCHK(hipMemcpy(B->d_pages, B->pages.data(), sizeof(PageDesc) * npages, hipMemcpyHostToDevice));
+  // pages that fail before k_prepare contribute zero counts to the scans
+  if (npages) HIPCHK(hipMemset(B->d_info, 0, sizeof(PageInfo) * npages));
   {
     std::vector<int32_t> lists;
     lists.insert(lists.end(), B->snappy_list.begin(), B->snappy_list.end());
@@ -1312,7 +1317,8 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   }
   if (!B->cols.empty())
     HIPCHK(hipMemcpy(B->d_cols, B->hcols.data(), sizeof(ColDesc) * B->cols.size(), hipMemcpyHostToDevice));
-  for (int i = 0; i < 8; i++) hipEventCreate(&B->ev[i]);
+  for (int k = 0; k < pqg_batch::kRing; k++)
+    for (int i = 0; i < 8; i++) hipEventCreate(&B->ev[k][i]);
   *out = B;
   return PQG_OK;
 }
@@ -1342,8 +1348,9 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
                 ndata = (int32_t)B->data_list.size();
   int e = 0;
   B->nev = 0;
+  hipEvent_t *evs = B->ev[B->ring_head];
   auto mark = [&]() {
-    if (timed) hipEventRecord(B->ev[B->nev++], s);
+    if (timed) hipEventRecord(evs[B->nev++], s);
   };
   mark();
   a.list = B->d_lists;
@@ -1370,6 +1377,10 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     set_err("kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     return PQG_ERR_DEVICE;
   }
+  if (timed) {
+    B->ring_head = (B->ring_head + 1) % pqg_batch::kRing;
+    B->ring_count = std::min(B->ring_count + 1, pqg_batch::kRing);
+  }
   return PQG_OK;
 }
 
@@ -1385,9 +1396,6 @@ int pqg_batch_sync(pqg_batch *B) {
   if (!B) return PQG_ERR_ARG;
   HIPCHK(hipSetDevice(B->ctx->device));
   HIPCHK(hipStreamSynchronize(B->ctx->stream));
-  if (B->nev >= 2) {
-    for (int i = 0; i + 1 < B->nev; i++) hipEventElapsedTime(&B->kms[i], B->ev[i], B->ev[i + 1]);
-  }
   const size_t npages = B->pages.size();
   std::vector<uint32_t> st(npages);
   if (npages) HIPCHK(hipMemcpy(st.data(), B->d_status, sizeof(uint32_t) * npages, hipMemcpyDeviceToHost));
@@ -1510,12 +1518,30 @@ int pqg_batch_stats_get(const pqg_batch *B, pqg_batch_stats *o) {
   return PQG_OK;
 }
 
+// Average per-kernel device time over the decodes issued since the previous
+// call (up to the last 64), from HIP events recorded on the context stream
+// between consecutive launches: [snappy, dict, prepare, scan, decode, level_check].
 int pqg_batch_kernel_times(pqg_batch *B, const char **names, float *ms, int cap) {
   int n = B->nev > 0 ? B->nev - 1 : 0;
-  // timeline: [snappy, dict, prepare, scan, decode, level_check]
+  if (hipSetDevice(B->ctx->device) != hipSuccess) return 0;
+  if (B->ring_count > 0) {
+    hipStreamSynchronize(B->ctx->stream);
+    for (int i = 0; i < 8; i++) B->kms_sum[i] = 0;
+    B->kms_n = 0;
+    for (int k = 0; k < B->ring_count; k++) {
+      int slot = (B->ring_head - 1 - k + 2 * pqg_batch::kRing) % pqg_batch::kRing;
+      for (int i = 0; i < n; i++) {
+        float t = 0;
+        hipEventElapsedTime(&t, B->ev[slot][i], B->ev[slot][i + 1]);
+        B->kms_sum[i] += t;
+      }
+      B->kms_n++;
+    }
+    B->ring_count = 0;
+  }
   for (int i = 0; i < n && i < cap; i++) {
     if (names) names[i] = kKernelNames[i];
-    if (ms) ms[i] = B->kms[i];
+    if (ms) ms[i] = B->kms_n ? (float)(B->kms_sum[i] / B->kms_n) : 0.f;
   }
   return n;
 }
@@ -1542,8 +1568,9 @@ void pqg_batch_destroy(pqg_batch *B) {
   hipFree(B->d_dict);
   hipFree(B->d_lists);
   if (B->h_status) hipHostFree(B->h_status);
-  for (int i = 0; i < 8; i++)
-    if (B->ev[i]) hipEventDestroy(B->ev[i]);
+  for (int k = 0; k < pqg_batch::kRing; k++)
+    for (int i = 0; i < 8; i++)
+      if (B->ev[k][i]) hipEventDestroy(B->ev[k][i]);
   delete B;
 }
 

@@ -131,21 +131,22 @@ def test_snappy_block_roundtrip():
 
 
 def test_snappy_block_errors_match_oracle():
+    """DecompressBlock = snappy.Decode + the exact-size check of newBlockReader
+    (compress.go:112-119): class SNAPPY if the stream is corrupt, else SIZE if
+    the decoded length differs from the page header's."""
     cases = [bytes([4, 0b01, 0]), bytes([4, 0x0c, 1, 2, 3]), bytes([5, 0x0c, 1, 2, 3]), b"", bytes([0x80]),
-             bytes([3, 0x08, 1, 2, 3]), bytes([2, 0x04, 7, 8, 0x01, 1])]
+             bytes([3, 0x08, 1, 2, 3]), bytes([2, 0x04, 7, 8, 0x01, 1]), bytes([6, 0x04, 7, 8, 0x05, 1]),
+             bytes([8, 0x04, 7, 8, 0x0a, 2, 0]), bytes([0xff] * 11)]
     for c in cases:
-        rc_o, _ = oracle.snappy_decode(c, 4)
-        for expect in (4, 3, 2):
-            rc_o, _ = oracle.snappy_decode(c, expect)
+        for expect in (8, 6, 4, 3, 2):
+            rc_o, _, n = oracle.snappy_decode(c, 64)
+            want = rc_o if rc_o else (pqgpu.ERR_SIZE if n != expect else 0)
             try:
                 pqgpu.DecompressBlock(pqgpu.CompressionCodec_SNAPPY, c, expect)
                 rc_g = 0
             except pqgpu.PqgError as e:
                 rc_g = e.code
-            # oracle reports SIZE when the decoded length (header) differs from cap
-            if rc_o == 0:
-                rc_o = 0
-            assert (rc_g == 0) == (rc_o == 0), (c, expect, rc_g, rc_o)
+            assert rc_g == want, (c, expect, rc_g, want)
 
 
 def _pq_bytes(table, **kw):

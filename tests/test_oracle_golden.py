@@ -99,7 +99,7 @@ def test_snappy_oracle_roundtrip():
             data = rng.integers(0, 256, n, dtype=np.uint8).tobytes() if kind == "rand" else \
                 (b"abcdefgh12" * (n // 10 + 1))[:n]
             comp = pa.compress(data, codec="snappy", asbytes=True)
-            rc, out = oracle.snappy_decode(comp, n)
+            rc, out, _ = oracle.snappy_decode(comp, n)
             assert rc == 0 and out == data
     # corrupt inputs: offset 0, offset beyond output, truncated literal
     assert oracle.snappy_decode(bytes([4, 0b01, 0]), 4)[0] == oracle_status("SNAPPY")
