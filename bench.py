@@ -147,7 +147,7 @@ def main():
     dom = max(avg, key=avg.get)
     # algorithmic bytes per launch of each kernel
     alg = {
-        "k_snappy": stats["input_bytes"] + stats["staged_bytes"],     # compressed in + uncompressed out
+        "k_snappy+k_copy": stats["input_bytes"] + stats["staged_bytes"],     # compressed in + uncompressed out
         "k_decode": stats["staged_bytes"] + out_b,                    # encoded indices in + decoded values out
     }
     ach = alg.get(dom, in_b + out_b) / (avg[dom] * 1e-3) / 1e9

@@ -35,6 +35,15 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
   uint32_t lo = shfl32((uint32_t)v, src), hi = shfl32((uint32_t)(v >> 32), src);
   return ((uint64_t)hi << 32) | lo;
 }
+__device__ __forceinline__ int32_t wave_incl_scan32_impl(int32_t v) {
+  int lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    int32_t o = (int32_t)shfl32((uint32_t)v, lane >= d ? lane - d : lane);
+    if (lane >= d) v += o;
+  }
+  return v;
+}
 // inclusive wave prefix sum
 __device__ __forceinline__ int64_t wave_incl_scan64(int64_t v) {
   int lane = lane_id();
@@ -53,6 +62,12 @@ __device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {  // wrappin
     if (lane >= d) v += o;
   }
   return v;
+}
+// exclusive wave prefix sum; *total receives the wave total (uniform)
+__device__ __forceinline__ int32_t wave_excl_scan32(int32_t v, int32_t *total) {
+  int32_t incl = wave_incl_scan32_impl(v);
+  *total = (int32_t)__builtin_amdgcn_readlane((uint32_t)incl, 63);
+  return incl - v;
 }
 __device__ __forceinline__ int32_t wave_incl_scan32(int32_t v) {
   int lane = lane_id();
@@ -226,6 +241,43 @@ struct Hyb {
     return E_OK;
   }
 
+  // Produce the next n (<= 256) values, four per lane: value j goes to lane
+  // j >> 2, element j & 3.
+  __device__ uint32_t next4(int n, uint32_t (&out)[4]) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int k = 0; k < 4; k++) out[k] = 0;
+    if (bw == 0) return E_OK;
+    int got = 0;
+    while (got < n) {
+      if (rem == 0) {
+        uint32_t e = header();
+        if (e) return e;
+      }
+      const int take = (int)min<int64_t>(rem, (int64_t)(n - got));
+      if (rle) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          int j = 4 * lane + k;
+          if (j >= got && j < got + take) out[k] = rle_val;
+        }
+      } else {
+        int64_t last_group = (vi + take - 1) >> 3;
+        if (data + last_group * bw >= len) return E_EOF;
+        const int64_t bit0 = data * 8 + (vi - got) * (int64_t)bw;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          int j = 4 * lane + k;
+          if (j >= got && j < got + take) out[k] = unpack_u32(p, len, bit0 + (int64_t)j * bw, bw);
+        }
+        vi += take;
+      }
+      rem -= take;
+      got += take;
+    }
+    return E_OK;
+  }
+
   // Produce the next n (<= 64) values: lane l < n receives value l.
   __device__ uint32_t next(int n, uint32_t &out) {
     int lane = lane_id();
@@ -323,6 +375,41 @@ struct Delta {
     mb_vi = mbvc;  // no miniblock started yet
     cur_mb = 0;
     position = 0;
+    return E_OK;
+  }
+
+  // four per lane: value j of the next n (<= 256) goes to lane j >> 2, element j & 3
+  __device__ uint32_t next4(int n, uint64_t (&out)[4]) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int k = 0; k < 4; k++) out[k] = 0;
+    if (position + n > total) return E_EOF;
+    int got = 0;
+    while (got < n) {
+      if (mb_vi >= mbvc) {
+        if (cur_mb >= mb_count) {
+          uint32_t e = read_mb_header();
+          if (e) return e;
+        }
+        mb_w = (int32_t)__builtin_amdgcn_readlane(widths, cur_mb);
+        mb_data = pos;
+        pos = mb_data + (int64_t)(mbvc >> 3) * mb_w;
+        cur_mb++;
+        mb_vi = 0;
+      }
+      const int take = min(mbvc - mb_vi, n - got);
+      int64_t last_group = (mb_vi + take - 1) >> 3;
+      if (mb_data + (last_group + 1) * mb_w > len) return E_EOF;
+      const int64_t bit0 = mb_data * 8 + (int64_t)(mb_vi - got) * mb_w;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        int j = 4 * lane + k;
+        if (j >= got && j < got + take) out[k] = unpack_u64(p, len, bit0 + (int64_t)j * mb_w, mb_w) + (uint64_t)min_delta;
+      }
+      mb_vi += take;
+      position += take;
+      got += take;
+    }
     return E_OK;
   }
 

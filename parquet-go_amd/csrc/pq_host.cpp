@@ -43,6 +43,9 @@ struct pq_launch_args {
   const int32_t *list;
   int32_t nlist;
   int32_t ncols;
+  void *jobs;
+  uint32_t *njobs;
+  uint32_t max_jobs;
 };
 int pq_launch(int which, const pq_launch_args *p, hipStream_t s);
 }
@@ -500,6 +503,9 @@ struct pqg_batch {
   ColDesc *d_cols = nullptr;
   uint64_t *d_dict = nullptr;
   int32_t *d_lists = nullptr;
+  void *d_jobs = nullptr;        // deferred long-literal copy jobs (k_snappy -> k_copy)
+  uint32_t *d_njobs = nullptr;
+  uint32_t max_jobs = 0;
   uint32_t *h_status = nullptr;  // pinned mirror
   std::vector<ColDesc> hcols;
   // timing: a ring of event sets, one per decode, harvested by pqg_batch_kernel_times
@@ -513,7 +519,7 @@ struct pqg_batch {
   bool decoded = false;
 };
 
-static const char *kKernelNames[] = {"k_snappy", "k_dict_prepare", "k_prepare", "k_scan", "k_decode",
+static const char *kKernelNames[] = {"k_snappy+k_copy", "k_dict_prepare", "k_prepare", "k_scan", "k_decode",
                                      "k_level_check"};
 
 #define HIPCHK(x)                                                                 \
@@ -1194,6 +1200,9 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   rc |= alloc_dev((void **)&B->d_dict, sizeof(uint64_t) * (size_t)B->dict_entries);
   size_t nl = B->snappy_list.size() + B->dict_list.size() + B->data_list.size();
   rc |= alloc_dev((void **)&B->d_lists, sizeof(int32_t) * nl);
+  B->max_jobs = B->snappy_list.empty() ? 0u : (uint32_t)(B->staged_bytes / 65536 + 64);
+  rc |= alloc_dev(&B->d_jobs, 32 * (size_t)B->max_jobs);
+  rc |= alloc_dev((void **)&B->d_njobs, 16);
   if (rc) {
     pqg_batch_destroy(B);
     return PQG_ERR_DEVICE;
@@ -1344,6 +1353,10 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.cols = B->d_cols;
   a.dict_ent = B->d_dict;
   a.ncols = (int32_t)B->cols.size();
+  a.jobs = B->d_jobs;
+  a.njobs = B->d_njobs;
+  a.max_jobs = B->max_jobs;
+  if (B->max_jobs) HIPCHK(hipMemsetAsync(B->d_njobs, 0, 16, s));
   const int32_t ns = (int32_t)B->snappy_list.size(), nd = (int32_t)B->dict_list.size(),
                 ndata = (int32_t)B->data_list.size();
   int e = 0;
@@ -1356,6 +1369,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.list = B->d_lists;
   a.nlist = ns;
   e |= pq_launch(0, &a, s);
+  e |= pq_launch(6, &a, s);  // k_copy: long literals, timed together with k_snappy
   mark();
   a.list = B->d_lists + ns;
   a.nlist = nd;
@@ -1567,6 +1581,8 @@ void pqg_batch_destroy(pqg_batch *B) {
   hipFree(B->d_cols);
   hipFree(B->d_dict);
   hipFree(B->d_lists);
+  hipFree(B->d_jobs);
+  hipFree(B->d_njobs);
   if (B->h_status) hipHostFree(B->h_status);
   for (int k = 0; k < pqg_batch::kRing; k++)
     for (int i = 0; i < 8; i++)
@@ -1590,6 +1606,11 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
   rc |= alloc_dev((void **)&d_page, sizeof(PageDesc));
   rc |= alloc_dev((void **)&d_st, sizeof(uint32_t));
   rc |= alloc_dev((void **)&d_list, sizeof(int32_t));
+  void *d_jobs = nullptr;
+  uint32_t *d_njobs = nullptr;
+  const uint32_t max_jobs = (uint32_t)(expect / 65536 + 8);
+  rc |= alloc_dev(&d_jobs, 32 * (size_t)max_jobs);
+  rc |= alloc_dev((void **)&d_njobs, 16);
   if (!rc) {
     PageDesc d;
     memset(&d, 0, sizeof(d));
@@ -1611,7 +1632,12 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
     a.status = d_st;
     a.list = d_list;
     a.nlist = 1;
+    a.jobs = d_jobs;
+    a.njobs = d_njobs;
+    a.max_jobs = max_jobs;
+    hipMemsetAsync(d_njobs, 0, 16, s);
     rc = pq_launch(0, &a, s);
+    rc |= pq_launch(6, &a, s);
     hipStreamSynchronize(s);
     hipMemcpy(&st, d_st, 4, hipMemcpyDeviceToHost);
     *code = st == STATUS_OK ? 0 : (int)(st & 0xffff);
@@ -1622,6 +1648,8 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
   hipFree(d_page);
   hipFree(d_st);
   hipFree(d_list);
+  hipFree(d_jobs);
+  hipFree(d_njobs);
   if (rc) {
     set_err("device snappy failed");
     return PQG_ERR_DEVICE;

@@ -21,6 +21,12 @@
 
 namespace pq {
 
+struct CopyJob {  // dst[0, len) = src[0, len), both in device memory
+  const uint8_t *src;
+  uint8_t *dst;
+  int64_t len;
+};
+
 struct KArgs {
   const uint8_t *in;      // input buffer: every selected column chunk's bytes
   uint8_t *stage;         // staging: uncompressed values sections
@@ -32,6 +38,9 @@ struct KArgs {
   const int32_t *list;    // page indices handled by this launch
   int32_t nlist;
   int32_t ncols;
+  CopyJob *jobs;          // long Snappy literals deferred to k_copy
+  uint32_t *njobs;
+  uint32_t max_jobs;
 };
 
 __device__ __forceinline__ void set_status(uint32_t *status, int page, uint32_t stage, uint32_t code) {
@@ -52,8 +61,96 @@ constexpr int RING = 8192;  // per-wave LDS history (bytes)
 constexpr int RING_MASK = RING - 1;
 constexpr int SNAPPY_WAVES = 4;
 
+// Literal run: dst[dpos, dpos+len) = s[0, len).  The staging page base is
+// 16-byte aligned, so after a <16-byte head every lane stores whole 16-byte
+// chunks (1 KiB per wave instruction); the source is read as aligned dwords
+// and funnel-shifted (v_alignbyte) by the uniform source/destination skew.
+// Only the last RING bytes also enter the LDS history.
+__device__ __forceinline__ void copy_literal(const uint8_t *s, uint8_t *dst, int64_t dpos, int64_t len, uint8_t *ring,
+                                             int lane) {
+  uint8_t *D = dst + dpos;
+  const int64_t ring_from = dpos + len - RING;  // page offsets >= ring_from go to the history
+  int64_t head = (int64_t)((16 - ((uintptr_t)D & 15)) & 15);
+  if (head > len) head = len;
+  if (lane < head) {
+    uint8_t b = s[lane];
+    D[lane] = b;
+    if (dpos + lane >= ring_from) ring[(dpos + lane) & RING_MASK] = b;
+  }
+  const int64_t body = (len - head) >> 4;
+  const uint8_t *S = s + head;
+  uint8_t *D16 = D + head;
+  const int64_t q0 = dpos + head;  // page offset of the first 16-byte chunk (multiple of 16)
+  const uint32_t skew = (uint32_t)((uintptr_t)S & 3);
+  const uint32_t *SA = (const uint32_t *)((uintptr_t)S & ~(uintptr_t)3);
+  for (int64_t c = lane; c < body; c += 128) {
+    int64_t c2 = c + 64;
+    uint4 a = *(const uint4 *)(SA + 4 * c);
+    uint32_t a4 = SA[4 * c + 4];
+    uint4 b = make_uint4(0, 0, 0, 0);
+    uint32_t b4 = 0;
+    if (c2 < body) {
+      b = *(const uint4 *)(SA + 4 * c2);
+      b4 = SA[4 * c2 + 4];
+    }
+    uint4 o;
+    o.x = __builtin_amdgcn_alignbyte(a.y, a.x, skew);
+    o.y = __builtin_amdgcn_alignbyte(a.z, a.y, skew);
+    o.z = __builtin_amdgcn_alignbyte(a.w, a.z, skew);
+    o.w = __builtin_amdgcn_alignbyte(a4, a.w, skew);
+    *(uint4 *)(D16 + 16 * c) = o;
+    if (q0 + 16 * c + 16 > ring_from) *(uint4 *)(ring + ((q0 + 16 * c) & RING_MASK)) = o;
+    if (c2 < body) {
+      uint4 p;
+      p.x = __builtin_amdgcn_alignbyte(b.y, b.x, skew);
+      p.y = __builtin_amdgcn_alignbyte(b.z, b.y, skew);
+      p.z = __builtin_amdgcn_alignbyte(b.w, b.z, skew);
+      p.w = __builtin_amdgcn_alignbyte(b4, b.w, skew);
+      *(uint4 *)(D16 + 16 * c2) = p;
+      if (q0 + 16 * c2 + 16 > ring_from) *(uint4 *)(ring + ((q0 + 16 * c2) & RING_MASK)) = p;
+    }
+  }
+  const int64_t done = head + body * 16;
+  const int64_t tail = len - done;
+  if (lane < tail) {
+    uint8_t b = s[done + lane];
+    D[done + lane] = b;
+    ring[(dpos + done + lane) & RING_MASK] = b;
+  }
+}
+
+// Put the last min(len, RING) bytes of a deferred literal into the history
+// (16-byte LDS stores from funnel-shifted dword loads; done lazily, only when
+// a copy token follows the literal).
+__device__ __forceinline__ void ring_fill(const uint8_t *s, int64_t dpos, int64_t len, uint8_t *ring, int lane) {
+  const int64_t from = len > RING ? len - RING : 0;     // literal offset of the first history byte
+  const int64_t q_end = dpos + len;
+  int64_t q0 = (dpos + from + 15) & ~(int64_t)15;        // first 16-byte aligned page offset
+  // unaligned head bytes
+  if (lane < q0 - (dpos + from) && dpos + from + lane < q_end) ring[(dpos + from + lane) & RING_MASK] = s[from + lane];
+  const int64_t nchunks = (q_end - q0) >> 4;
+  for (int64_t c = lane; c < nchunks; c += 64) {
+    const uint8_t *sp = s + (q0 + 16 * c - dpos);
+    const uint32_t skew = (uint32_t)((uintptr_t)sp & 3);
+    const uint32_t *sa = (const uint32_t *)((uintptr_t)sp & ~(uintptr_t)3);
+    uint4 x = *(const uint4 *)sa;
+    uint32_t x4 = sa[4];
+    uint4 o;
+    o.x = __builtin_amdgcn_alignbyte(x.y, x.x, skew);
+    o.y = __builtin_amdgcn_alignbyte(x.z, x.y, skew);
+    o.z = __builtin_amdgcn_alignbyte(x.w, x.z, skew);
+    o.w = __builtin_amdgcn_alignbyte(x4, x.w, skew);
+    *(uint4 *)(ring + ((q0 + 16 * c) & RING_MASK)) = o;
+  }
+  const int64_t t0 = q0 + nchunks * 16;
+  if (t0 + lane < q_end) ring[(t0 + lane) & RING_MASK] = s[t0 + lane - dpos];
+}
+
+constexpr int64_t BIG_LITERAL = 64 * 1024;  // longer literals are copied by k_copy (many workgroups)
+constexpr int MAX_DEFER = 64;  // one entry per lane
+
 __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
-  __shared__ uint8_t ring_all[SNAPPY_WAVES][RING];
+  __shared__ __attribute__((aligned(16))) uint8_t ring_all[SNAPPY_WAVES][RING];
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
   const int gi = blockIdx.x * SNAPPY_WAVES + wv;
@@ -100,6 +197,11 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
   const int64_t dl = (int64_t)dlen;
   int64_t dpos = 0;
   uint32_t err = E_OK;
+  int ndefer = 0;                      // deferred literals: lane k holds entry k
+  const uint8_t *pend_src = nullptr;   // last deferred literal whose tail is not yet in the history
+  int64_t pend_dpos = 0, pend_len = 0;
+  int64_t def_dst = 0, def_len = 0;
+  uint64_t def_src = 0;
   while (s < slen) {
     uint32_t tag = W.byte_at(src + s);
     int64_t length, offset;
@@ -123,17 +225,32 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
         break;
       }
       if (write) {
-        const int64_t ring_from = length - RING;  // only the tail needs to enter the history
-        for (int64_t k = 0; k < length; k += 256) {
-#pragma unroll
-          for (int j = 0; j < 4; j++) {
-            int64_t idx = k + j * 64 + lane;
-            if (idx < length) {
-              uint8_t b = src[s + idx];
-              dst[dpos + idx] = b;
-              if (idx >= ring_from) ring[(dpos + idx) & RING_MASK] = b;
+        bool deferred = false;
+        if (length >= BIG_LITERAL && ndefer < MAX_DEFER && a.max_jobs > 0) {
+          uint32_t slot = 0;
+          if (lane == 0) slot = atomicAdd(a.njobs, 1u);
+          slot = ufirst(slot);
+          if (slot < a.max_jobs) {
+            if (lane == 0) a.jobs[slot] = CopyJob{src + s, dst + dpos, length};
+            // remember it: far copies that land inside read the literal from the payload
+            if (lane == ndefer) {
+              def_dst = dpos;
+              def_len = length;
+              def_src = (uint64_t)(uintptr_t)(src + s);
             }
+            ndefer++;
+            pend_src = src + s;  // history filled lazily, if a copy follows
+            pend_dpos = dpos;
+            pend_len = length;
+            deferred = true;
           }
+        }
+        if (!deferred) {
+          if (pend_len) {  // history must hold the deferred literal's tail before newer bytes land
+            ring_fill(pend_src, pend_dpos, pend_len, ring, lane);
+            pend_len = 0;
+          }
+          copy_literal(src + s, dst, dpos, length, ring, lane);
         }
       }
       dpos += length;
@@ -171,6 +288,10 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
       break;
     }
     if (write) {
+      if (pend_len) {
+        ring_fill(pend_src, pend_dpos, pend_len, ring, lane);
+        pend_len = 0;
+      }
       // forward, possibly self-overlapping copy of <= 64 bytes
       uint8_t b = 0;
       bool act = lane < length;
@@ -180,10 +301,20 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
       } else {
         // far copy: make this wave's earlier stores visible, read through L2
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        const uint8_t *lit = nullptr;  // inside a deferred literal: read the payload instead
+        for (int k = 0; k < ndefer; k++) {
+          int64_t kd = (int64_t)shfl64((uint64_t)def_dst, k), kl = (int64_t)shfl64((uint64_t)def_len, k);
+          uint64_t ks = shfl64(def_src, k);
+          if (from >= kd && from < kd + kl) lit = (const uint8_t *)(uintptr_t)ks + (from - kd);
+        }
         if (act) {
-          const uint32_t *wp = (const uint32_t *)((uintptr_t)(dst + from) & ~(uintptr_t)3);
-          uint32_t word = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          b = (uint8_t)(word >> (((uintptr_t)(dst + from) & 3) * 8));
+          if (lit) {
+            b = *lit;
+          } else {
+            const uint32_t *wp = (const uint32_t *)((uintptr_t)(dst + from) & ~(uintptr_t)3);
+            uint32_t word = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            b = (uint8_t)(word >> (((uintptr_t)(dst + from) & 3) * 8));
+          }
         }
       }
       if (act) {
@@ -196,6 +327,46 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
   if (err == E_OK && dpos != dl) err = E_SNAPPY;
   if (err == E_OK && !write) err = E_SIZE;  // compress.go:117-119
   if (err) set_status(a.status, page, ST_DECOMPRESS, err);
+}
+
+// ===========================================================================
+// K1b: long literals deferred by k_snappy, copied by every workgroup
+// ===========================================================================
+constexpr int COPY_TILE = 4096;  // bytes per workgroup step (256 lanes x 16 B)
+
+__global__ __launch_bounds__(256) void k_copy(KArgs a) {
+  // one workgroup per job (google/Go snappy literals are <= 64 KB; longer ones loop)
+  const uint32_t j = blockIdx.x;
+  if (j >= min(*a.njobs, a.max_jobs)) return;
+  const CopyJob job = a.jobs[j];
+  const int t = threadIdx.x;
+  const uintptr_t d0 = (uintptr_t)job.dst, d1 = d0 + (uintptr_t)job.len;
+  const uintptr_t A = d0 & ~(uintptr_t)15;
+  for (uintptr_t base = A; base < d1; base += 4 * COPY_TILE) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      uintptr_t u = base + (uintptr_t)k * COPY_TILE + (uintptr_t)t * 16;
+      if (u >= d1) continue;
+      if (u >= d0 && u + 16 <= d1) {
+        const uint8_t *s = job.src + (u - d0);
+        const uint32_t skew = (uint32_t)((uintptr_t)s & 3);
+        const uint32_t *sa = (const uint32_t *)((uintptr_t)s & ~(uintptr_t)3);
+        uint4 x = *(const uint4 *)sa;
+        uint32_t x4 = sa[4];
+        uint4 o;
+        o.x = __builtin_amdgcn_alignbyte(x.y, x.x, skew);
+        o.y = __builtin_amdgcn_alignbyte(x.z, x.y, skew);
+        o.z = __builtin_amdgcn_alignbyte(x.w, x.z, skew);
+        o.w = __builtin_amdgcn_alignbyte(x4, x.w, skew);
+        *(uint4 *)u = o;
+      } else {
+        for (int b = 0; b < 16; b++) {
+          uintptr_t x = u + b;
+          if (x >= d0 && x < d1) *(uint8_t *)x = job.src[x - d0];
+        }
+      }
+    }
+  }
 }
 
 // ===========================================================================
@@ -541,6 +712,23 @@ __device__ __forceinline__ void or_bits(uint32_t *bm, int64_t bit0, uint64_t bit
   if (hi) atomicOr(&bm[w + 2], hi);
 }
 
+// gather element j (0..255, four per lane) of a 4-per-lane vector
+__device__ __forceinline__ uint32_t pick4(const uint32_t (&v)[4], int j) {
+  uint32_t x0 = shfl32(v[0], j >> 2), x1 = shfl32(v[1], j >> 2), x2 = shfl32(v[2], j >> 2), x3 = shfl32(v[3], j >> 2);
+  int k = j & 3;
+  return k == 0 ? x0 : k == 1 ? x1 : k == 2 ? x2 : x3;
+}
+__device__ __forceinline__ uint64_t pick4_64(const uint64_t (&v)[4], int j) {
+  uint32_t lo[4] = {(uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]};
+  uint32_t hi[4] = {(uint32_t)(v[0] >> 32), (uint32_t)(v[1] >> 32), (uint32_t)(v[2] >> 32), (uint32_t)(v[3] >> 32)};
+  return ((uint64_t)pick4(hi, j) << 32) | pick4(lo, j);
+}
+
+// Decode one data page with one wavefront, 256 level entries per step, four
+// consecutive entries per lane (page_v1.go:27-55 readValues + data_store.go
+// semantics for validity / list offsets).  For flat columns the steps are
+// aligned to 256 output slots so each lane owns a 16-byte-aligned slice of
+// the values and whole validity words.
 __global__ __launch_bounds__(256) void k_decode(KArgs a) {
   const int gi = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (gi >= a.nlist) return;
@@ -555,8 +743,7 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
   if (n == 0) return;
 
   const uint8_t *lvl = d.kind == PAGE_V1 ? body_ptr(a, d) : a.in + d.src;
-  const uint8_t *body = body_ptr(a, d);
-  const uint8_t *vals = body + pi.val_off;
+  const uint8_t *vals = body_ptr(a, d) + pi.val_off;
   const int64_t vlen = pi.val_len;
   const int w = c.width;
   const bool flat = c.max_rep == 0;
@@ -566,12 +753,12 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
   rep.init(lvl + pi.rep_off, pi.rep_len, bits_len(c.max_rep));
   def.init(lvl + pi.def_off, pi.def_len, bits_len(c.max_def));
 
-  // value decoders
   Hyb keys;
   Delta dz;
   const PageDesc *dp = d.dict >= 0 ? &a.pages[d.dict] : nullptr;
   const uint8_t *dict_vals = nullptr;
   int64_t dict_n = 0, dict_base = 0;
+  uint64_t delta_prev = 0;
   if (d.enc == ENC_RLE_DICT) {
     keys.init(vals + 1, vlen - 1, pi.idx_bw);
     if (dp) {
@@ -581,8 +768,8 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
     }
   } else if (d.enc == ENC_DELTA_BP) {
     dz.init(vals, vlen, c.ptype == T_INT32);
+    delta_prev = (uint64_t)dz.first;
   }
-  uint64_t delta_prev = (uint64_t)dz.first;
   Win SW;  // string-length window (PLAIN BYTE_ARRAY)
   SW.reset();
   int64_t spos = 0;
@@ -592,54 +779,67 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
   uint32_t err = E_OK, err_stage = 0;
 
   while (e0 < n) {
-    // first chunk of a flat page ends on a 64-slot boundary so that later
-    // chunks own whole 64-bit validity words
-    int cnt = (int)min<int64_t>(n - e0, flat ? 64 - ((slot_base + e0) & 63) : 64);
-    const bool act = lane < cnt;
-    uint32_t r = 0, dl = 0;
+    const int cnt = (int)min<int64_t>(n - e0, flat ? 256 - ((slot_base + e0) & 255) : 256);
+    uint32_t r[4] = {0, 0, 0, 0}, dl[4] = {0, 0, 0, 0};
     if (c.max_rep > 0) {
-      err = rep.next(cnt, r);
+      err = rep.next4(cnt, r);
       if (err) {
         err_stage = ST_REP;
         break;
       }
     }
     if (c.max_def > 0) {
-      err = def.next(cnt, dl);
+      err = def.next4(cnt, dl);
       if (err) {
         err_stage = ST_DEF;
         break;
       }
     }
-    const bool valid = act && (int)dl == c.max_def;
-    const bool slot = act && (flat || (int)dl >= c.rep_def);
-    const uint64_t vmask = ballot(valid);
-    const uint64_t smask = ballot(slot);
-    const int m = __popcll(vmask);
-    const int vr = rank_in(vmask);   // dense rank among valid lanes
-    const int sr = rank_in(smask);   // rank among slot lanes
-    const int64_t myslot = slot_base + slot_run + sr;
+    bool act[4], valid[4], slot[4];
+    int nv = 0, ns = 0, nr = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      act[k] = 4 * lane + k < cnt;
+      valid[k] = act[k] && (int)dl[k] == c.max_def;
+      slot[k] = act[k] && (flat || (int)dl[k] >= c.rep_def);
+      nv += valid[k];
+      ns += slot[k];
+      nr += act[k] && r[k] == 0;
+    }
+    int32_t m, mslots, mrows;
+    const int32_t vbase = wave_excl_scan32(nv, &m);       // dense rank of my first valid entry
+    const int32_t sbase = flat ? 4 * lane : wave_excl_scan32(ns, &mslots);
+    if (flat) mslots = cnt;
+    const bool dense = m == cnt;  // no nulls in this step: entry j is dense value j
 
     if (c.flags & COL_EMIT_LEVELS) {
-      if (act) {
-        c.def_out[d.level_base + e0 + lane] = (uint8_t)dl;
-        c.rep_out[d.level_base + e0 + lane] = (uint8_t)r;
-      }
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (act[k]) {
+          c.def_out[d.level_base + e0 + 4 * lane + k] = (uint8_t)dl[k];
+          c.rep_out[d.level_base + e0 + 4 * lane + k] = (uint8_t)r[k];
+        }
     }
-    if (!flat) {  // list rows start where rep == 0 (data_store.go:188-202)
-      const uint64_t rmask = ballot(act && r == 0);
-      if (act && r == 0) {
-        int64_t row = pi.row_base + row_run + rank_in(rmask);
-        c.list_offsets[row] = (int32_t)myslot;
-        if ((int)dl >= c.rep_def - 1) atomicOr(&c.list_validity[row >> 5], 1u << (row & 31));
+    if (!flat) {  // rows start where rep == 0 (data_store.go:188-202)
+      const int32_t rbase = wave_excl_scan32(nr, &mrows);
+      int ri = 0, si = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        if (act[k] && r[k] == 0) {
+          int64_t row = pi.row_base + row_run + rbase + ri;
+          c.list_offsets[row] = (int32_t)(slot_base + slot_run + sbase + si);
+          if ((int)dl[k] >= c.rep_def - 1) atomicOr(&c.list_validity[row >> 5], 1u << (row & 31));
+          ri++;
+        }
+        si += slot[k];
       }
-      row_run += __popcll(rmask);
+      row_run += mrows;
     }
 
-    // ---- values for the m valid lanes (dense index nn_run + vr) ----
-    uint64_t v = 0;
-    const uint8_t *vsrc = nullptr;  // for widths other than 4 / 8
-    int64_t slen_mine = 0, soff_mine = 0;
+    // ---- the m dense values of this step, in dense order (value j: lane j>>2, element j&3) ----
+    uint64_t v[4] = {0, 0, 0, 0};
+    int64_t soff[4] = {0, 0, 0, 0}, slen[4] = {0, 0, 0, 0};
+    const uint8_t *sbase_ptr = nullptr;
     if (m > 0) {
       if (d.enc == ENC_PLAIN && !is_ba) {
         if ((nn_run + m) * (int64_t)w > vlen) {
@@ -647,61 +847,98 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
           err_stage = ST_VALUES;
           break;
         }
-        if (valid) {
-          const uint8_t *vp = vals + (nn_run + vr) * (int64_t)w;
-          if (w == 4) v = load_u32_unaligned(vp);
-          else if (w == 8) v = load_u64_unaligned(vp);
-          else vsrc = vp;
+        if (w == 4 || w == 8) {
+          int vi = 0;
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+            if (valid[k]) {
+              const uint8_t *vp = vals + (nn_run + vbase + vi) * (int64_t)w;
+              v[k] = w == 4 ? (uint64_t)load_u32_unaligned(vp) : load_u64_unaligned(vp);
+              vi++;
+            }
         }
       } else if (d.enc == ENC_RLE_DICT) {
-        uint32_t k;
-        err = keys.next(m, k);
-        if (err) {
-          err_stage = ST_VALUES;
-          break;
-        }
-        uint32_t key = shfl32(k, valid ? vr : 0);
         if (!dp) {
           err = E_DICT;
           err_stage = ST_VALUES;
           break;
         }
-        if (ballot(valid && (int64_t)key >= dict_n)) {
-          err = E_DICT;
-          err_stage = ST_VALUES;
-          break;
-        }
-        if (valid) {
-          if (is_ba) {
-            uint64_t ent = a.dict_ent[dict_base + key];
-            soff_mine = (int64_t)(ent >> 32);
-            slen_mine = (int64_t)(ent & 0xffffffffu);
-            vsrc = dict_vals;
-          } else {
-            const uint8_t *vp = dict_vals + (int64_t)key * w;
-            if (w == 4) v = load_u32_unaligned(vp);
-            else if (w == 8) v = load_u64_unaligned(vp);
-            else vsrc = vp;
-          }
-        }
-      } else if (d.enc == ENC_DELTA_BP) {
-        uint64_t dv;
-        err = dz.next(m, dv);
+        uint32_t kk[4];
+        err = keys.next4(m, kk);
         if (err) {
           err_stage = ST_VALUES;
           break;
         }
-        if (lane >= m) dv = 0;
-        uint64_t incl = wave_incl_scan_u64(dv);
-        uint64_t excl = incl - dv;
-        uint64_t val = delta_prev + excl;
-        uint64_t tot = shfl64(incl, 63);
-        v = shfl64(val, valid ? vr : 0);
-        delta_prev += tot;
-        if (c.ptype == T_INT32) v &= 0xffffffffull;
+        uint32_t key[4];
+        if (dense) {
+#pragma unroll
+          for (int k = 0; k < 4; k++) key[k] = kk[k];
+        } else {
+          int vi = 0;
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            key[k] = pick4(kk, valid[k] ? vbase + vi : 0);
+            vi += valid[k];
+          }
+        }
+        bool bad = false;
+#pragma unroll
+        for (int k = 0; k < 4; k++) bad |= valid[k] && (int64_t)key[k] >= dict_n;
+        if (ballot(bad)) {
+          err = E_DICT;
+          err_stage = ST_VALUES;
+          break;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if (valid[k]) {
+            if (is_ba) {
+              uint64_t ent = a.dict_ent[dict_base + key[k]];
+              soff[k] = (int64_t)(ent >> 32);
+              slen[k] = (int64_t)(ent & 0xffffffffu);
+            } else if (w == 4) {
+              v[k] = load_u32_unaligned(dict_vals + (int64_t)key[k] * 4);
+            } else if (w == 8) {
+              v[k] = load_u64_unaligned(dict_vals + (int64_t)key[k] * 8);
+            } else {
+              soff[k] = (int64_t)key[k] * w;
+            }
+          }
+        sbase_ptr = dict_vals;
+      } else if (d.enc == ENC_DELTA_BP) {
+        uint64_t dv[4];
+        err = dz.next4(m, dv);
+        if (err) {
+          err_stage = ST_VALUES;
+          break;
+        }
+        // v[j] = prev + sum of the deltas before j (wrapping, deltabp_decoder.go:327-333)
+        uint64_t loc = dv[0] + dv[1] + dv[2] + dv[3];
+        uint64_t incl = wave_incl_scan_u64(loc);
+        uint64_t base = delta_prev + (incl - loc);
+        uint64_t val[4];
+        val[0] = base;
+        val[1] = base + dv[0];
+        val[2] = val[1] + dv[1];
+        val[3] = val[2] + dv[2];
+        delta_prev += shfl64(incl, 63);
+        if (dense) {
+#pragma unroll
+          for (int k = 0; k < 4; k++) v[k] = val[k];
+        } else {
+          int vi = 0;
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            v[k] = pick4_64(val, valid[k] ? vbase + vi : 0);
+            vi += valid[k];
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if (c.ptype == T_INT32) v[k] &= 0xffffffffull;
       } else if (d.enc == ENC_PLAIN && is_ba) {
-        // serial length walk (type_bytearray.go:24-45)
-        uint64_t ent = 0;
+        // serial length walk (type_bytearray.go:24-45); value j -> lane j>>2, element j&3
+        uint32_t eo[4] = {0, 0, 0, 0}, el[4] = {0, 0, 0, 0};
         for (int j = 0; j < m; j++) {
           if (spos + 4 > vlen) {
             err = E_EOF;
@@ -716,19 +953,31 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
             err = E_EOF;
             break;
           }
-          if (lane == j) ent = ((uint64_t)(spos + 4) << 32) | (uint32_t)l;
+          if (lane == (j >> 2)) {
+            int k = j & 3;
+            if (k == 0) { eo[0] = (uint32_t)(spos + 4); el[0] = (uint32_t)l; }
+            else if (k == 1) { eo[1] = (uint32_t)(spos + 4); el[1] = (uint32_t)l; }
+            else if (k == 2) { eo[2] = (uint32_t)(spos + 4); el[2] = (uint32_t)l; }
+            else { eo[3] = (uint32_t)(spos + 4); el[3] = (uint32_t)l; }
+          }
           spos += 4 + l;
         }
         if (err) {
           err_stage = ST_VALUES;
           break;
         }
-        ent = shfl64(ent, valid ? vr : 0);
-        if (valid) {
-          soff_mine = (int64_t)(ent >> 32);
-          slen_mine = (int64_t)(ent & 0xffffffffu);
-          vsrc = vals;
+        int vi = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          int j = valid[k] ? vbase + vi : 0;
+          uint32_t o = dense ? eo[k] : pick4(eo, j), l = dense ? el[k] : pick4(el, j);
+          if (valid[k]) {
+            soff[k] = o;
+            slen[k] = l;
+          }
+          vi += valid[k];
         }
+        sbase_ptr = vals;
       } else {
         err = E_UNSUPPORTED;
         err_stage = ST_VALUES;
@@ -736,42 +985,114 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
       }
     }
 
+    // ---- outputs ----
     if (is_ba) {
-      // offsets over slots (nulls have zero length), then byte copies
-      int64_t l = valid ? slen_mine : 0;
-      int64_t incl = wave_incl_scan64(slot ? l : 0);
-      int64_t start = str_run + incl - l;
-      if (slot) c.str_offsets[myslot + 1] = str_run + incl;
-      if (valid) {
-        const uint8_t *sp = vsrc + soff_mine;
-        uint8_t *op = c.values + start;
-        for (int64_t k = 0; k < l; k++) op[k] = sp[k];
+      int64_t ll[4], tot = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        ll[k] = valid[k] ? slen[k] : 0;
+        tot += ll[k];
+      }
+      int64_t incl = wave_incl_scan64(tot);
+      int64_t start = str_run + incl - tot;
+      int si = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        if (slot[k]) {
+          start += ll[k];
+          c.str_offsets[slot_base + slot_run + sbase + si + 1] = start;
+          if (valid[k]) {
+            const uint8_t *sp = sbase_ptr + soff[k];
+            uint8_t *op = c.values + start - ll[k];
+            for (int64_t b = 0; b < ll[k]; b++) op[b] = sp[b];
+          }
+          si++;
+        }
       }
       str_run += (int64_t)shfl64((uint64_t)incl, 63);
+    } else if (flat && (w == 4 || w == 8)) {
+      const int64_t s0 = slot_base + slot_run + 4 * lane;  // my four slots
+      uint64_t o[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) o[k] = valid[k] ? v[k] : 0;
+      if (act[3] && (s0 & 3) == 0) {
+        if (w == 4) {
+          *(uint4 *)(c.values + s0 * 4) = make_uint4((uint32_t)o[0], (uint32_t)o[1], (uint32_t)o[2], (uint32_t)o[3]);
+        } else {
+          *(uint4 *)(c.values + s0 * 8) = make_uint4((uint32_t)o[0], (uint32_t)(o[0] >> 32), (uint32_t)o[1], (uint32_t)(o[1] >> 32));
+          *(uint4 *)(c.values + s0 * 8 + 16) = make_uint4((uint32_t)o[2], (uint32_t)(o[2] >> 32), (uint32_t)o[3], (uint32_t)(o[3] >> 32));
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if (act[k]) {
+            if (w == 4) *(uint32_t *)(c.values + (s0 + k) * 4) = (uint32_t)o[k];
+            else *(uint64_t *)(c.values + (s0 + k) * 8) = o[k];
+          }
+      }
     } else {
-      if (slot) {
-        if (w == 4 || w == 8) store_value(c.values, myslot, w, valid ? v : 0, nullptr);
-        else store_value(c.values, myslot, w, 0, valid ? vsrc : nullptr);
+      int si = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        if (slot[k]) {
+          int64_t sl = slot_base + slot_run + sbase + si;
+          if (w == 4) *(uint32_t *)(c.values + sl * 4) = valid[k] ? (uint32_t)v[k] : 0u;
+          else if (w == 8) *(uint64_t *)(c.values + sl * 8) = valid[k] ? v[k] : 0ull;
+          else {
+            uint8_t *op = c.values + sl * (int64_t)w;
+            const uint8_t *sp = d.enc == ENC_PLAIN ? vals + (nn_run + vbase) * (int64_t)w : sbase_ptr + soff[k];
+            if (valid[k] && d.enc == ENC_PLAIN) {
+              int vi = 0;
+              for (int q = 0; q < k; q++) vi += valid[q];
+              sp = vals + (nn_run + vbase + vi) * (int64_t)w;
+            }
+            for (int b = 0; b < w; b++) op[b] = valid[k] ? sp[b] : 0;
+          }
+          si++;
+        }
       }
     }
     if (c.max_def > 0) {
       if (flat) {
-        or_bits(c.validity, slot_base + slot_run, vmask, cnt, true);
-      } else if (valid) {
-        atomicOr(&c.validity[myslot >> 5], 1u << (myslot & 31));
+        // 4 bits per lane -> 32-bit words owned by lanes 8q (this step covers 256 aligned slots
+        // except a page's first/last step, which share words with neighbouring pages)
+        uint32_t nib = (valid[0] ? 1u : 0u) | (valid[1] ? 2u : 0u) | (valid[2] ? 4u : 0u) | (valid[3] ? 8u : 0u);
+        uint32_t word = nib << (4 * (lane & 7));
+        word |= __shfl_xor(word, 1);
+        word |= __shfl_xor(word, 2);
+        word |= __shfl_xor(word, 4);
+        const int64_t sbit = slot_base + slot_run;  // first slot of this step
+        if ((lane & 7) == 0 && 4 * lane < cnt) {
+          const int64_t b0 = sbit + 4 * lane;  // first bit of my word
+          const bool whole = (b0 & 31) == 0 && 4 * lane + 32 <= cnt;
+          if (whole) c.validity[b0 >> 5] = word;
+          else {
+            int sh = (int)(b0 & 31);
+            uint64_t wv = (uint64_t)word << sh;
+            if ((uint32_t)wv) atomicOr(&c.validity[b0 >> 5], (uint32_t)wv);
+            if ((uint32_t)(wv >> 32)) atomicOr(&c.validity[(b0 >> 5) + 1], (uint32_t)(wv >> 32));
+          }
+        }
+      } else {
+        int si = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          if (slot[k]) {
+            int64_t sl = slot_base + slot_run + sbase + si;
+            if (valid[k]) atomicOr(&c.validity[sl >> 5], 1u << (sl & 31));
+            si++;
+          }
+        }
       }
     }
-    slot_run += __popcll(smask);
+    slot_run += mslots;
     nn_run += m;
     e0 += cnt;
   }
-
   // a later-found level error can outrank this one: k_level_check re-walks
   // the earlier level streams (the reference decodes all rep levels, then all
   // def levels, then the values, page_v1.go:37-52)
-  if (err) {
-    set_status(a.status, page, err_stage, err);
-  }
+  if (err) set_status(a.status, page, err_stage, err);
 }
 
 // level-error precedence pass: for pages that failed in k_decode at the
@@ -832,6 +1153,9 @@ struct pq_launch_args {
   const int32_t *list;
   int32_t nlist;
   int32_t ncols;
+  void *jobs;
+  uint32_t *njobs;
+  uint32_t max_jobs;
 };
 
 static pq::KArgs to_k(const pq_launch_args *p) {
@@ -846,6 +1170,9 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   k.list = p->list;
   k.nlist = p->nlist;
   k.ncols = p->ncols;
+  k.jobs = (pq::CopyJob *)p->jobs;
+  k.njobs = p->njobs;
+  k.max_jobs = p->max_jobs;
   return k;
 }
 
@@ -854,6 +1181,11 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
   if (which == 4) {
     if (k.ncols <= 0) return 0;
     hipLaunchKernelGGL(pq::k_scan, dim3(k.ncols), dim3(256), 0, s, k);
+    return hipGetLastError() == hipSuccess ? 0 : 17;
+  }
+  if (which == 6) {  // deferred literal copies: fixed grid, the job count lives on the device
+    if (k.max_jobs == 0) return 0;
+    hipLaunchKernelGGL(pq::k_copy, dim3(k.max_jobs), dim3(256), 0, s, k);
     return hipGetLastError() == hipSuccess ? 0 : 17;
   }
   if (k.nlist <= 0) return 0;

@@ -123,6 +123,31 @@ def test_snappy_block_roundtrip():
                 data = np.round(rng.standard_normal(n // 8 + 1), 2).tobytes()[:n]
             comp = pa.compress(data, codec="snappy", asbytes=True)
             assert pqgpu.DecompressBlock(pqgpu.CompressionCodec_SNAPPY, comp, n) == data, (n, kind)
+    # a literal long enough to be deferred to k_copy, then far copies that reach back
+    # into it (offset > the 8 KB LDS history), hand-assembled: google snappy never
+    # emits offsets beyond its 64 KB block, other encoders may
+    lit = rng.integers(0, 256, 70000, dtype=np.uint8).tobytes()
+    stream = bytearray()
+    total = 70000 + 40 + 64 + 5
+    v = total
+    while True:
+        b = v & 0x7f
+        v >>= 7
+        stream.append(b | (0x80 if v else 0))
+        if not v:
+            break
+    stream += bytes([62 << 2]) + (70000 - 1).to_bytes(3, "little") + lit
+    stream += bytes([((40 - 1) << 2) | 3]) + (68000).to_bytes(4, "little")   # copy4 into the literal
+    stream += bytes([((64 - 1) << 2) | 3]) + (9000).to_bytes(4, "little")    # far copy
+    stream += bytes([((5 - 1) << 2) | 2]) + (3).to_bytes(2, "little")         # overlapping near copy
+    want = bytearray(lit)
+    for off, ln in ((68000, 40), (9000, 64), (3, 5)):
+        for _ in range(ln):
+            want.append(want[len(want) - off])
+    assert len(want) == total
+    rc_o, got_o, _ = oracle.snappy_decode(bytes(stream), total)
+    assert rc_o == 0 and got_o == bytes(want)
+    assert pqgpu.DecompressBlock(pqgpu.CompressionCodec_SNAPPY, bytes(stream), total) == bytes(want)
     # far back-references (offset > the 8 KB LDS history): repeat a random 20 KB block
     blk = rng.integers(0, 256, 20000, dtype=np.uint8).tobytes()
     data = blk * 3
