@@ -29,7 +29,7 @@ sys.path.insert(0, os.path.join(ROOT, "parquet-go_amd"))
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def make_file(path, rows, rg_rows, seed=2):
+def make_file(path, rows, rg_rows, seed=2, fixed_bw=0):
     import pyarrow as pa
     import pyarrow.parquet as pq
     rng = np.random.default_rng(seed)
@@ -40,7 +40,7 @@ def make_file(path, rows, rg_rows, seed=2):
         done, i = 0, 0
         while done < rows:
             n = min(rg_rows, rows - done)
-            bw = 1 + (i % 20)
+            bw = fixed_bw if fixed_bw else 1 + (i % 20)
             K = 1 << bw
             dvals = (rng.permutation(K).astype(np.int64) * 2654435761 % (1 << 32) - (1 << 31)).astype(np.int32)
             idx = rng.integers(0, K, n)
@@ -87,6 +87,7 @@ def main():
     ap.add_argument("--file", default=None)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--bw", type=int, default=0, help="analysis: one dictionary bit width for every row group")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -105,9 +106,9 @@ def main():
 
     import pqgpu
     path = args.file or os.path.join(os.environ.get("TMPDIR", "/tmp"),
-                                     "pqgpu_bench_c2_%d_%d.parquet" % (args.rows, args.rg_rows))
+                                     "pqgpu_bench_c2_%d_%d_%d.parquet" % (args.rows, args.rg_rows, args.bw))
     if local == 0 and not os.path.exists(path):
-        make_file(path, args.rows, args.rg_rows)
+        make_file(path, args.rows, args.rg_rows, fixed_bw=args.bw)
     barrier()
 
     ctx = pqgpu.Context(local if world > 1 else 0)
@@ -148,7 +149,7 @@ def main():
     # algorithmic bytes per launch of each kernel
     alg = {
         "k_snappy+k_copy": stats["input_bytes"] + stats["staged_bytes"],     # compressed in + uncompressed out
-        "k_decode": stats["staged_bytes"] + out_b,                    # encoded indices in + decoded values out
+        "k_decode+k_decode_flat": stats["staged_bytes"] + out_b,                    # encoded indices in + decoded values out
     }
     ach = alg.get(dom, in_b + out_b) / (avg[dom] * 1e-3) / 1e9
     line = {

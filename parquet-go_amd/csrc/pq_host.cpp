@@ -46,6 +46,7 @@ struct pq_launch_args {
   void *jobs;
   uint32_t *njobs;
   uint32_t max_jobs;
+  uint64_t *dbg;
 };
 int pq_launch(int which, const pq_launch_args *p, hipStream_t s);
 }
@@ -449,6 +450,8 @@ bool codec_builtin(int codec, bool *registered) {
 struct pqg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t side[3] = {nullptr, nullptr, nullptr};  // concurrent size-class decode launches
+  hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr};
   std::string err;
 };
 
@@ -493,6 +496,9 @@ struct pqg_batch {
   std::vector<PageDesc> pages;
   std::vector<uint32_t> status0;  // host-side initial status per page
   std::vector<int32_t> snappy_list, dict_list, data_list;
+  std::vector<int32_t> general_list, flat_list;  // data pages for k_decode / k_decode_flat
+  std::vector<int32_t> dictwg_list[3];            // k_decode_dict_wg<8K / 24K / 56K>
+  bool any_count = false;
   std::vector<ChunkError> chunk_errors;
   int64_t input_bytes = 0, staged_bytes = 0, h2d_bytes = 0, host_inflated = 0, dict_entries = 0;
   // device
@@ -506,6 +512,7 @@ struct pqg_batch {
   void *d_jobs = nullptr;        // deferred long-literal copy jobs (k_snappy -> k_copy)
   uint32_t *d_njobs = nullptr;
   uint32_t max_jobs = 0;
+  uint64_t *d_dbg = nullptr;     // diagnostic stamps (PQ_STAMPS builds only)
   uint32_t *h_status = nullptr;  // pinned mirror
   std::vector<ColDesc> hcols;
   // timing: a ring of event sets, one per decode, harvested by pqg_batch_kernel_times
@@ -519,7 +526,7 @@ struct pqg_batch {
   bool decoded = false;
 };
 
-static const char *kKernelNames[] = {"k_snappy+k_copy", "k_dict_prepare", "k_prepare", "k_scan", "k_decode",
+static const char *kKernelNames[] = {"k_snappy+k_copy", "k_dict_prepare", "k_prepare", "k_scan", "k_decode+k_decode_flat",
                                      "k_level_check"};
 
 #define HIPCHK(x)                                                                 \
@@ -566,6 +573,14 @@ int pqg_ctx_create(int device, pqg_ctx **out) {
     set_err("hipStreamCreate failed");
     return PQG_ERR_DEVICE;
   }
+  for (int i = 0; i < 3; i++) {
+    if (hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming) != hipSuccess) {
+      set_err("hipStreamCreate failed");
+      return PQG_ERR_DEVICE;
+    }
+  }
+  hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
   *out = c;
   return PQG_OK;
 }
@@ -574,6 +589,11 @@ void pqg_ctx_destroy(pqg_ctx *ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
+  for (int i = 0; i < 3; i++) {
+    if (ctx->side[i]) hipStreamDestroy(ctx->side[i]);
+    if (ctx->join[i]) hipEventDestroy(ctx->join[i]);
+  }
+  if (ctx->fork) hipEventDestroy(ctx->fork);
   delete ctx;
 }
 
@@ -1187,6 +1207,49 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
     B->cols[ci].page_end = (int32_t)B->pages.size();
   }
   const size_t npages = B->pages.size();
+  // route data pages: flat required fixed-width PLAIN / RLE_DICTIONARY pages take the fast kernel
+  for (int32_t pi : B->data_list) {
+    const PageDesc &d = B->pages[(size_t)pi];
+    const ColumnPlan &cp = B->cols[(size_t)d.col];
+    const pqg_column_info &L = cp.info;
+    bool fast = L.max_rep == 0 && L.max_def == 0 && (L.value_width == 4 || L.value_width == 8) &&
+                L.physical_type != T_BYTE_ARRAY && !(cp.flags & COL_EMIT_LEVELS) &&
+                (d.enc == ENC_PLAIN || d.enc == ENC_RLE_DICT);
+    // V1 required pages have no level streams, so the key stream is body_len - 1 bytes
+    bool wg = fast && d.enc == ENC_RLE_DICT && d.kind == PAGE_V1 && d.body_len <= 56 * 1024 - 32;
+    if (wg) {
+      int cls = d.body_len <= 8 * 1024 - 32 ? 0 : d.body_len <= 24 * 1024 - 32 ? 1 : 2;
+      B->dictwg_list[cls].push_back(pi);
+    } else {
+      (fast ? B->flat_list : B->general_list).push_back(pi);
+    }
+  }
+  for (auto &cp : B->cols) B->any_count |= (cp.flags & COL_NEEDS_COUNT) != 0;
+  // XCD affinity (speed only, never correctness): workgroups b and b + 8 share an
+  // XCD's L2 under round-robin dispatch, so deal whole chunks (one dictionary
+  // each) to the 8 block residues, balanced by page count, then interleave.
+  for (int c = 0; c < 3; c++) {
+    std::vector<int32_t> &L = B->dictwg_list[c];
+    if (L.size() < 16) continue;
+    std::vector<std::vector<int32_t>> x(8);
+    size_t i = 0;
+    while (i < L.size()) {
+      size_t j = i;
+      while (j < L.size() && B->pages[(size_t)L[j]].dict == B->pages[(size_t)L[i]].dict) j++;
+      size_t best = 0;
+      for (size_t q = 1; q < 8; q++)
+        if (x[q].size() < x[best].size()) best = q;
+      x[best].insert(x[best].end(), L.begin() + (long)i, L.begin() + (long)j);
+      i = j;
+    }
+    std::vector<int32_t> out;
+    size_t maxlen = 0;
+    for (auto &v : x) maxlen = std::max(maxlen, v.size());
+    for (size_t r = 0; r < maxlen; r++)
+      for (size_t q = 0; q < 8; q++)
+        if (r < x[q].size()) out.push_back(x[q][r]);
+    L.swap(out);
+  }
 
   // device buffers
   int rc = 0;
@@ -1198,11 +1261,14 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   rc |= alloc_dev((void **)&B->d_status, sizeof(uint32_t) * npages);
   rc |= alloc_dev((void **)&B->d_cols, sizeof(ColDesc) * B->cols.size());
   rc |= alloc_dev((void **)&B->d_dict, sizeof(uint64_t) * (size_t)B->dict_entries);
-  size_t nl = B->snappy_list.size() + B->dict_list.size() + B->data_list.size();
+  size_t nl = B->snappy_list.size() + B->dict_list.size() + 2 * B->data_list.size() + 16;
   rc |= alloc_dev((void **)&B->d_lists, sizeof(int32_t) * nl);
   B->max_jobs = B->snappy_list.empty() ? 0u : (uint32_t)(B->staged_bytes / 65536 + 64);
   rc |= alloc_dev(&B->d_jobs, 32 * (size_t)B->max_jobs);
   rc |= alloc_dev((void **)&B->d_njobs, 16);
+#ifdef PQ_STAMPS
+  rc |= alloc_dev((void **)&B->d_dbg, sizeof(uint64_t) * 8 * (B->data_list.size() + 1));
+#endif
   if (rc) {
     pqg_batch_destroy(B);
     return PQG_ERR_DEVICE;
@@ -1239,6 +1305,9 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
     lists.insert(lists.end(), B->snappy_list.begin(), B->snappy_list.end());
     lists.insert(lists.end(), B->dict_list.begin(), B->dict_list.end());
     lists.insert(lists.end(), B->data_list.begin(), B->data_list.end());
+    lists.insert(lists.end(), B->general_list.begin(), B->general_list.end());
+    lists.insert(lists.end(), B->flat_list.begin(), B->flat_list.end());
+    for (int c = 0; c < 3; c++) lists.insert(lists.end(), B->dictwg_list[c].begin(), B->dictwg_list[c].end());
     if (!lists.empty()) HIPCHK(hipMemcpy(B->d_lists, lists.data(), sizeof(int32_t) * lists.size(), hipMemcpyHostToDevice));
   }
   memcpy(B->h_status, B->status0.data(), sizeof(uint32_t) * npages);
@@ -1259,8 +1328,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
     c.flags = cp.flags;
     c.total_levels = cp.levels;
   }
-  bool any_count = false;
-  for (auto &cp : B->cols) any_count |= (cp.flags & COL_NEEDS_COUNT) != 0;
+  const bool any_count = B->any_count;
   if (!B->cols.empty())
     HIPCHK(hipMemcpy(B->d_cols, B->hcols.data(), sizeof(ColDesc) * B->cols.size(), hipMemcpyHostToDevice));
   if (any_count) {
@@ -1356,6 +1424,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.jobs = B->d_jobs;
   a.njobs = B->d_njobs;
   a.max_jobs = B->max_jobs;
+  a.dbg = B->d_dbg;
   if (B->max_jobs) HIPCHK(hipMemsetAsync(B->d_njobs, 0, 16, s));
   const int32_t ns = (int32_t)B->snappy_list.size(), nd = (int32_t)B->dict_list.size(),
                 ndata = (int32_t)B->data_list.size();
@@ -1379,11 +1448,32 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.nlist = ndata;
   e |= pq_launch(2, &a, s);
   mark();
-  e |= pq_launch(4, &a, s);
+  if (B->any_count) e |= pq_launch(4, &a, s);  // scans only feed lists / strings
   mark();
   if (!upto_scan) {
+    const int32_t ngen = (int32_t)B->general_list.size(), nflat = (int32_t)B->flat_list.size();
+    a.list = B->d_lists + ns + nd + ndata;
+    a.nlist = ngen;
     e |= pq_launch(3, &a, s);
+    a.list = B->d_lists + ns + nd + ndata + ngen;
+    a.nlist = nflat;
+    e |= pq_launch(7, &a, s);
+    // size classes, largest pages first (they have the longest tails)
+    int32_t offs[3], cnt[3];
+    int32_t off = ns + nd + ndata + ngen + nflat;
+    for (int c = 0; c < 3; c++) {
+      offs[c] = off;
+      cnt[c] = (int32_t)B->dictwg_list[c].size();
+      off += cnt[c];
+    }
+    for (int c = 2; c >= 0; c--) {
+      a.list = B->d_lists + offs[c];
+      a.nlist = cnt[c];
+      e |= pq_launch(8 + c, &a, s);
+    }
     mark();
+    a.list = B->d_lists + ns + nd;
+    a.nlist = ndata;
     e |= pq_launch(5, &a, s);
     mark();
   }
@@ -1583,6 +1673,7 @@ void pqg_batch_destroy(pqg_batch *B) {
   hipFree(B->d_lists);
   hipFree(B->d_jobs);
   hipFree(B->d_njobs);
+  hipFree(B->d_dbg);
   if (B->h_status) hipHostFree(B->h_status);
   for (int k = 0; k < pqg_batch::kRing; k++)
     for (int i = 0; i < 8; i++)
@@ -1635,6 +1726,7 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
     a.jobs = d_jobs;
     a.njobs = d_njobs;
     a.max_jobs = max_jobs;
+    a.dbg = nullptr;
     hipMemsetAsync(d_njobs, 0, 16, s);
     rc = pq_launch(0, &a, s);
     rc |= pq_launch(6, &a, s);
@@ -1656,3 +1748,13 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
   }
   return PQG_OK;
 }
+
+#ifdef PQ_STAMPS
+// diagnostic build only (not part of include/pqgpu.h): copy the stamp buffer
+extern "C" int pqg_diag_stamps(pqg_batch *B, uint64_t *out, size_t n) {
+  hipStreamSynchronize(B->ctx->stream);
+  size_t cap = 8 * (B->data_list.size() + 1);
+  if (n > cap) n = cap;
+  return hipMemcpy(out, B->d_dbg, n * 8, hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
+}
+#endif

@@ -41,7 +41,19 @@ struct KArgs {
   CopyJob *jobs;          // long Snappy literals deferred to k_copy
   uint32_t *njobs;
   uint32_t max_jobs;
+  uint64_t *dbg;          // diagnostic build only (-DPQ_STAMPS): per-workgroup s_memtime stamps
 };
+
+#ifdef PQ_STAMPS
+#define STAMP(i)                                                                              \
+  do {                                                                                        \
+    if (a.dbg && threadIdx.x == 0) a.dbg[(size_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
 
 __device__ __forceinline__ void set_status(uint32_t *status, int page, uint32_t stage, uint32_t code) {
   if (lane_id() == 0) atomicMin(&status[page], make_status(stage, code));
@@ -119,6 +131,31 @@ __device__ __forceinline__ void copy_literal(const uint8_t *s, uint8_t *dst, int
   }
 }
 
+// Wave copy of len bytes between arbitrary addresses: 16-byte aligned stores
+// after a short head, funnel-shifted dword loads (no LDS history).
+__device__ __forceinline__ void copy_bytes_wave(const uint8_t *s, uint8_t *D, int64_t len, int lane) {
+  int64_t head = (int64_t)((16 - ((uintptr_t)D & 15)) & 15);
+  if (head > len) head = len;
+  if (lane < head) D[lane] = s[lane];
+  const int64_t body = (len - head) >> 4;
+  const uint8_t *S = s + head;
+  uint8_t *D16 = D + head;
+  const uint32_t skew = (uint32_t)((uintptr_t)S & 3);
+  const uint32_t *SA = (const uint32_t *)((uintptr_t)S & ~(uintptr_t)3);
+  for (int64_t c = lane; c < body; c += 64) {
+    uint4 x = *(const uint4 *)(SA + 4 * c);
+    uint32_t x4 = SA[4 * c + 4];
+    uint4 o;
+    o.x = __builtin_amdgcn_alignbyte(x.y, x.x, skew);
+    o.y = __builtin_amdgcn_alignbyte(x.z, x.y, skew);
+    o.z = __builtin_amdgcn_alignbyte(x.w, x.z, skew);
+    o.w = __builtin_amdgcn_alignbyte(x4, x.w, skew);
+    *(uint4 *)(D16 + 16 * c) = o;
+  }
+  const int64_t done = head + body * 16;
+  if (lane < len - done) D[done + lane] = s[done + lane];
+}
+
 // Put the last min(len, RING) bytes of a deferred literal into the history
 // (16-byte LDS stores from funnel-shifted dword loads; done lazily, only when
 // a copy token follows the literal).
@@ -152,7 +189,7 @@ constexpr int MAX_DEFER = 64;  // one entry per lane
 __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t ring_all[SNAPPY_WAVES][RING];
   const int lane = lane_id();
-  const int wv = threadIdx.x >> 6;
+  const int wv = (int)ufirst(threadIdx.x >> 6);  // wave-uniform (keeps per-wave state in SGPRs)
   const int gi = blockIdx.x * SNAPPY_WAVES + wv;
   if (gi >= a.nlist) return;
   const int page = ufirst(a.list[gi]);
@@ -373,7 +410,7 @@ __global__ __launch_bounds__(256) void k_copy(KArgs a) {
 // K2: dictionary pages (page_dict.go:30-64)
 // ===========================================================================
 __global__ __launch_bounds__(256) void k_dict_prepare(KArgs a) {
-  const int gi = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int gi = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
   if (gi >= a.nlist) return;
   const int lane = lane_id();
   const int page = ufirst(a.list[gi]);
@@ -476,7 +513,7 @@ __device__ __forceinline__ int bits_len(int v) { return v ? 32 - __clz(v) : 0; }
 // K3: data page prepare
 // ===========================================================================
 __global__ __launch_bounds__(256) void k_prepare(KArgs a) {
-  const int gi = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int gi = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
   if (gi >= a.nlist) return;
   const int lane = lane_id();
   const int page = ufirst(a.list[gi]);
@@ -730,7 +767,7 @@ __device__ __forceinline__ uint64_t pick4_64(const uint64_t (&v)[4], int j) {
 // aligned to 256 output slots so each lane owns a 16-byte-aligned slice of
 // the values and whole validity words.
 __global__ __launch_bounds__(256) void k_decode(KArgs a) {
-  const int gi = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int gi = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
   if (gi >= a.nlist) return;
   const int lane = lane_id();
   const int page = ufirst(a.list[gi]);
@@ -1095,11 +1132,589 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
   if (err) set_status(a.status, page, err_stage, err);
 }
 
+// ===========================================================================
+// K5f: flat, required, fixed-width pages (PLAIN / RLE_DICTIONARY) — the hot
+// shape of C1/C2/C5.  One wave per page, 1024 values per step, 16
+// consecutive values per lane (64-128 output bytes per lane, 16-byte
+// stores).  The encoded index stream is read through an 8 KB per-wave LDS
+// window (headers and bit-packed data alike), so a step costs one global
+// round trip: the dictionary gathers.
+// ===========================================================================
+constexpr int FW_WIN = 8192;     // LDS window per wave
+constexpr int FW_WAVES = 4;
+constexpr int FW_STEP = 1024;    // values per step
+constexpr int FW_PER_LANE = 16;
+
+struct LdsWin {
+  uint8_t *lds;        // this wave's window
+  const uint8_t *p;    // stream start
+  int64_t len;         // stream length
+  int64_t lo, hi;      // stream offsets currently held: [lo, hi)
+  const uint8_t *ab;   // absolute address of lds[0]
+
+  // make [a, b) (stream offsets, b - a <= FW_WIN - 32) resident
+  __device__ __forceinline__ void ensure(int64_t a, int64_t b) {
+    if (a >= lo && b <= hi) return;
+    const uintptr_t A = (uintptr_t)(p + a) & ~(uintptr_t)15;
+    const uintptr_t E = (uintptr_t)(p + len) + 16;  // never read past the stream end + 16 (buffers are padded)
+    const uintptr_t last = (E - 16) & ~(uintptr_t)15;
+    const int lane = lane_id();
+    uint4 v[FW_WIN / 1024];
+#pragma unroll
+    for (int k = 0; k < FW_WIN / 1024; k++) {  // all loads first, then all LDS stores
+      uintptr_t src = A + (uintptr_t)(k * 1024 + lane * 16);
+      v[k] = *(const uint4 *)(src < E ? src : last);
+    }
+#pragma unroll
+    for (int k = 0; k < FW_WIN / 1024; k++) {
+      uintptr_t src = A + (uintptr_t)(k * 1024 + lane * 16);
+      *(uint4 *)(lds + k * 1024 + lane * 16) = src < E ? v[k] : make_uint4(0, 0, 0, 0);
+    }
+    ab = (const uint8_t *)A;
+    lo = (int64_t)(A - (uintptr_t)p);
+    hi = lo + FW_WIN;
+  }
+  __device__ __forceinline__ uint32_t byte(int64_t off) { return lds[(p + off) - ab]; }
+  // bits [bitpos, bitpos + bw) of the stream; bytes at/after len read as zero
+  __device__ __forceinline__ uint32_t bits(int64_t bitpos, int bw) {
+    int64_t byteoff = bitpos >> 3;
+    int sh = (int)(bitpos & 7);
+    uintptr_t la = (uintptr_t)((p + byteoff) - ab);
+    const uint32_t *q = (const uint32_t *)(lds + (la & ~(uintptr_t)3));
+    uint64_t v = ((uint64_t)q[1] << 32) | q[0];
+    v >>= (la & 3) * 8 + sh;
+    uint32_t val = (uint32_t)v & (bw == 32 ? 0xffffffffu : ((1u << bw) - 1));
+    int64_t avail = (len - byteoff) * 8 - sh;
+    if (avail < bw) val = avail <= 0 ? 0u : (val & ((1u << avail) - 1));
+    return val;
+  }
+};
+
+__global__ __launch_bounds__(256) void k_decode_flat(KArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t win_all[FW_WAVES][FW_WIN + 16];
+  const int wv = (int)ufirst(threadIdx.x >> 6);  // wave-uniform (keeps per-wave state in SGPRs)
+  const int gi = blockIdx.x * FW_WAVES + wv;
+  if (gi >= a.nlist) return;
+  const int lane = lane_id();
+  const int page = ufirst(a.list[gi]);
+  if (page_status(a.status, page) != STATUS_OK) return;
+  const PageDesc d = a.pages[page];
+  if (d.dict >= 0 && page_status(a.status, d.dict) != STATUS_OK) return;
+  const ColDesc c = a.cols[d.col];
+  const PageInfo pi = a.info[page];
+  const int n = d.num_values;
+  if (n == 0) return;
+  const uint8_t *vals = body_ptr(a, d) + pi.val_off;
+  const int64_t vlen = pi.val_len;
+  const int w = c.width;  // 4 or 8
+  uint8_t *out = c.values + d.level_base * w;
+
+  if (d.enc == ENC_PLAIN) {
+    // a straight copy of n*w bytes (binary.Read per value, type_int32.go:23-37)
+    if ((int64_t)n * w > vlen) {
+      set_status(a.status, page, ST_VALUES, E_EOF);
+      return;
+    }
+    copy_bytes_wave(vals, out, (int64_t)n * w, lane);
+    return;
+  }
+
+  // RLE_DICTIONARY (type_dict.go:39-59) over the hybrid key stream
+  const PageDesc *dp = d.dict >= 0 ? &a.pages[d.dict] : nullptr;
+  if (!dp) {
+    set_status(a.status, page, ST_VALUES, E_DICT);
+    return;
+  }
+  const uint8_t *dict = body_ptr(a, *dp);
+  const int64_t dict_n = dp->num_values;
+  const int bw = pi.idx_bw;
+
+  LdsWin L;
+  L.lds = win_all[wv];
+  L.p = vals + 1;
+  L.len = vlen - 1;
+  L.lo = 1;
+  L.hi = 0;  // empty
+  L.ab = nullptr;
+
+  // hybrid run state (hybrid_decoder.go:82-166), wave-uniform
+  int64_t pos = 0, rem = 0, data = 0, vi = 0;
+  uint32_t rle_val = 0;
+  bool rle = false;
+  uint32_t err = E_OK;
+  const bool aligned_dict = (((uintptr_t)dict) & (w - 1)) == 0;
+
+  for (int64_t e0 = 0; e0 < n && !err; e0 += FW_STEP) {
+    const int cnt = (int)min<int64_t>(FW_STEP, n - e0);
+    uint32_t key[FW_PER_LANE];
+#pragma unroll
+    for (int k = 0; k < FW_PER_LANE; k++) key[k] = 0;
+    int got = 0;
+    if (bw > 0) {
+      while (got < cnt) {
+        if (rem == 0) {
+          // readRunHeader: uvarint from the LDS window
+          uint64_t h = 0;
+          uint32_t sh = 0;
+          for (int i = 0;; i++) {
+            if (pos >= L.len) {
+              err = E_EOF;
+              break;
+            }
+            L.ensure(pos, pos + 16);
+            uint32_t b = ufirst(L.byte(pos));
+            pos++;
+            if (b < 0x80) {
+              if (i > 9 || (i == 9 && b > 1)) err = E_RLE;
+              h |= (uint64_t)b << (sh & 63);
+              break;
+            }
+            if (sh < 64) h |= (uint64_t)(b & 0x7f) << sh;
+            sh += 7;
+          }
+          if (err) break;
+          if (h > 0x7fffffffull) {
+            err = E_RLE;
+            break;
+          }
+          if (h & 1) {
+            int64_t g = (int64_t)(h >> 1);
+            if (g == 0) {
+              err = E_RLE;
+              break;
+            }
+            rle = false;
+            rem = g * 8;
+            data = pos;
+            vi = 0;
+            pos = data + g * (int64_t)bw;
+          } else {
+            int64_t cr = (int64_t)(h >> 1);
+            if (cr == 0) {
+              err = E_RLE;
+              break;
+            }
+            int sz = (bw + 7) >> 3;
+            if (pos >= L.len || pos + sz > L.len) {
+              err = E_EOF;
+              break;
+            }
+            L.ensure(pos, pos + 16);
+            uint32_t v = 0;
+            for (int k = 0; k < sz; k++) v |= ufirst(L.byte(pos + k)) << (8 * k);
+            pos += sz;
+            if (bw < 32 && (v >> bw) != 0) {
+              err = E_RLE;
+              break;
+            }
+            rle = true;
+            rem = cr;
+            rle_val = v;
+          }
+        }
+        const int take = (int)min<int64_t>(rem, (int64_t)(cnt - got));
+        if (rle) {
+#pragma unroll
+          for (int k = 0; k < FW_PER_LANE; k++) {
+            int j = FW_PER_LANE * lane + k;
+            key[k] = (j >= got && j < got + take) ? rle_val : key[k];
+          }
+        } else {
+          const int64_t last_group = (vi + take - 1) >> 3;
+          if (data + last_group * bw >= L.len) {
+            err = E_EOF;
+            break;
+          }
+          const int64_t b_first = data + ((vi * bw) >> 3);
+          const int64_t b_last = data + (((vi + take) * (int64_t)bw + 7) >> 3);
+          L.ensure(b_first, b_last + 8);
+          // bit offset of chunk value 0 relative to lds[0] (fits 32 bits: the window is 8 KB)
+          const int32_t rbit0 = (int32_t)(((L.p + data) - L.ab) * 8 + (vi - got) * (int64_t)bw);
+          const uint32_t mask = bw == 32 ? 0xffffffffu : ((1u << bw) - 1);
+          const bool tail = b_last + 8 > L.len;  // values may touch bytes past the stream end
+          const int64_t end_bit = ((L.p + L.len) - L.ab) * 8;
+          // issue every LDS read of the lane's 16 values back to back, select afterwards
+#pragma unroll
+          for (int k = 0; k < FW_PER_LANE; k++) {
+            const int j = FW_PER_LANE * lane + k;
+            const bool in = j >= got && j < got + take;
+            const int32_t rb = in ? rbit0 + j * bw : 0;
+            const uint32_t *q = (const uint32_t *)(L.lds + ((rb >> 3) & ~3));
+            uint64_t v = ((uint64_t)q[1] << 32) | q[0];
+            uint32_t val = (uint32_t)(v >> (rb & 31)) & mask;
+            // zero-fill past the stream end (hybrid_decoder.go:133-141), branch-free
+            const int32_t avail = tail ? (int32_t)min<int64_t>(end_bit - rb, 64) : 64;
+            const uint32_t amask = avail <= 0 ? 0u : (avail >= 32 ? 0xffffffffu : ((1u << avail) - 1));
+            val &= amask;
+            key[k] = in ? val : key[k];
+          }
+          vi += take;
+        }
+        rem -= take;
+        got += take;
+      }
+      if (err) break;
+    }
+    // gather + store
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < FW_PER_LANE; k++) bad |= (FW_PER_LANE * lane + k < cnt) && (int64_t)key[k] >= dict_n;
+    if (ballot(bad)) {
+      err = E_DICT;
+      break;
+    }
+    const int64_t s0 = e0 + FW_PER_LANE * lane;  // my first entry
+    const bool full = FW_PER_LANE * lane + FW_PER_LANE <= cnt;
+    if (w == 4) {
+      uint32_t v[FW_PER_LANE];
+#pragma unroll
+      for (int k = 0; k < FW_PER_LANE; k++) {
+        const uint8_t *src = dict + (int64_t)key[k] * 4;
+        v[k] = aligned_dict ? *(const uint32_t *)src : load_u32_unaligned(src);
+      }
+      uint32_t *o = (uint32_t *)(out + s0 * 4);
+      if (full && (((uintptr_t)o) & 15) == 0) {
+#pragma unroll
+        for (int k = 0; k < FW_PER_LANE; k += 4) *(uint4 *)(o + k) = make_uint4(v[k], v[k + 1], v[k + 2], v[k + 3]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < FW_PER_LANE; k++)
+          if (FW_PER_LANE * lane + k < cnt) o[k] = v[k];
+      }
+    } else {
+      uint64_t v[FW_PER_LANE];
+#pragma unroll
+      for (int k = 0; k < FW_PER_LANE; k++) {
+        const uint8_t *src = dict + (int64_t)key[k] * 8;
+        v[k] = aligned_dict ? *(const uint64_t *)src : load_u64_unaligned(src);
+      }
+      uint64_t *o = (uint64_t *)(out + s0 * 8);
+      if (full && (((uintptr_t)o) & 15) == 0) {
+#pragma unroll
+        for (int k = 0; k < FW_PER_LANE; k += 2)
+          *(uint4 *)(o + k) = make_uint4((uint32_t)v[k], (uint32_t)(v[k] >> 32), (uint32_t)v[k + 1], (uint32_t)(v[k + 1] >> 32));
+      } else {
+#pragma unroll
+        for (int k = 0; k < FW_PER_LANE; k++)
+          if (FW_PER_LANE * lane + k < cnt) o[k] = v[k];
+      }
+    }
+  }
+  if (err) set_status(a.status, page, ST_VALUES, err);
+}
+
+// ===========================================================================
+// K5d: flat, required, fixed-width RLE_DICTIONARY pages whose key stream fits
+// in LDS — one 256-thread workgroup per page.
+//   1. the whole key stream is staged into LDS with 16-byte loads;
+//   2. wave 0 walks the run headers (hybrid_decoder.go:143-166) into an LDS
+//      run table.  The walk is speculative: after a bit-packed header it
+//      checks, one candidate per lane, whether the next 63 runs repeat the
+//      same header at the same stride (what an encoder writes for
+//      high-entropy keys) and accepts the matching prefix in one step;
+//   3. all four waves decode 1024-value steps (step s -> wave s % 4) with the
+//      run table held in registers (lane i = entry i of a 64-entry window):
+//      keys from LDS, dictionary gathers from HBM/L2, 16-byte stores.
+// A page with more runs than the table holds is processed in table-sized
+// rounds.
+// ===========================================================================
+constexpr int DW_RUNS = 512;  // run-table entries per round
+
+struct RunEnt {
+  int32_t start;    // first value of the run (page-relative)
+  int32_t bitpos;   // bit offset of the run's data in the staged stream; -1 for RLE
+  uint32_t rle_val;
+  int32_t pad;
+};
+
+// DW_STREAM: staged key-stream bytes per workgroup.  Three instantiations
+// (8 / 24 / 56 KB) so small pages do not pay the LDS (occupancy) of big ones;
+// the host routes each page by its body length.
+template <int DW_STREAM>
+__global__ __launch_bounds__(256) void k_decode_dict_wg(KArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t sstream[DW_STREAM + 32];
+  __shared__ __attribute__((aligned(16))) RunEnt runs[DW_RUNS + 1];
+  __shared__ int32_t s_nruns, s_cover, s_err, s_dict_err;
+  const int wv = (int)ufirst(threadIdx.x >> 6);
+  const int lane = lane_id();
+  if ((int)blockIdx.x >= a.nlist) return;
+  const int page = ufirst(a.list[blockIdx.x]);
+  if (page_status(a.status, page) != STATUS_OK) return;
+  const PageDesc d = a.pages[page];
+  if (d.dict < 0 || page_status(a.status, d.dict) != STATUS_OK) {
+    if (d.dict < 0 && threadIdx.x == 0) atomicMin(&a.status[page], make_status(ST_VALUES, E_DICT));
+    return;
+  }
+  const ColDesc c = a.cols[d.col];
+  const PageInfo pi = a.info[page];
+  const int n = (int)ufirst((uint32_t)d.num_values);
+  if (n == 0) return;
+  const uint8_t *vals = body_ptr(a, d) + pi.val_off;
+  const int64_t slen = ufirst64((int64_t)pi.val_len - 1);  // key stream after the bit-width byte
+  const uint8_t *ks = vals + 1;
+  const int w = (int)ufirst((uint32_t)c.width);
+  uint8_t *out = c.values + d.level_base * w;
+  const PageDesc dp = a.pages[d.dict];
+  const uint8_t *dict = body_ptr(a, dp);
+  const int64_t dict_n = ufirst64(dp.num_values);
+  const int bw = (int)ufirst((uint32_t)pi.idx_bw);
+  const bool aligned_dict = (((uintptr_t)dict) & (w - 1)) == 0;
+
+  STAMP(0);
+  // 1. stage the key stream: sstream[i] = byte at address A + i, A = ks aligned down to 16
+  const uintptr_t A = (uintptr_t)ks & ~(uintptr_t)15;
+  const int32_t skew = (int32_t)ufirst((uint32_t)((uintptr_t)ks - A));
+  const int64_t nbytes = skew + slen;  // the host routes only pages that fit
+  for (int64_t off = (int64_t)threadIdx.x * 16; off < nbytes + 16; off += 256 * 16)
+    *(uint4 *)(sstream + off) = off < nbytes ? *(const uint4 *)(A + off) : make_uint4(0, 0, 0, 0);
+  if (threadIdx.x == 0) {
+    s_err = 0;
+    s_dict_err = 0;
+  }
+  __syncthreads();
+  STAMP(1);
+
+  int64_t hpos = 0;        // wave 0: next header (stream offset)
+  int32_t covered = 0;     // values covered by completed rounds
+  const int64_t end_bit = (int64_t)(skew + slen) * 8;
+  const uint32_t mask = bw == 32 ? 0xffffffffu : ((1u << bw) - 1);
+
+  while (covered < n) {
+    // 2. wave 0 walks up to DW_RUNS run headers
+    if (wv == 0) {
+      int32_t nr = 0, v = covered;
+      uint32_t err = E_OK;
+      if (bw == 0) {  // hybrid_decoder.go:84-86: all zeros, nothing read
+        if (lane == 0) runs[0] = RunEnt{v, -1, 0u, 0};
+        nr = 1;
+        v = n;
+      }
+      while (v < n && nr < DW_RUNS && !err) {
+        hpos = ufirst64(hpos);
+        v = (int32_t)ufirst((uint32_t)v);
+        nr = (int32_t)ufirst((uint32_t)nr);
+        const int64_t h0 = hpos;
+        uint64_t h = 0;
+        uint32_t sh = 0;
+        for (int i = 0;; i++) {
+          if (hpos >= slen) {
+            err = E_EOF;
+            break;
+          }
+          uint32_t b = ufirst(sstream[skew + hpos]);
+          hpos++;
+          if (b < 0x80) {
+            if (i > 9 || (i == 9 && b > 1)) err = E_RLE;
+            h |= (uint64_t)b << (sh & 63);
+            break;
+          }
+          if (sh < 64) h |= (uint64_t)(b & 0x7f) << sh;
+          sh += 7;
+        }
+        if (err) break;
+        if (h > 0x7fffffffull) {
+          err = E_RLE;
+          break;
+        }
+        const int32_t hl = (int32_t)(hpos - h0);  // header length in bytes
+        if (h & 1) {
+          const int64_t g = (int64_t)(h >> 1);
+          if (g == 0) {
+            err = E_RLE;
+            break;
+          }
+          // every group the page needs must start inside the stream (:133-141)
+          int64_t need = min<int64_t>(g * 8, (int64_t)(n - v));
+          if (hpos + ((need - 1) >> 3) * bw >= slen) {
+            err = E_EOF;
+            break;
+          }
+          if (lane == 0) runs[nr] = RunEnt{v, (int32_t)((skew + hpos) * 8), 0u, 0};
+          v = (int32_t)min<int64_t>((int64_t)v + g * 8, (int64_t)n);
+          hpos += g * (int64_t)bw;
+          nr++;
+          // speculate: lane k checks for the same header again k strides ahead
+          const int64_t stride = hl + g * (int64_t)bw;
+          const int64_t cand = hpos + (int64_t)lane * stride;  // candidate header of run nr + lane
+          const int64_t cstart = (int64_t)v + (int64_t)lane * g * 8;
+          bool ok = cstart < n && nr + lane < DW_RUNS && cand + hl <= slen;
+          if (ok) {
+            for (int q = 0; q < hl; q++) ok &= sstream[skew + cand + q] == sstream[skew + h0 + q];
+            const int64_t cneed = min<int64_t>(g * 8, (int64_t)n - cstart);
+            ok &= cand + hl + ((cneed - 1) >> 3) * bw < slen;
+          }
+          const uint64_t okm = ballot(ok);
+          const int m = (int)__builtin_ctzll(~okm);  // leading accepted candidates (lanes 0..m-1)
+          if (m > 0) {
+            if (lane < m) runs[nr + lane] = RunEnt{(int32_t)cstart, (int32_t)((skew + cand + hl) * 8), 0u, 0};
+            v = (int32_t)min<int64_t>((int64_t)v + (int64_t)m * g * 8, (int64_t)n);
+            hpos += (int64_t)m * stride;
+            nr += m;
+          }
+        } else {
+          int64_t cr = (int64_t)(h >> 1);
+          if (cr == 0) {
+            err = E_RLE;
+            break;
+          }
+          int sz = (bw + 7) >> 3;
+          if (hpos >= slen || hpos + sz > slen) {
+            err = E_EOF;
+            break;
+          }
+          uint32_t val = 0;
+          for (int k = 0; k < sz; k++) val |= ufirst(sstream[skew + hpos + k]) << (8 * k);
+          hpos += sz;
+          if (bw < 32 && (val >> bw) != 0) {
+            err = E_RLE;
+            break;
+          }
+          if (lane == 0) runs[nr] = RunEnt{v, -1, val, 0};
+          v = (int32_t)min<int64_t>((int64_t)v + cr, (int64_t)n);
+          nr++;
+        }
+      }
+      if (lane == 0) {
+        runs[nr] = RunEnt{v, 0, 0u, 0};  // sentinel: end of coverage
+        s_nruns = nr;
+        s_cover = v;
+        if (err) s_err = (int32_t)err;
+      }
+    }
+    __syncthreads();
+    STAMP(2);
+    const int32_t nr = (int32_t)ufirst((uint32_t)s_nruns), cover = (int32_t)ufirst((uint32_t)s_cover);
+    // on a header error, the values before it are still decoded: a dictionary
+    // index error among them comes first in the reference (type_dict.go:45-53)
+
+    // 3. steps of 1024 values over [covered, cover); step boundaries are page-absolute.
+    // Run table window in registers: lane i holds entry wb + i (and the next start).
+    int32_t wb = -1;
+    int32_t r_start = 0, r_next = 0, r_bit = 0;
+    uint32_t r_val = 0;
+    for (int32_t e0 = (covered / FW_STEP) * FW_STEP + wv * FW_STEP; e0 < cover; e0 += FW_WAVES * FW_STEP) {
+      const int32_t lo = max(e0, covered), hi = min(e0 + FW_STEP, cover);
+      // window containing the run of `lo`: first entry with start <= lo < next start
+      while (true) {
+        if (wb < 0 || !(ufirst(__builtin_amdgcn_readlane(r_start, 0)) <= lo &&
+                        lo < (int32_t)__builtin_amdgcn_readlane(r_next, min(63, nr - 1 - wb)))) {
+          // (re)load: binary search the LDS table for the run of lo, window starts there
+          int32_t l = 0, h2 = nr - 1;
+          while (l < h2) {
+            int32_t mid = (l + h2 + 1) >> 1;
+            if ((int32_t)ufirst((uint32_t)runs[mid].start) <= lo) l = mid;
+            else h2 = mid - 1;
+          }
+          wb = l;
+          const int32_t ei = min(wb + lane, nr - 1);
+          const RunEnt re = runs[ei];
+          r_start = re.start;
+          r_bit = re.bitpos;
+          r_val = re.rle_val;
+          r_next = runs[ei + 1].start;
+        }
+        break;
+      }
+      // per-lane: run of my first value j0, found by binary search over the window lanes
+      const int32_t j0 = e0 + FW_PER_LANE * lane;
+      const int32_t wn = min(64, nr - wb);  // valid window entries
+      int32_t ri = 0;
+#pragma unroll
+      for (int stp = 32; stp >= 1; stp >>= 1) {
+        int32_t cand = ri + stp;
+        int32_t cs = (int32_t)shfl32((uint32_t)r_start, min(cand, 63));
+        if (cand < wn && cs <= j0) ri = cand;
+      }
+      int32_t my_start = (int32_t)shfl32((uint32_t)r_start, ri);
+      int32_t my_next = (int32_t)shfl32((uint32_t)r_next, ri);
+      int32_t my_bit = (int32_t)shfl32((uint32_t)r_bit, ri);
+      uint32_t my_val = shfl32(r_val, ri);
+      uint32_t key[FW_PER_LANE];
+#pragma unroll
+      for (int k = 0; k < FW_PER_LANE; k++) {
+        const int32_t j = j0 + k;
+        const bool cross = j >= my_next && ri + 1 < wn;  // crossed into the next run (rare: runs are long)
+        if (ballot(cross)) {  // wave-uniform branch: every lane takes part in the shuffles
+          ri += cross ? 1 : 0;
+          my_start = (int32_t)shfl32((uint32_t)r_start, ri);
+          my_next = (int32_t)shfl32((uint32_t)r_next, ri);
+          my_bit = (int32_t)shfl32((uint32_t)r_bit, ri);
+          my_val = shfl32(r_val, ri);
+        }
+        const bool in = j >= lo && j < hi;
+        const int32_t rb = (in && my_bit >= 0) ? my_bit + (j - my_start) * bw : 0;
+        const uint32_t *q = (const uint32_t *)(sstream + ((rb >> 3) & ~3));
+        uint64_t vv = ((uint64_t)q[1] << 32) | q[0];
+        uint32_t val = (uint32_t)(vv >> (rb & 31)) & mask;
+        const int32_t avail = (int32_t)min<int64_t>(end_bit - rb, 64);  // zero past the stream end
+        val &= avail <= 0 ? 0u : (avail >= 32 ? 0xffffffffu : ((1u << avail) - 1));
+        key[k] = my_bit < 0 ? my_val : val;
+      }
+      bool bad = false;
+#pragma unroll
+      for (int k = 0; k < FW_PER_LANE; k++) {
+        const int32_t j = j0 + k;
+        bad |= j >= lo && j < hi && (int64_t)key[k] >= dict_n;
+      }
+      if (ballot(bad)) {
+        if (lane == 0) {
+          atomicMin(&a.status[page], make_status(ST_VALUES, E_DICT));
+          s_dict_err = 1;
+        }
+        continue;
+      }
+      const bool full = j0 >= lo && j0 + FW_PER_LANE <= hi;
+      if (w == 4) {
+        uint32_t vv[FW_PER_LANE];
+#pragma unroll
+        for (int k = 0; k < FW_PER_LANE; k++) {
+          const uint8_t *sp = dict + (int64_t)(j0 + k < hi ? key[k] : 0) * 4;
+          vv[k] = aligned_dict ? *(const uint32_t *)sp : load_u32_unaligned(sp);
+        }
+        uint32_t *o = (uint32_t *)(out + (int64_t)j0 * 4);
+        if (full && (((uintptr_t)o) & 15) == 0) {
+#pragma unroll
+          for (int k = 0; k < FW_PER_LANE; k += 4) *(uint4 *)(o + k) = make_uint4(vv[k], vv[k + 1], vv[k + 2], vv[k + 3]);
+        } else {
+#pragma unroll
+          for (int k = 0; k < FW_PER_LANE; k++)
+            if (j0 + k >= lo && j0 + k < hi) o[k] = vv[k];
+        }
+      } else {
+        uint64_t vv[FW_PER_LANE];
+#pragma unroll
+        for (int k = 0; k < FW_PER_LANE; k++) {
+          const uint8_t *sp = dict + (int64_t)(j0 + k < hi ? key[k] : 0) * 8;
+          vv[k] = aligned_dict ? *(const uint64_t *)sp : load_u64_unaligned(sp);
+        }
+        uint64_t *o = (uint64_t *)(out + (int64_t)j0 * 8);
+        if (full && (((uintptr_t)o) & 15) == 0) {
+#pragma unroll
+          for (int k = 0; k < FW_PER_LANE; k += 2)
+            *(uint4 *)(o + k) = make_uint4((uint32_t)vv[k], (uint32_t)(vv[k] >> 32), (uint32_t)vv[k + 1], (uint32_t)(vv[k + 1] >> 32));
+        } else {
+#pragma unroll
+          for (int k = 0; k < FW_PER_LANE; k++)
+            if (j0 + k >= lo && j0 + k < hi) o[k] = vv[k];
+        }
+      }
+    }
+    covered = cover;
+    __syncthreads();  // the run table is rewritten next round
+    STAMP(3);
+    if (s_err) {
+      if (threadIdx.x == 0 && !s_dict_err) atomicMin(&a.status[page], make_status(ST_VALUES, (uint32_t)s_err));
+      return;
+    }
+    if (s_dict_err) return;
+  }
+}
+
 // level-error precedence pass: for pages that failed in k_decode at the
 // values or def stage, finish decoding the earlier level streams to see if
 // the reference would have failed there first.
 __global__ __launch_bounds__(256) void k_level_check(KArgs a) {
-  const int gi = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int gi = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
   if (gi >= a.nlist) return;
   const int page = ufirst(a.list[gi]);
   uint32_t st = page_status(a.status, page);
@@ -1156,6 +1771,7 @@ struct pq_launch_args {
   void *jobs;
   uint32_t *njobs;
   uint32_t max_jobs;
+  uint64_t *dbg;
 };
 
 static pq::KArgs to_k(const pq_launch_args *p) {
@@ -1173,6 +1789,7 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   k.jobs = (pq::CopyJob *)p->jobs;
   k.njobs = p->njobs;
   k.max_jobs = p->max_jobs;
+  k.dbg = p->dbg;
   return k;
 }
 
@@ -1196,6 +1813,10 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     case 2: hipLaunchKernelGGL(pq::k_prepare, grid, block, 0, s, k); break;
     case 3: hipLaunchKernelGGL(pq::k_decode, grid, block, 0, s, k); break;
     case 5: hipLaunchKernelGGL(pq::k_level_check, grid, block, 0, s, k); break;
+    case 7: hipLaunchKernelGGL(pq::k_decode_flat, grid, block, 0, s, k); break;
+    case 8: hipLaunchKernelGGL(pq::k_decode_dict_wg<8 * 1024>, dim3(k.nlist), block, 0, s, k); break;
+    case 9: hipLaunchKernelGGL(pq::k_decode_dict_wg<24 * 1024>, dim3(k.nlist), block, 0, s, k); break;
+    case 10: hipLaunchKernelGGL(pq::k_decode_dict_wg<56 * 1024>, dim3(k.nlist), block, 0, s, k); break;
     default: return 1;
   }
   return hipGetLastError() == hipSuccess ? 0 : 17;
