@@ -90,6 +90,7 @@ struct PageInfo {
   int32_t pad;
   int64_t rows, slots, non_null, str_bytes;  // counts (prepare)
   int64_t row_base, slot_base, str_base;     // exclusive scans over the column's pages
+  int64_t alias1;  // k_snappy: 1 + input offset of the body when the block is one literal (0: none)
 };
 
 }  // namespace pq

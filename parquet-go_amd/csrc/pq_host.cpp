@@ -46,6 +46,8 @@ struct pq_launch_args {
   void *jobs;
   uint32_t *njobs;
   uint32_t max_jobs;
+  const int32_t *job_base;
+  const int32_t *job_owner;
   uint64_t *dbg;
 };
 int pq_launch(int which, const pq_launch_args *p, hipStream_t s);
@@ -497,7 +499,7 @@ struct pqg_batch {
   std::vector<uint32_t> status0;  // host-side initial status per page
   std::vector<int32_t> snappy_list, dict_list, data_list;
   std::vector<int32_t> general_list, flat_list;  // data pages for k_decode / k_decode_flat
-  std::vector<int32_t> dictwg_list[3];            // k_decode_dict_wg<8K / 24K / 56K>
+  std::vector<int32_t> dictwg_list[3];            // k_decode_dict_wg<8K / 31K / 56K>
   bool any_count = false;
   std::vector<ChunkError> chunk_errors;
   int64_t input_bytes = 0, staged_bytes = 0, h2d_bytes = 0, host_inflated = 0, dict_entries = 0;
@@ -510,7 +512,8 @@ struct pqg_batch {
   uint64_t *d_dict = nullptr;
   int32_t *d_lists = nullptr;
   void *d_jobs = nullptr;        // deferred long-literal copy jobs (k_snappy -> k_copy)
-  uint32_t *d_njobs = nullptr;
+  uint32_t *d_njobs = nullptr;   // per Snappy page: jobs written
+  int32_t *d_job_base = nullptr, *d_job_owner = nullptr;
   uint32_t max_jobs = 0;
   uint64_t *d_dbg = nullptr;     // diagnostic stamps (PQ_STAMPS builds only)
   uint32_t *h_status = nullptr;  // pinned mirror
@@ -1218,7 +1221,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
     // V1 required pages have no level streams, so the key stream is body_len - 1 bytes
     bool wg = fast && d.enc == ENC_RLE_DICT && d.kind == PAGE_V1 && d.body_len <= 56 * 1024 - 32;
     if (wg) {
-      int cls = d.body_len <= 8 * 1024 - 32 ? 0 : d.body_len <= 24 * 1024 - 32 ? 1 : 2;
+      int cls = d.body_len <= 8 * 1024 - 32 ? 0 : d.body_len <= 31 * 1024 - 32 ? 1 : 2;
       B->dictwg_list[cls].push_back(pi);
     } else {
       (fast ? B->flat_list : B->general_list).push_back(pi);
@@ -1263,9 +1266,22 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   rc |= alloc_dev((void **)&B->d_dict, sizeof(uint64_t) * (size_t)B->dict_entries);
   size_t nl = B->snappy_list.size() + B->dict_list.size() + 2 * B->data_list.size() + 16;
   rc |= alloc_dev((void **)&B->d_lists, sizeof(int32_t) * nl);
-  B->max_jobs = B->snappy_list.empty() ? 0u : (uint32_t)(B->staged_bytes / 65536 + 64);
+  // per Snappy page a region of job slots: at most body_len / 16 KB literals are long enough to defer
+  std::vector<int32_t> job_base(B->snappy_list.size() + 1), job_owner;
+  for (size_t q = 0; q < B->snappy_list.size(); q++) {
+    job_base[q] = (int32_t)job_owner.size();
+    int32_t cap = std::min(64, B->pages[(size_t)B->snappy_list[q]].body_len / (16 * 1024));
+    for (int32_t k = 0; k < cap; k++) job_owner.push_back((int32_t)q);
+  }
+  B->max_jobs = (uint32_t)job_owner.size();
   rc |= alloc_dev(&B->d_jobs, 32 * (size_t)B->max_jobs);
-  rc |= alloc_dev((void **)&B->d_njobs, 16);
+  rc |= alloc_dev((void **)&B->d_njobs, 4 * (B->snappy_list.size() + 1));
+  rc |= alloc_dev((void **)&B->d_job_base, 4 * job_base.size());
+  rc |= alloc_dev((void **)&B->d_job_owner, 4 * (job_owner.size() + 1));
+  if (!rc) {
+    hipMemcpy(B->d_job_base, job_base.data(), 4 * job_base.size(), hipMemcpyHostToDevice);
+    if (!job_owner.empty()) hipMemcpy(B->d_job_owner, job_owner.data(), 4 * job_owner.size(), hipMemcpyHostToDevice);
+  }
 #ifdef PQ_STAMPS
   rc |= alloc_dev((void **)&B->d_dbg, sizeof(uint64_t) * 8 * (B->data_list.size() + 1));
 #endif
@@ -1424,8 +1440,9 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.jobs = B->d_jobs;
   a.njobs = B->d_njobs;
   a.max_jobs = B->max_jobs;
+  a.job_base = B->d_job_base;
+  a.job_owner = B->d_job_owner;
   a.dbg = B->d_dbg;
-  if (B->max_jobs) HIPCHK(hipMemsetAsync(B->d_njobs, 0, 16, s));
   const int32_t ns = (int32_t)B->snappy_list.size(), nd = (int32_t)B->dict_list.size(),
                 ndata = (int32_t)B->data_list.size();
   int e = 0;
@@ -1673,6 +1690,8 @@ void pqg_batch_destroy(pqg_batch *B) {
   hipFree(B->d_lists);
   hipFree(B->d_jobs);
   hipFree(B->d_njobs);
+  hipFree(B->d_job_base);
+  hipFree(B->d_job_owner);
   hipFree(B->d_dbg);
   if (B->h_status) hipHostFree(B->h_status);
   for (int k = 0; k < pqg_batch::kRing; k++)
@@ -1699,9 +1718,18 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
   rc |= alloc_dev((void **)&d_list, sizeof(int32_t));
   void *d_jobs = nullptr;
   uint32_t *d_njobs = nullptr;
-  const uint32_t max_jobs = (uint32_t)(expect / 65536 + 8);
+  int32_t *d_jb = nullptr, *d_jo = nullptr;
+  const uint32_t max_jobs = (uint32_t)std::min<size_t>(64, expect / (16 * 1024));
   rc |= alloc_dev(&d_jobs, 32 * (size_t)max_jobs);
   rc |= alloc_dev((void **)&d_njobs, 16);
+  rc |= alloc_dev((void **)&d_jb, 16);
+  rc |= alloc_dev((void **)&d_jo, 4 * (size_t)(max_jobs + 1));
+  if (!rc) {
+    int32_t zero4[4] = {0, 0, 0, 0};
+    hipMemcpy(d_jb, zero4, 16, hipMemcpyHostToDevice);
+    std::vector<int32_t> owners(max_jobs + 1, 0);
+    hipMemcpy(d_jo, owners.data(), 4 * owners.size(), hipMemcpyHostToDevice);
+  }
   if (!rc) {
     PageDesc d;
     memset(&d, 0, sizeof(d));
@@ -1726,10 +1754,20 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
     a.jobs = d_jobs;
     a.njobs = d_njobs;
     a.max_jobs = max_jobs;
+    a.job_base = d_jb;
+    a.job_owner = d_jo;
     a.dbg = nullptr;
-    hipMemsetAsync(d_njobs, 0, 16, s);
-    rc = pq_launch(0, &a, s);
+    PageInfo *d_info = nullptr;
+    rc |= alloc_dev((void **)&d_info, sizeof(PageInfo));
+    hipMemset(d_info, 0, sizeof(PageInfo));
+    a.info = d_info;
+    rc |= pq_launch(0, &a, s);
     rc |= pq_launch(6, &a, s);
+    hipStreamSynchronize(s);
+    PageInfo hi;
+    hipMemcpy(&hi, d_info, sizeof(hi), hipMemcpyDeviceToHost);
+    if (hi.alias1 && expect) hipMemcpy(d_out, d_in + (hi.alias1 - 1), expect, hipMemcpyDeviceToDevice);
+    hipFree(d_info);
     hipStreamSynchronize(s);
     hipMemcpy(&st, d_st, 4, hipMemcpyDeviceToHost);
     *code = st == STATUS_OK ? 0 : (int)(st & 0xffff);
@@ -1742,6 +1780,8 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
   hipFree(d_list);
   hipFree(d_jobs);
   hipFree(d_njobs);
+  hipFree(d_jb);
+  hipFree(d_jo);
   if (rc) {
     set_err("device snappy failed");
     return PQG_ERR_DEVICE;

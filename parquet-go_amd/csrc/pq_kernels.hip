@@ -38,9 +38,11 @@ struct KArgs {
   const int32_t *list;    // page indices handled by this launch
   int32_t nlist;
   int32_t ncols;
-  CopyJob *jobs;          // long Snappy literals deferred to k_copy
-  uint32_t *njobs;
-  uint32_t max_jobs;
+  CopyJob *jobs;          // long Snappy literals deferred to k_copy, in per-page regions
+  uint32_t *njobs;        // per Snappy-list position: jobs written this decode
+  uint32_t max_jobs;      // total job slots
+  const int32_t *job_base;   // per Snappy-list position: first slot of its region
+  const int32_t *job_owner;  // per slot: Snappy-list position that owns it
   uint64_t *dbg;          // diagnostic build only (-DPQ_STAMPS): per-workgroup s_memtime stamps
 };
 
@@ -62,8 +64,16 @@ __device__ __forceinline__ uint32_t page_status(const uint32_t *status, int page
   return ufirst(__atomic_load_n(&status[page], __ATOMIC_RELAXED));
 }
 
-__device__ __forceinline__ const uint8_t *body_ptr(const KArgs &a, const PageDesc &d) {
-  return d.body_src == BODY_RAW ? a.in + d.body : a.stage + d.body;
+// Values section of page `idx`.  A Snappy block that is a single literal is
+// its own content: k_snappy then leaves it in place (PageInfo.alias1) instead
+// of copying it to staging.
+__device__ __forceinline__ const uint8_t *body_ptr(const KArgs &a, const PageDesc &d, int idx) {
+  if (d.body_src == BODY_RAW) return a.in + d.body;
+  if (d.body_src == BODY_SNAPPY) {
+    const int64_t al = a.info[idx].alias1;
+    if (al) return a.in + (al - 1);
+  }
+  return a.stage + d.body;
 }
 
 // ===========================================================================
@@ -183,7 +193,7 @@ __device__ __forceinline__ void ring_fill(const uint8_t *s, int64_t dpos, int64_
   if (t0 + lane < q_end) ring[(t0 + lane) & RING_MASK] = s[t0 + lane - dpos];
 }
 
-constexpr int64_t BIG_LITERAL = 64 * 1024;  // longer literals are copied by k_copy (many workgroups)
+constexpr int64_t BIG_LITERAL = 16 * 1024;  // longer literals are copied by k_copy (many workgroups)
 constexpr int MAX_DEFER = 64;  // one entry per lane
 
 __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
@@ -194,6 +204,7 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
   if (gi >= a.nlist) return;
   const int page = ufirst(a.list[gi]);
   const PageDesc d = a.pages[page];
+  if (a.max_jobs > 0 && lane == 0) a.njobs[gi] = 0u;  // no deferred jobs unless written below
   if (page_status(a.status, page) < make_status(ST_DECOMPRESS, 0)) return;
   uint8_t *ring = ring_all[wv];
 
@@ -232,6 +243,30 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
   // decoder (validate only, no stores) to tell ErrCorrupt from a size mismatch
   const bool write = dlen == (uint64_t)expect;
   const int64_t dl = (int64_t)dlen;
+  // a block that is exactly one literal is its own content: leave it in place
+  if (write && lane == 0) a.info[page].alias1 = 0;
+  // (data pages only: dictionaries stay in 16-byte aligned staging for aligned gathers)
+  if (write && dl > 0 && s < slen && d.kind != PAGE_DICT) {
+    uint32_t tag = W.byte_at(src + s);
+    if ((tag & 3) == 0) {
+      uint32_t x = tag >> 2;
+      int64_t hs = 1;
+      bool ok = true;
+      if (x >= 60) {
+        int extra = (int)x - 59;
+        hs = 1 + extra;
+        if (s + hs > slen) ok = false;
+        else {
+          x = 0;
+          for (int k = 0; k < extra; k++) x |= W.byte_at(src + s + 1 + k) << (8 * k);
+        }
+      }
+      if (ok && (int64_t)x + 1 == dl && s + hs + dl == slen) {
+        if (lane == 0) a.info[page].alias1 = 1 + (int64_t)(d.src + lsize + s + hs);
+        return;
+      }
+    }
+  }
   int64_t dpos = 0;
   uint32_t err = E_OK;
   int ndefer = 0;                      // deferred literals: lane k holds entry k
@@ -264,10 +299,10 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
       if (write) {
         bool deferred = false;
         if (length >= BIG_LITERAL && ndefer < MAX_DEFER && a.max_jobs > 0) {
-          uint32_t slot = 0;
-          if (lane == 0) slot = atomicAdd(a.njobs, 1u);
-          slot = ufirst(slot);
-          if (slot < a.max_jobs) {
+          // deterministic slot in this page's region (sized by the host: body_len / BIG_LITERAL)
+          const uint32_t slot = (uint32_t)(a.job_base[gi] + ndefer);
+          const uint32_t region_end = (gi + 1 < a.nlist) ? (uint32_t)a.job_base[gi + 1] : a.max_jobs;
+          if (slot < region_end) {
             if (lane == 0) a.jobs[slot] = CopyJob{src + s, dst + dpos, length};
             // remember it: far copies that land inside read the literal from the payload
             if (lane == ndefer) {
@@ -292,6 +327,41 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
       }
       dpos += length;
       s += length;
+      if (write && pend_len == length && pend_dpos + length == dpos) {
+        // speculative skip: an incompressible region is a train of identical
+        // maximal literals (same tag bytes, same length); lane k checks the
+        // k-th next token and the matching prefix is deferred in one step
+        const int64_t hs = (int64_t)((tag >> 2) < 60 ? 1 : 1 + (int)(tag >> 2) - 59);
+        const int64_t stride = hs + length;
+        const int64_t cs = s + (int64_t)lane * stride;  // candidate tag position
+        const uint32_t region_end = (gi + 1 < a.nlist) ? (uint32_t)a.job_base[gi + 1] : a.max_jobs;
+        bool ok = ndefer + lane < MAX_DEFER && (uint32_t)(a.job_base[gi] + ndefer + lane) < region_end &&
+                  cs + stride <= slen && dpos + (int64_t)(lane + 1) * length <= dl;
+        if (ok) {
+          const uint8_t *t0 = src + s - stride;  // the accepted token's tag
+          for (int q = 0; q < hs; q++) ok &= src[cs + q] == t0[q];
+        }
+        const uint64_t okm = ballot(ok);
+        const int m = (int)__builtin_ctzll(~okm);
+        if (m > 0) {
+          if (lane < m) {
+            a.jobs[a.job_base[gi] + ndefer + lane] = CopyJob{src + cs + hs, dst + dpos + (int64_t)lane * length, length};
+          }
+          // deferred-literal table: lane ndefer + k holds candidate k
+          const int k = lane - ndefer;
+          if (k >= 0 && k < m) {
+            def_dst = dpos + (int64_t)k * length;
+            def_len = length;
+            def_src = (uint64_t)(uintptr_t)(src + s + (int64_t)k * stride + hs);
+          }
+          ndefer += m;
+          pend_src = src + s + (int64_t)(m - 1) * stride + hs;
+          pend_dpos = dpos + (int64_t)(m - 1) * length;
+          pend_len = length;
+          dpos += (int64_t)m * length;
+          s += (int64_t)m * stride;
+        }
+      }
       continue;
     }
     if ((tag & 3) == 1) {  // copy1
@@ -363,6 +433,7 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
   }
   if (err == E_OK && dpos != dl) err = E_SNAPPY;
   if (err == E_OK && !write) err = E_SIZE;  // compress.go:117-119
+  if (a.max_jobs > 0 && lane == 0) a.njobs[gi] = err ? 0u : (uint32_t)ndefer;
   if (err) set_status(a.status, page, ST_DECOMPRESS, err);
 }
 
@@ -374,7 +445,9 @@ constexpr int COPY_TILE = 4096;  // bytes per workgroup step (256 lanes x 16 B)
 __global__ __launch_bounds__(256) void k_copy(KArgs a) {
   // one workgroup per job (google/Go snappy literals are <= 64 KB; longer ones loop)
   const uint32_t j = blockIdx.x;
-  if (j >= min(*a.njobs, a.max_jobs)) return;
+  if (j >= a.max_jobs) return;
+  const int32_t q = a.job_owner[j];
+  if ((uint32_t)(j - a.job_base[q]) >= a.njobs[q]) return;
   const CopyJob job = a.jobs[j];
   const int t = threadIdx.x;
   const uintptr_t d0 = (uintptr_t)job.dst, d1 = d0 + (uintptr_t)job.len;
@@ -417,7 +490,7 @@ __global__ __launch_bounds__(256) void k_dict_prepare(KArgs a) {
   const PageDesc d = a.pages[page];
   if (page_status(a.status, page) != STATUS_OK) return;
   const ColDesc c = a.cols[d.col];
-  const uint8_t *body = body_ptr(a, d);
+  const uint8_t *body = body_ptr(a, d, page);
   const int64_t n = d.num_values, len = d.body_len;
   if (c.ptype != T_BYTE_ARRAY) {
     if (n * (int64_t)c.width > len) set_status(a.status, page, ST_DICT_VALUES, E_EOF);
@@ -463,8 +536,9 @@ struct PageStreams {
 
 // V1: [u32 len][rep RLE] [u32 len][def RLE] values  (page_v1.go:99-107, hybrid_decoder.go:57-67)
 // V2: rep bytes, def bytes raw in the payload; values section decompressed separately
-__device__ uint32_t layout(const KArgs &a, const PageDesc &d, const ColDesc &c, PageStreams &ps, uint32_t &stage) {
-  ps.body = body_ptr(a, d);
+__device__ uint32_t layout(const KArgs &a, const PageDesc &d, int page, const ColDesc &c, PageStreams &ps,
+                       uint32_t &stage) {
+  ps.body = body_ptr(a, d, page);
   const int64_t blen = d.body_len;
   if (d.kind == PAGE_V1) {
     ps.lvl = ps.body;
@@ -524,7 +598,7 @@ __global__ __launch_bounds__(256) void k_prepare(KArgs a) {
   const ColDesc c = a.cols[d.col];
   PageStreams ps;
   uint32_t stage = ST_REP_INIT;
-  uint32_t e = layout(a, d, c, ps, stage);
+  uint32_t e = layout(a, d, page, c, ps, stage);
   if (e) {
     set_status(a.status, page, stage, e);
     return;
@@ -779,8 +853,8 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
   const int n = d.num_values;
   if (n == 0) return;
 
-  const uint8_t *lvl = d.kind == PAGE_V1 ? body_ptr(a, d) : a.in + d.src;
-  const uint8_t *vals = body_ptr(a, d) + pi.val_off;
+  const uint8_t *lvl = d.kind == PAGE_V1 ? body_ptr(a, d, page) : a.in + d.src;
+  const uint8_t *vals = body_ptr(a, d, page) + pi.val_off;
   const int64_t vlen = pi.val_len;
   const int w = c.width;
   const bool flat = c.max_rep == 0;
@@ -799,7 +873,7 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
   if (d.enc == ENC_RLE_DICT) {
     keys.init(vals + 1, vlen - 1, pi.idx_bw);
     if (dp) {
-      dict_vals = body_ptr(a, *dp);
+      dict_vals = body_ptr(a, *dp, d.dict);
       dict_n = dp->num_values;
       dict_base = dp->dict_base;
     }
@@ -1204,7 +1278,7 @@ __global__ __launch_bounds__(256) void k_decode_flat(KArgs a) {
   const PageInfo pi = a.info[page];
   const int n = d.num_values;
   if (n == 0) return;
-  const uint8_t *vals = body_ptr(a, d) + pi.val_off;
+  const uint8_t *vals = body_ptr(a, d, page) + pi.val_off;
   const int64_t vlen = pi.val_len;
   const int w = c.width;  // 4 or 8
   uint8_t *out = c.values + d.level_base * w;
@@ -1225,7 +1299,7 @@ __global__ __launch_bounds__(256) void k_decode_flat(KArgs a) {
     set_status(a.status, page, ST_VALUES, E_DICT);
     return;
   }
-  const uint8_t *dict = body_ptr(a, *dp);
+  const uint8_t *dict = body_ptr(a, *dp, d.dict);
   const int64_t dict_n = dp->num_values;
   const int bw = pi.idx_bw;
 
@@ -1428,7 +1502,7 @@ struct RunEnt {
 };
 
 // DW_STREAM: staged key-stream bytes per workgroup.  Three instantiations
-// (8 / 24 / 56 KB) so small pages do not pay the LDS (occupancy) of big ones;
+// (8 / 31 / 56 KB) so small pages do not pay the LDS (occupancy) of big ones;
 // the host routes each page by its body length.
 template <int DW_STREAM>
 __global__ __launch_bounds__(256) void k_decode_dict_wg(KArgs a) {
@@ -1449,13 +1523,13 @@ __global__ __launch_bounds__(256) void k_decode_dict_wg(KArgs a) {
   const PageInfo pi = a.info[page];
   const int n = (int)ufirst((uint32_t)d.num_values);
   if (n == 0) return;
-  const uint8_t *vals = body_ptr(a, d) + pi.val_off;
+  const uint8_t *vals = body_ptr(a, d, page) + pi.val_off;
   const int64_t slen = ufirst64((int64_t)pi.val_len - 1);  // key stream after the bit-width byte
   const uint8_t *ks = vals + 1;
   const int w = (int)ufirst((uint32_t)c.width);
   uint8_t *out = c.values + d.level_base * w;
   const PageDesc dp = a.pages[d.dict];
-  const uint8_t *dict = body_ptr(a, dp);
+  const uint8_t *dict = body_ptr(a, dp, d.dict);
   const int64_t dict_n = ufirst64(dp.num_values);
   const int bw = (int)ufirst((uint32_t)pi.idx_bw);
   const bool aligned_dict = (((uintptr_t)dict) & (w - 1)) == 0;
@@ -1723,7 +1797,7 @@ __global__ __launch_bounds__(256) void k_level_check(KArgs a) {
   const ColDesc c = a.cols[d.col];
   const PageInfo pi = a.info[page];
   const int n = d.num_values;
-  const uint8_t *lvl = d.kind == PAGE_V1 ? body_ptr(a, d) : a.in + d.src;
+  const uint8_t *lvl = d.kind == PAGE_V1 ? body_ptr(a, d, page) : a.in + d.src;
   if (c.max_rep > 0) {
     Hyb rep;
     rep.init(lvl + pi.rep_off, pi.rep_len, bits_len(c.max_rep));
@@ -1771,6 +1845,8 @@ struct pq_launch_args {
   void *jobs;
   uint32_t *njobs;
   uint32_t max_jobs;
+  const int32_t *job_base;
+  const int32_t *job_owner;
   uint64_t *dbg;
 };
 
@@ -1789,6 +1865,8 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   k.jobs = (pq::CopyJob *)p->jobs;
   k.njobs = p->njobs;
   k.max_jobs = p->max_jobs;
+  k.job_base = p->job_base;
+  k.job_owner = p->job_owner;
   k.dbg = p->dbg;
   return k;
 }
@@ -1815,7 +1893,7 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     case 5: hipLaunchKernelGGL(pq::k_level_check, grid, block, 0, s, k); break;
     case 7: hipLaunchKernelGGL(pq::k_decode_flat, grid, block, 0, s, k); break;
     case 8: hipLaunchKernelGGL(pq::k_decode_dict_wg<8 * 1024>, dim3(k.nlist), block, 0, s, k); break;
-    case 9: hipLaunchKernelGGL(pq::k_decode_dict_wg<24 * 1024>, dim3(k.nlist), block, 0, s, k); break;
+    case 9: hipLaunchKernelGGL(pq::k_decode_dict_wg<31 * 1024>, dim3(k.nlist), block, 0, s, k); break;
     case 10: hipLaunchKernelGGL(pq::k_decode_dict_wg<56 * 1024>, dim3(k.nlist), block, 0, s, k); break;
     default: return 1;
   }
