@@ -149,7 +149,7 @@ def main():
     # algorithmic bytes per launch of each kernel
     alg = {
         "k_snappy+k_copy": stats["input_bytes"] + stats["staged_bytes"],     # compressed in + uncompressed out
-        "k_decode+k_decode_flat": stats["staged_bytes"] + out_b,                    # encoded indices in + decoded values out
+        "k_decode+k_expand": in_b + out_b,                                         # encoded pages in + decoded values out
     }
     ach = alg.get(dom, in_b + out_b) / (avg[dom] * 1e-3) / 1e9
     line = {

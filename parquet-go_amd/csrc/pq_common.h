@@ -62,7 +62,30 @@ struct PageDesc {
   int32_t v2_def_len;    // V2: def level bytes at src + v2_rep_len
   int64_t level_base;    // first level entry of the page inside its column (flat slot base)
   int64_t dict_base;     // BYTE_ARRAY dictionary page: first entry in the dict offsets scratch
+  int64_t run_base;      // tiled RLE_DICTIONARY page: first entry of its run table (k_runs -> k_expand)
+  int32_t run_cap;       // run-table entries reserved for the page (runs + sentinel)
+  int32_t tile_base;     // tiled page: first entry of its tile -> first-run index table
 };
+
+// Tiled flat decode (k_prepare's run walk + k_expand).  The run walk records,
+// per RUN_TILE values of a page, the run holding the first of them; a k_expand
+// workgroup takes 4 waves x EX_WAVE_VALUES consecutive values of one page.
+constexpr int RUN_TILE = 512;
+constexpr int EX_WAVE_VALUES = 2048;
+struct TileJob {         // one k_expand workgroup (host-built, XCD-affine order)
+  uint8_t *out;          // the page's first output value
+  int32_t page;          // PageDesc index
+  int32_t dict;          // its dictionary page, -1 if none
+  int32_t v0;            // first value of the job (page-relative)
+  int32_t tf;            // tile_first index of the job's first value (RUN_TILE granularity)
+  int32_t width;         // value bytes (4 / 8)
+  int32_t pad;
+};
+// One RLE/bit-packed run of a key stream (hybrid_decoder.go:143-166), as
+// written by k_runs: x = first value (page-relative) | RUN_RLE for an RLE run;
+// y = the repeated value (RLE) or the byte offset of the run's packed data in
+// the key stream (bit-packed).
+constexpr uint32_t RUN_RLE = 0x80000000u;
 
 struct ColDesc {
   int32_t ptype, width;        // physical type, bytes per value (0 = BYTE_ARRAY)
@@ -91,6 +114,9 @@ struct PageInfo {
   int64_t rows, slots, non_null, str_bytes;  // counts (prepare)
   int64_t row_base, slot_base, str_base;     // exclusive scans over the column's pages
   int64_t alias1;  // k_snappy: 1 + input offset of the body when the block is one literal (0: none)
+  int32_t cover;      // k_runs: values decodable before the first key-stream header error (n when none)
+  uint32_t walk_err;  // k_runs: that header error (0: none); applied by k_level_check unless a
+                      // dictionary error among the first `cover` values came first
 };
 
 }  // namespace pq

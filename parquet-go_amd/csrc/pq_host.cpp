@@ -49,6 +49,12 @@ struct pq_launch_args {
   const int32_t *job_base;
   const int32_t *job_owner;
   uint64_t *dbg;
+  void *runs;
+  void *tile_info;
+  const void *tiles;
+  int32_t ntiles, ntiles4;
+  int32_t ex_lds;
+  int32_t gather_aux;
 };
 int pq_launch(int which, const pq_launch_args *p, hipStream_t s);
 }
@@ -498,8 +504,9 @@ struct pqg_batch {
   std::vector<PageDesc> pages;
   std::vector<uint32_t> status0;  // host-side initial status per page
   std::vector<int32_t> snappy_list, dict_list, data_list;
-  std::vector<int32_t> general_list, flat_list;  // data pages for k_decode / k_decode_flat
-  std::vector<int32_t> dictwg_list[3];            // k_decode_dict_wg<8K / 31K / 56K>
+  std::vector<int32_t> general_list;  // data pages for k_decode (wave per page)
+  std::vector<TileJob> tiles;         // k_expand work list (XCD-affine order)
+  int64_t run_entries = 0, tile_entries = 0;
   bool any_count = false;
   std::vector<ChunkError> chunk_errors;
   int64_t input_bytes = 0, staged_bytes = 0, h2d_bytes = 0, host_inflated = 0, dict_entries = 0;
@@ -516,12 +523,18 @@ struct pqg_batch {
   int32_t *d_job_base = nullptr, *d_job_owner = nullptr;
   uint32_t max_jobs = 0;
   uint64_t *d_dbg = nullptr;     // diagnostic stamps (PQ_STAMPS builds only)
+  void *d_runs = nullptr;        // run tables (k_prepare's run walk -> k_expand)
+  void *d_tile_info = nullptr;     // per RUN_TILE values of a tiled page: {first run, first key byte}
+  int32_t ex_lds = 0;              // k_expand staged key bytes per wave
+  int32_t ntiles4 = 0;             // k_expand jobs of 4-byte columns (they come first)
+  TileJob *d_tiles = nullptr;
   uint32_t *h_status = nullptr;  // pinned mirror
   std::vector<ColDesc> hcols;
   // timing: a ring of event sets, one per decode, harvested by pqg_batch_kernel_times
   static constexpr int kRing = 64;
   hipEvent_t ev[kRing][8] = {};
   int nev = 0;
+  bool seg_times = false;  // PQG_SEGMENT_TIMES=1: events between every phase (adds launch gaps)
   int ring_head = 0, ring_count = 0;
   double kms_sum[8] = {};
   int kms_n = 0;
@@ -529,8 +542,10 @@ struct pqg_batch {
   bool decoded = false;
 };
 
-static const char *kKernelNames[] = {"k_snappy+k_copy", "k_dict_prepare", "k_prepare", "k_scan", "k_decode+k_decode_flat",
-                                     "k_level_check"};
+// timed segments: with PQG_SEGMENT_TIMES every phase, otherwise the decode phase only
+static const char *kSegNames[] = {"k_snappy+k_copy", "k_dict_prepare", "k_prepare", "k_scan", "k_decode+k_expand",
+                                  "k_level_check"};
+static const char *kDecodeName[] = {"k_decode+k_expand"};
 
 #define HIPCHK(x)                                                                 \
   do {                                                                            \
@@ -948,7 +963,7 @@ struct HostBuf {  // growable host staging for the input upload / host-inflated 
     return off;
   }
 };
-constexpr size_t kPad = 1024;  // readable slack after every device buffer
+constexpr size_t kPad = 4096;  // readable slack after every device buffer (1 KiB register windows)
 }  // namespace
 
 static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t, std::vector<uint8_t>>> &host_bodies,
@@ -1176,6 +1191,10 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   B->rg_begin = rg_begin;
   B->rg_end = rg_end;
   B->flags = flags;
+  {
+    const char *st = getenv("PQG_SEGMENT_TIMES");
+    B->seg_times = st && st[0] == '1';
+  }
   std::vector<int> sel;
   if (nleaves == 0 || !leaves) {
     for (int i = 0; i < (int)f->leaves.size(); i++) sel.push_back(i);
@@ -1210,49 +1229,72 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
     B->cols[ci].page_end = (int32_t)B->pages.size();
   }
   const size_t npages = B->pages.size();
-  // route data pages: flat required fixed-width PLAIN / RLE_DICTIONARY pages take the fast kernel
+  // route data pages: flat required fixed-width PLAIN / RLE_DICTIONARY pages
+  // take the tiled path (run walk in k_prepare + k_expand), everything else k_decode
+  std::vector<std::vector<TileJob>> chunk_tiles;  // tiles grouped by column chunk (one dictionary)
+  int32_t last_chunk_key = -1;
   for (int32_t pi : B->data_list) {
-    const PageDesc &d = B->pages[(size_t)pi];
+    PageDesc &d = B->pages[(size_t)pi];
     const ColumnPlan &cp = B->cols[(size_t)d.col];
     const pqg_column_info &L = cp.info;
-    bool fast = L.max_rep == 0 && L.max_def == 0 && (L.value_width == 4 || L.value_width == 8) &&
-                L.physical_type != T_BYTE_ARRAY && !(cp.flags & COL_EMIT_LEVELS) &&
-                (d.enc == ENC_PLAIN || d.enc == ENC_RLE_DICT);
-    // V1 required pages have no level streams, so the key stream is body_len - 1 bytes
-    bool wg = fast && d.enc == ENC_RLE_DICT && d.kind == PAGE_V1 && d.body_len <= 56 * 1024 - 32;
-    if (wg) {
-      int cls = d.body_len <= 8 * 1024 - 32 ? 0 : d.body_len <= 31 * 1024 - 32 ? 1 : 2;
-      B->dictwg_list[cls].push_back(pi);
-    } else {
-      (fast ? B->flat_list : B->general_list).push_back(pi);
+    bool tiled = L.max_rep == 0 && L.max_def == 0 && (L.value_width == 4 || L.value_width == 8) &&
+                 L.physical_type != T_BYTE_ARRAY && !(cp.flags & COL_EMIT_LEVELS) &&
+                 (d.enc == ENC_PLAIN || d.enc == ENC_RLE_DICT);
+    if (!tiled) {
+      B->general_list.push_back(pi);
+      continue;
     }
+    const int32_t n = std::max(d.num_values, 0);
+    const int32_t nt = (n + RUN_TILE - 1) / RUN_TILE;
+    d.tile_base = (int32_t)B->tile_entries;
+    B->tile_entries += nt;
+    if (d.enc == ENC_RLE_DICT) {
+      // every run holds >= 1 value and >= 2 key-stream bytes (bit width >= 1), so
+      // runs <= min(n, len / 2 + 1); + the sentinel
+      d.run_base = B->run_entries;
+      d.run_cap = (int32_t)std::min<int64_t>(n, (int64_t)d.body_len / 2 + 1) + 2;
+      B->run_entries += d.run_cap;
+      // staged key bytes of a wave: the page's bytes per value x EX_WAVE_VALUES (+ slack);
+      // denser spots fall back to direct loads
+      if (n > 0) {
+        const int64_t need = ((int64_t)d.body_len * EX_WAVE_VALUES + n - 1) / n + 96;
+        B->ex_lds = (int32_t)std::max<int64_t>(B->ex_lds, std::min<int64_t>(need, EX_WAVE_VALUES * 4 + 256));
+      }
+    }
+    const int32_t key = d.dict >= 0 ? d.dict : -2 - d.col * 1000003 - d.rg;
+    if (chunk_tiles.empty() || key != last_chunk_key) chunk_tiles.emplace_back();
+    last_chunk_key = key;
+    // output pointer and width are filled in once the outputs exist
+    for (int32_t v = 0; v < n; v += EX_WAVE_VALUES)
+      chunk_tiles.back().push_back(TileJob{nullptr, pi, d.dict, v, d.tile_base + v / RUN_TILE, 0, 0});
   }
   for (auto &cp : B->cols) B->any_count |= (cp.flags & COL_NEEDS_COUNT) != 0;
+  // 4-byte columns' jobs first (k_expand<4>), then 8-byte ones (k_expand<8>).
   // XCD affinity (speed only, never correctness): workgroups b and b + 8 share an
   // XCD's L2 under round-robin dispatch, so deal whole chunks (one dictionary
-  // each) to the 8 block residues, balanced by page count, then interleave.
-  for (int c = 0; c < 3; c++) {
-    std::vector<int32_t> &L = B->dictwg_list[c];
-    if (L.size() < 16) continue;
-    std::vector<std::vector<int32_t>> x(8);
-    size_t i = 0;
-    while (i < L.size()) {
-      size_t j = i;
-      while (j < L.size() && B->pages[(size_t)L[j]].dict == B->pages[(size_t)L[i]].dict) j++;
+  // each) to the 8 block residues, balanced by job count, then interleave four
+  // jobs (one workgroup) at a time.
+  auto is4 = [&](const std::vector<TileJob> &ct) {
+    return ct.empty() || B->cols[(size_t)B->pages[(size_t)ct[0].page].col].info.value_width == 4;
+  };
+  auto mid = std::stable_partition(chunk_tiles.begin(), chunk_tiles.end(), is4);
+  auto deal = [&](std::vector<std::vector<TileJob>>::iterator b, std::vector<std::vector<TileJob>>::iterator e) {
+    std::vector<std::vector<TileJob>> x(8);
+    for (auto it = b; it != e; ++it) {
       size_t best = 0;
       for (size_t q = 1; q < 8; q++)
         if (x[q].size() < x[best].size()) best = q;
-      x[best].insert(x[best].end(), L.begin() + (long)i, L.begin() + (long)j);
-      i = j;
+      x[best].insert(x[best].end(), it->begin(), it->end());
     }
-    std::vector<int32_t> out;
     size_t maxlen = 0;
     for (auto &v : x) maxlen = std::max(maxlen, v.size());
-    for (size_t r = 0; r < maxlen; r++)
+    for (size_t r = 0; r < maxlen; r += 4)
       for (size_t q = 0; q < 8; q++)
-        if (r < x[q].size()) out.push_back(x[q][r]);
-    L.swap(out);
-  }
+        for (size_t k = r; k < r + 4 && k < x[q].size(); k++) B->tiles.push_back(x[q][k]);
+  };
+  deal(chunk_tiles.begin(), mid);
+  B->ntiles4 = (int32_t)B->tiles.size();
+  deal(mid, chunk_tiles.end());
 
   // device buffers
   int rc = 0;
@@ -1266,6 +1308,10 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   rc |= alloc_dev((void **)&B->d_dict, sizeof(uint64_t) * (size_t)B->dict_entries);
   size_t nl = B->snappy_list.size() + B->dict_list.size() + 2 * B->data_list.size() + 16;
   rc |= alloc_dev((void **)&B->d_lists, sizeof(int32_t) * nl);
+  rc |= alloc_dev(&B->d_runs, 8 * (size_t)(B->run_entries + 64));
+  rc |= alloc_dev(&B->d_tile_info, 8 * (size_t)(B->tile_entries + EX_WAVE_VALUES / RUN_TILE + 1));
+  B->ex_lds = (B->ex_lds + 255) & ~255;
+  rc |= alloc_dev((void **)&B->d_tiles, sizeof(TileJob) * (B->tiles.size() + 1));
   // per Snappy page a region of job slots: at most body_len / 16 KB literals are long enough to defer
   std::vector<int32_t> job_base(B->snappy_list.size() + 1), job_owner;
   for (size_t q = 0; q < B->snappy_list.size(); q++) {
@@ -1283,7 +1329,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
     if (!job_owner.empty()) hipMemcpy(B->d_job_owner, job_owner.data(), 4 * job_owner.size(), hipMemcpyHostToDevice);
   }
 #ifdef PQ_STAMPS
-  rc |= alloc_dev((void **)&B->d_dbg, sizeof(uint64_t) * 8 * (B->data_list.size() + 1));
+  rc |= alloc_dev((void **)&B->d_dbg, sizeof(uint64_t) * 8 * 4 * (B->tiles.size() + 1));
 #endif
   if (rc) {
     pqg_batch_destroy(B);
@@ -1322,8 +1368,6 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
     lists.insert(lists.end(), B->dict_list.begin(), B->dict_list.end());
     lists.insert(lists.end(), B->data_list.begin(), B->data_list.end());
     lists.insert(lists.end(), B->general_list.begin(), B->general_list.end());
-    lists.insert(lists.end(), B->flat_list.begin(), B->flat_list.end());
-    for (int c = 0; c < 3; c++) lists.insert(lists.end(), B->dictwg_list[c].begin(), B->dictwg_list[c].end());
     if (!lists.empty()) HIPCHK(hipMemcpy(B->d_lists, lists.data(), sizeof(int32_t) * lists.size(), hipMemcpyHostToDevice));
   }
   memcpy(B->h_status, B->status0.data(), sizeof(uint32_t) * npages);
@@ -1410,6 +1454,15 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   }
   if (!B->cols.empty())
     HIPCHK(hipMemcpy(B->d_cols, B->hcols.data(), sizeof(ColDesc) * B->cols.size(), hipMemcpyHostToDevice));
+  // k_expand jobs: output pointers now that the outputs exist
+  for (TileJob &tj : B->tiles) {
+    const PageDesc &d = B->pages[(size_t)tj.page];
+    const ColDesc &c = B->hcols[(size_t)d.col];
+    tj.width = c.width;
+    tj.out = c.values + d.level_base * (int64_t)c.width;
+  }
+  if (!B->tiles.empty())
+    HIPCHK(hipMemcpy(B->d_tiles, B->tiles.data(), sizeof(TileJob) * B->tiles.size(), hipMemcpyHostToDevice));
   for (int k = 0; k < pqg_batch::kRing; k++)
     for (int i = 0; i < 8; i++) hipEventCreate(&B->ev[k][i]);
   *out = B;
@@ -1428,7 +1481,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
       if (cp.list_validity) HIPCHK(hipMemsetAsync(cp.list_validity, 0, cp.list_val_bytes, s));
     }
   }
-  pq_launch_args a;
+  pq_launch_args a = {};
   a.in = B->d_in;
   a.stage = B->d_stage;
   a.pages = B->d_pages;
@@ -1443,56 +1496,50 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.job_base = B->d_job_base;
   a.job_owner = B->d_job_owner;
   a.dbg = B->d_dbg;
+  a.runs = B->d_runs;
+  a.tile_info = B->d_tile_info;
+  a.ex_lds = B->ex_lds;
+  a.gather_aux = getenv("PQG_GATHER_AUX") ? atoi(getenv("PQG_GATHER_AUX")) : 0;
+  a.tiles = B->d_tiles;
+  a.ntiles = (int32_t)B->tiles.size();
+  a.ntiles4 = B->ntiles4;
   const int32_t ns = (int32_t)B->snappy_list.size(), nd = (int32_t)B->dict_list.size(),
-                ndata = (int32_t)B->data_list.size();
+                ndata = (int32_t)B->data_list.size(), ngen = (int32_t)B->general_list.size();
   int e = 0;
   B->nev = 0;
   hipEvent_t *evs = B->ev[B->ring_head];
-  auto mark = [&]() {
-    if (timed) hipEventRecord(evs[B->nev++], s);
+  // events cost a gap between dependent kernels: by default only the decode
+  // phase is bracketed (the roofline kernel), PQG_SEGMENT_TIMES=1 brackets all
+  auto mark = [&](bool decode_edge) {
+    if (timed && (B->seg_times || decode_edge)) hipEventRecord(evs[B->nev++], s);
   };
-  mark();
+  mark(false);
   a.list = B->d_lists;
   a.nlist = ns;
   e |= pq_launch(0, &a, s);
   e |= pq_launch(6, &a, s);  // k_copy: long literals, timed together with k_snappy
-  mark();
+  mark(false);
   a.list = B->d_lists + ns;
   a.nlist = nd;
   e |= pq_launch(1, &a, s);
-  mark();
+  mark(false);
   a.list = B->d_lists + ns + nd;
   a.nlist = ndata;
-  e |= pq_launch(2, &a, s);
-  mark();
+  e |= pq_launch(2, &a, s);  // (+ the run walk of tiled RLE_DICTIONARY pages)
+  mark(false);
   if (B->any_count) e |= pq_launch(4, &a, s);  // scans only feed lists / strings
-  mark();
+  mark(true);
   if (!upto_scan) {
-    const int32_t ngen = (int32_t)B->general_list.size(), nflat = (int32_t)B->flat_list.size();
     a.list = B->d_lists + ns + nd + ndata;
     a.nlist = ngen;
     e |= pq_launch(3, &a, s);
-    a.list = B->d_lists + ns + nd + ndata + ngen;
-    a.nlist = nflat;
-    e |= pq_launch(7, &a, s);
-    // size classes, largest pages first (they have the longest tails)
-    int32_t offs[3], cnt[3];
-    int32_t off = ns + nd + ndata + ngen + nflat;
-    for (int c = 0; c < 3; c++) {
-      offs[c] = off;
-      cnt[c] = (int32_t)B->dictwg_list[c].size();
-      off += cnt[c];
-    }
-    for (int c = 2; c >= 0; c--) {
-      a.list = B->d_lists + offs[c];
-      a.nlist = cnt[c];
-      e |= pq_launch(8 + c, &a, s);
-    }
-    mark();
+    a.nlist = (int32_t)B->tiles.size();
+    e |= pq_launch(8, &a, s);  // k_expand
+    mark(true);
     a.list = B->d_lists + ns + nd;
     a.nlist = ndata;
     e |= pq_launch(5, &a, s);
-    mark();
+    mark(false);
   }
   if (e) {
     set_err("kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
@@ -1661,7 +1708,7 @@ int pqg_batch_kernel_times(pqg_batch *B, const char **names, float *ms, int cap)
     B->ring_count = 0;
   }
   for (int i = 0; i < n && i < cap; i++) {
-    if (names) names[i] = kKernelNames[i];
+    if (names) names[i] = B->seg_times ? kSegNames[i] : kDecodeName[i];
     if (ms) ms[i] = B->kms_n ? (float)(B->kms_sum[i] / B->kms_n) : 0.f;
   }
   return n;
@@ -1693,6 +1740,9 @@ void pqg_batch_destroy(pqg_batch *B) {
   hipFree(B->d_job_base);
   hipFree(B->d_job_owner);
   hipFree(B->d_dbg);
+  hipFree(B->d_runs);
+  hipFree(B->d_tile_info);
+  hipFree(B->d_tiles);
   if (B->h_status) hipHostFree(B->h_status);
   for (int k = 0; k < pqg_batch::kRing; k++)
     for (int i = 0; i < 8; i++)
@@ -1743,7 +1793,7 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
     hipMemcpy(d_page, &d, sizeof(d), hipMemcpyHostToDevice);
     hipMemcpy(d_st, &st, 4, hipMemcpyHostToDevice);
     hipMemcpy(d_list, &zero, 4, hipMemcpyHostToDevice);
-    pq_launch_args a;
+    pq_launch_args a = {};
     memset(&a, 0, sizeof(a));
     a.in = d_in;
     a.stage = d_out;
@@ -1793,7 +1843,7 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
 // diagnostic build only (not part of include/pqgpu.h): copy the stamp buffer
 extern "C" int pqg_diag_stamps(pqg_batch *B, uint64_t *out, size_t n) {
   hipStreamSynchronize(B->ctx->stream);
-  size_t cap = 8 * (B->data_list.size() + 1);
+  size_t cap = 8 * 4 * (B->tiles.size() + 1);
   if (n > cap) n = cap;
   return hipMemcpy(out, B->d_dbg, n * 8, hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
 }

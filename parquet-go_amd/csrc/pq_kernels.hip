@@ -16,6 +16,8 @@
 // window (pq_device.h).  Nothing here is a contraction, so no MFMA.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "pq_common.h"
 #include "pq_device.h"
 
@@ -44,12 +46,19 @@ struct KArgs {
   const int32_t *job_base;   // per Snappy-list position: first slot of its region
   const int32_t *job_owner;  // per slot: Snappy-list position that owns it
   uint64_t *dbg;          // diagnostic build only (-DPQ_STAMPS): per-workgroup s_memtime stamps
+  uint2 *runs;            // k_runs -> k_expand: run tables (PageDesc.run_base)
+  int2 *tile_info;        // per RUN_TILE values: {first run, byte of its first key} (PageDesc.tile_base)
+  int32_t ex_lds;         // k_expand: staged key bytes per wave (dynamic LDS)
+  int32_t gather_aux;     // experiment knob (PQG_GATHER_AUX)
+  const TileJob *tiles;   // k_expand: one workgroup per entry
 };
 
 #ifdef PQ_STAMPS
+// per-wave s_memrealtime (100 MHz) stamps: slot (blockIdx * 4 + wave) * 8 + i
 #define STAMP(i)                                                                              \
   do {                                                                                        \
-    if (a.dbg && threadIdx.x == 0) a.dbg[(size_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+    if (a.dbg && lane_id() == 0)                                                              \
+      a.dbg[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
 #define STAMP(i) \
@@ -245,8 +254,7 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
   const int64_t dl = (int64_t)dlen;
   // a block that is exactly one literal is its own content: leave it in place
   if (write && lane == 0) a.info[page].alias1 = 0;
-  // (data pages only: dictionaries stay in 16-byte aligned staging for aligned gathers)
-  if (write && dl > 0 && s < slen && d.kind != PAGE_DICT) {
+  if (write && dl > 0 && s < slen) {
     uint32_t tag = W.byte_at(src + s);
     if ((tag & 3) == 0) {
       uint32_t x = tag >> 2;
@@ -443,11 +451,10 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
 constexpr int COPY_TILE = 4096;  // bytes per workgroup step (256 lanes x 16 B)
 
 __global__ __launch_bounds__(256) void k_copy(KArgs a) {
-  // one workgroup per job (google/Go snappy literals are <= 64 KB; longer ones loop)
-  const uint32_t j = blockIdx.x;
-  if (j >= a.max_jobs) return;
+  // a workgroup per job, grid-strided (google/Go snappy literals are <= 64 KB; longer ones loop)
+  for (uint32_t j = blockIdx.x; j < a.max_jobs; j += gridDim.x) {
   const int32_t q = a.job_owner[j];
-  if ((uint32_t)(j - a.job_base[q]) >= a.njobs[q]) return;
+  if ((uint32_t)(j - a.job_base[q]) >= a.njobs[q]) continue;
   const CopyJob job = a.jobs[j];
   const int t = threadIdx.x;
   const uintptr_t d0 = (uintptr_t)job.dst, d1 = d0 + (uintptr_t)job.len;
@@ -476,6 +483,7 @@ __global__ __launch_bounds__(256) void k_copy(KArgs a) {
         }
       }
     }
+  }
   }
 }
 
@@ -584,6 +592,205 @@ __device__ uint32_t layout(const KArgs &a, const PageDesc &d, int page, const Co
 __device__ __forceinline__ int bits_len(int v) { return v ? 32 - __clz(v) : 0; }
 
 // ===========================================================================
+// Run walk for the tiled decode of flat, required, fixed-width RLE_DICTIONARY
+// pages (called by k_prepare, consumed by k_expand).
+//
+// One wave walks the key stream's run headers (hybrid_decoder.go:82-166) into
+// a run table in HBM and records, for every RUN_TILE values, the run
+// holding the tile's first value.  Trains of identical bit-packed headers
+// (what an encoder writes for high-entropy keys) are accepted 64 candidates
+// at a time; the train check is only tried when the next header repeats the
+// current one, so alternating RLE / bit-packed streams stay a cheap serial
+// walk over a register window.
+// ===========================================================================
+
+// 1 KiB register window over a byte stream: lane l holds bytes [16l, 16l + 16)
+// of the 16-byte aligned window base.  Reads are uniform (v_readlane).
+struct Win1K {
+  const uint8_t *ab;
+  uint4 w;
+  __device__ __forceinline__ void reset() { ab = nullptr; }
+  __device__ __forceinline__ void at(const uint8_t *a) {  // make [a, a + 8) resident
+    if (!ab || (uint64_t)(a - ab) >= 1024 - 8) {
+      ab = (const uint8_t *)((uintptr_t)a & ~(uintptr_t)15);
+      w = ((const uint4 *)ab)[lane_id()];
+    }
+  }
+  __device__ __forceinline__ uint32_t dw(uint32_t i) {  // dword i of the window
+    const int l = (int)(i >> 2);
+    const uint32_t c = i & 3;
+    const uint32_t x = __builtin_amdgcn_readlane(w.x, l), y = __builtin_amdgcn_readlane(w.y, l),
+                   z = __builtin_amdgcn_readlane(w.z, l), q = __builtin_amdgcn_readlane(w.w, l);
+    return c == 0 ? x : c == 1 ? y : c == 2 ? z : q;
+  }
+  __device__ __forceinline__ uint32_t byte_at(const uint8_t *a) {
+    at(a);
+    const uint32_t off = (uint32_t)(a - ab);
+    return (dw(off >> 2) >> ((off & 3) * 8)) & 0xffu;
+  }
+};
+
+// byte q of the hl-byte uvarint encoding of h
+__device__ __forceinline__ uint32_t hdr_byte(uint64_t h, int hl, int q) {
+  return (uint32_t)((h >> (7 * q)) & 0x7f) | (q < hl - 1 ? 0x80u : 0u);
+}
+
+// record run r = [s, e) as the first run of every tile whose first value it
+// holds, with the byte of that value's key: bit-packed data at byte `prm`
+// (bw bits a value), or for an RLE run (bw < 0) the byte after it
+__device__ __forceinline__ void tiles_of_run(int2 *tf, int64_t s, int64_t e, int32_t r, int64_t prm, int bw) {
+  for (int64_t t = (s + RUN_TILE - 1) / RUN_TILE; t * RUN_TILE < e; t++)
+    tf[t] = make_int2(r, (int32_t)(bw < 0 ? prm : prm + (((t * RUN_TILE - s) * bw) >> 3)));
+}
+
+// ks / slen: the key stream after the bit-width byte; n values; bw bit width
+__device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const uint8_t *ks, int64_t slen,
+                          int32_t n, int bw) {
+  const int lane = lane_id();
+  uint2 *runs = a.runs + d.run_base;
+  int2 *tf = a.tile_info + d.tile_base;
+  const int32_t cap = d.run_cap - 1;  // entries before the sentinel
+
+  int32_t nr = 0;    // runs emitted
+  int64_t v = 0;     // values covered
+  int64_t hpos = 0;  // next header (stream offset)
+  uint32_t err = E_OK;
+  Win1K W;
+  W.reset();
+  if (bw == 0) {  // hybrid_decoder.go:84-86: all zeros, nothing read
+    if (lane == 0) {
+      runs[0] = make_uint2(RUN_RLE, 0u);
+      tiles_of_run(tf, 0, n, 0, 0, 0);
+    }
+    nr = 1;
+    v = n;
+  }
+  while (v < n) {
+    if (nr >= cap) {  // cannot happen: runs <= min(n, len / 2 + 1) (host sizing)
+      err = E_UNSUPPORTED;
+      break;
+    }
+    // readRunHeader :143-166 (readUVariant32, helpers.go:149-165)
+    const int64_t h0 = hpos;
+    uint64_t h = 0;
+    uint32_t sh = 0;
+    for (int i = 0;; i++) {
+      if (hpos >= slen) {
+        err = E_EOF;
+        break;
+      }
+      const uint32_t b = W.byte_at(ks + hpos);
+      hpos++;
+      if (b < 0x80) {
+        if (i > 9 || (i == 9 && b > 1)) err = E_RLE;
+        h |= (uint64_t)b << (sh & 63);
+        break;
+      }
+      if (sh < 64) h |= (uint64_t)(b & 0x7f) << sh;
+      sh += 7;
+    }
+    if (err) break;
+    if (h > 0x7fffffffull) {  // "int32 out of range"
+      err = E_RLE;
+      break;
+    }
+    const int32_t hl = (int32_t)(hpos - h0);
+    if (h & 1) {  // bit-packed run of g groups (readBitPackedRun :133-141)
+      const int64_t g = (int64_t)(h >> 1);
+      if (g == 0) {
+        err = E_RLE;
+        break;
+      }
+      // groups the page needs; each must start inside the stream (a short
+      // last group is zero-filled, a group starting at the end is io.EOF)
+      const int64_t ng = (min<int64_t>(g * 8, (int64_t)n - v) + 7) >> 3;
+      const int64_t have = hpos < slen ? (slen - hpos + bw - 1) / bw : 0;
+      if (have < ng) {
+        if (have > 0 && lane == 0) {
+          runs[nr] = make_uint2((uint32_t)v, (uint32_t)hpos);
+          tiles_of_run(tf, v, v + have * 8, nr, hpos, bw);
+        }
+        if (have > 0) nr++;
+        v += have * 8;
+        err = E_EOF;
+        break;
+      }
+      const int64_t e = min<int64_t>(v + g * 8, (int64_t)n);
+      if (lane == 0) {
+        runs[nr] = make_uint2((uint32_t)v, (uint32_t)hpos);
+        tiles_of_run(tf, v, e, nr, hpos, bw);
+      }
+      nr++;
+      v = e;
+      hpos += g * (int64_t)bw;
+      if (v >= n) break;
+      // a train?  only if the next header repeats this one (a uvarint's bytes
+      // are fixed by its value and length)
+      const int64_t stride = hl + g * (int64_t)bw;
+      bool same = hpos + hl <= slen;
+      for (int q = 0; q < hl && same; q++) same = W.byte_at(ks + hpos + q) == hdr_byte(h, hl, q);
+      if (!same) continue;
+      // lane k checks for the same header again k strides ahead
+      const int64_t cand = hpos + (int64_t)lane * stride;  // candidate header of run nr + lane
+      const int64_t cstart = v + (int64_t)lane * g * 8;
+      bool ok = cstart < n && nr + lane < cap && cand + hl <= slen;
+      if (ok) {
+        for (int q = 0; q < hl; q++) ok &= ks[cand + q] == hdr_byte(h, hl, q);
+        const int64_t cng = (min<int64_t>(g * 8, (int64_t)n - cstart) + 7) >> 3;
+        ok &= cand + hl + (cng - 1) * bw < slen;
+      }
+      const uint64_t okm = ballot(ok);
+      const int m = (int)__builtin_ctzll(~okm);  // leading accepted candidates (lanes 0..m-1)
+      if (m > 0) {
+        if (lane < m) {
+          runs[nr + lane] = make_uint2((uint32_t)cstart, (uint32_t)(cand + hl));
+          tiles_of_run(tf, cstart, min<int64_t>(cstart + g * 8, (int64_t)n), nr + lane, cand + hl, bw);
+        }
+        v = min<int64_t>(v + (int64_t)m * g * 8, (int64_t)n);
+        hpos += (int64_t)m * stride;
+        nr += m;
+      }
+    } else {  // RLE run (readRLERunValue :116-131)
+      const int64_t cr = (int64_t)(h >> 1);
+      if (cr == 0) {
+        err = E_RLE;
+        break;
+      }
+      const int sz = (bw + 7) >> 3;
+      if (hpos >= slen || hpos + sz > slen) {
+        err = E_EOF;
+        break;
+      }
+      uint32_t val = 0;
+      for (int k = 0; k < sz; k++) val |= W.byte_at(ks + hpos + k) << (8 * k);
+      hpos += sz;
+      if (bw < 32 && (val >> bw) != 0) {  // "RLE run value is too large"
+        err = E_RLE;
+        break;
+      }
+      const int64_t e = min<int64_t>(v + cr, (int64_t)n);
+      if (lane == 0) {
+        runs[nr] = make_uint2((uint32_t)v | RUN_RLE, val);
+        tiles_of_run(tf, v, e, nr, hpos, -1);
+      }
+      nr++;
+      v = e;
+    }
+  }
+  const int32_t cover = (int32_t)min<int64_t>(v, (int64_t)n);
+  // sentinel, and tiles past the coverage point at it
+  const int64_t ntiles = ((int64_t)n + RUN_TILE - 1) / RUN_TILE;
+  for (int64_t t = (cover + RUN_TILE - 1) / RUN_TILE + lane; t < ntiles; t += 64) tf[t] = make_int2(nr, (int32_t)slen);
+  if (lane == 0) {
+    runs[nr] = make_uint2((uint32_t)cover, 0u);
+    pi->cover = cover;
+    pi->walk_err = err;
+    pi->pad = nr;
+  }
+}
+
+
+// ===========================================================================
 // K3: data page prepare
 // ===========================================================================
 __global__ __launch_bounds__(256) void k_prepare(KArgs a) {
@@ -631,6 +838,15 @@ __global__ __launch_bounds__(256) void k_prepare(KArgs a) {
     pi->val_off = (int32_t)ps.val_off;
     pi->val_len = (int32_t)ps.val_len;
     pi->idx_bw = idx_bw;
+  }
+  if (d.run_cap > 0) {  // tiled RLE_DICTIONARY page: its run table for k_expand
+    if (d.num_values <= 0) return;
+    if (d.dict < 0) {  // dictDecoder without a dictionary (type_dict.go:40-42)
+      set_status(a.status, page, ST_VALUES, E_DICT);
+      return;
+    }
+    walk_runs(a, d, pi, ps.body + ps.val_off + 1, ps.val_len - 1, d.num_values, idx_bw);
+    return;
   }
   if (!(c.flags & COL_NEEDS_COUNT)) return;
 
@@ -1206,582 +1422,487 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
   if (err) set_status(a.status, page, err_stage, err);
 }
 
-// ===========================================================================
-// K5f: flat, required, fixed-width pages (PLAIN / RLE_DICTIONARY) — the hot
-// shape of C1/C2/C5.  One wave per page, 1024 values per step, 16
-// consecutive values per lane (64-128 output bytes per lane, 16-byte
-// stores).  The encoded index stream is read through an 8 KB per-wave LDS
-// window (headers and bit-packed data alike), so a step costs one global
-// round trip: the dictionary gathers.
-// ===========================================================================
-constexpr int FW_WIN = 8192;     // LDS window per wave
-constexpr int FW_WAVES = 4;
-constexpr int FW_STEP = 1024;    // values per step
-constexpr int FW_PER_LANE = 16;
+// global-address-space accessors for addresses held as integers (keeps the
+// compiler on global_load / global_store instead of flat)
+typedef __attribute__((address_space(1))) const uint32_t g_u32;
+typedef __attribute__((address_space(1))) const uint64_t g_u64;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t gld32(uintptr_t p) { return *(g_u32 *)p; }
+__device__ __forceinline__ uint64_t gld64(uintptr_t p) { return *(g_u64 *)p; }
+__device__ __forceinline__ void gst32(uintptr_t p, uint32_t v) { *(__attribute__((address_space(1))) uint32_t *)p = v; }
+__device__ __forceinline__ void gst64(uintptr_t p, uint64_t v) { *(__attribute__((address_space(1))) uint64_t *)p = v; }
+__device__ __forceinline__ void gst128(uintptr_t p, uint4 v) {
+  u32x4 x = {v.x, v.y, v.z, v.w};
+  *(__attribute__((address_space(1))) u32x4 *)p = x;
+}
 
-struct LdsWin {
-  uint8_t *lds;        // this wave's window
-  const uint8_t *p;    // stream start
-  int64_t len;         // stream length
-  int64_t lo, hi;      // stream offsets currently held: [lo, hi)
-  const uint8_t *ab;   // absolute address of lds[0]
-
-  // make [a, b) (stream offsets, b - a <= FW_WIN - 32) resident
-  __device__ __forceinline__ void ensure(int64_t a, int64_t b) {
-    if (a >= lo && b <= hi) return;
-    const uintptr_t A = (uintptr_t)(p + a) & ~(uintptr_t)15;
-    const uintptr_t E = (uintptr_t)(p + len) + 16;  // never read past the stream end + 16 (buffers are padded)
-    const uintptr_t last = (E - 16) & ~(uintptr_t)15;
-    const int lane = lane_id();
-    uint4 v[FW_WIN / 1024];
+// Wave copy of up to MAXC KiB, in passes of 4 KiB with every load of a pass
+// issued before its stores (16-byte aligned stores after a short head,
+// funnel-shifted dword loads).
+template <int MAXC>
+__device__ __forceinline__ void copy_tile(const uint8_t *s, uint8_t *D, int64_t len, int lane) {
+  constexpr int PASS = 4;
+  int64_t head = (int64_t)((16 - ((uintptr_t)D & 15)) & 15);
+  if (head > len) head = len;
+  if (lane < head) D[lane] = s[lane];
+  const int64_t body = (len - head) >> 4;
+  const uintptr_t S = (uintptr_t)(s + head);
+  const uintptr_t D16 = (uintptr_t)(D + head);
+  const uint32_t skew = (uint32_t)(S & 3);
+  const uintptr_t SA = S & ~(uintptr_t)3;
+  for (int i0 = 0; i0 < MAXC && 64 * i0 < body; i0 += PASS) {
+    uint4 x[PASS];
+    uint32_t x4[PASS];
 #pragma unroll
-    for (int k = 0; k < FW_WIN / 1024; k++) {  // all loads first, then all LDS stores
-      uintptr_t src = A + (uintptr_t)(k * 1024 + lane * 16);
-      v[k] = *(const uint4 *)(src < E ? src : last);
+    for (int i = 0; i < PASS; i++) {
+      const int64_t c = lane + 64 * (i0 + i);
+      const uintptr_t src = SA + 16 * (uintptr_t)(c < body ? c : 0);
+      x[i] = make_uint4(gld32(src), gld32(src + 4), gld32(src + 8), gld32(src + 12));
+      x4[i] = gld32(src + 16);
     }
 #pragma unroll
-    for (int k = 0; k < FW_WIN / 1024; k++) {
-      uintptr_t src = A + (uintptr_t)(k * 1024 + lane * 16);
-      *(uint4 *)(lds + k * 1024 + lane * 16) = src < E ? v[k] : make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < PASS; i++) {
+      const int64_t c = lane + 64 * (i0 + i);
+      if (c < body) {
+        uint4 o;
+        o.x = __builtin_amdgcn_alignbyte(x[i].y, x[i].x, skew);
+        o.y = __builtin_amdgcn_alignbyte(x[i].z, x[i].y, skew);
+        o.z = __builtin_amdgcn_alignbyte(x[i].w, x[i].z, skew);
+        o.w = __builtin_amdgcn_alignbyte(x4[i], x[i].w, skew);
+        gst128(D16 + 16 * (uintptr_t)c, o);
+      }
     }
-    ab = (const uint8_t *)A;
-    lo = (int64_t)(A - (uintptr_t)p);
-    hi = lo + FW_WIN;
   }
-  __device__ __forceinline__ uint32_t byte(int64_t off) { return lds[(p + off) - ab]; }
-  // bits [bitpos, bitpos + bw) of the stream; bytes at/after len read as zero
-  __device__ __forceinline__ uint32_t bits(int64_t bitpos, int bw) {
-    int64_t byteoff = bitpos >> 3;
-    int sh = (int)(bitpos & 7);
-    uintptr_t la = (uintptr_t)((p + byteoff) - ab);
-    const uint32_t *q = (const uint32_t *)(lds + (la & ~(uintptr_t)3));
-    uint64_t v = ((uint64_t)q[1] << 32) | q[0];
-    v >>= (la & 3) * 8 + sh;
-    uint32_t val = (uint32_t)v & (bw == 32 ? 0xffffffffu : ((1u << bw) - 1));
-    int64_t avail = (len - byteoff) * 8 - sh;
-    if (avail < bw) val = avail <= 0 ? 0u : (val & ((1u << avail) - 1));
-    return val;
+  const int64_t done = head + body * 16;
+  if (lane < len - done) D[done + lane] = s[done + lane];
+}
+
+__device__ __forceinline__ const uint8_t *body_of(const KArgs &a, uint8_t src, uint64_t body, int64_t alias1) {
+  if (src == BODY_RAW) return a.in + body;
+  if (src == BODY_SNAPPY && alias1) return a.in + (alias1 - 1);
+  return a.stage + body;
+}
+
+// Everything k_expand needs about its page, loaded in one round trip.
+struct ExPage {
+  int32_t n, cover, nr, bw, val_len;
+  uint32_t dict_n;
+  const uint8_t *vals;  // values section
+  const uint8_t *dict;  // dictionary values
+  const uint2 *runs;    // run table
+  bool ok;              // page and dictionary clean so far
+  bool plain;
+};
+
+// Run-table window in registers: lane i holds entry wb + i; the sentinel and
+// everything after it read as start = INT32_MAX, so "start <= j" ballots are
+// lane prefixes.
+struct RunWin {
+  int32_t wb, start;
+  uint32_t prm, rle;
+  __device__ __forceinline__ void load(const uint2 *runs, int32_t nr, int32_t base) {
+    wb = base;
+    const int32_t ei = wb + lane_id();
+    const uint2 e = ei < nr ? runs[ei] : make_uint2(0x7fffffffu, 0u);
+    start = ei < nr ? (int32_t)(e.x & ~RUN_RLE) : 0x7fffffff;
+    rle = e.x & RUN_RLE;
+    prm = e.y;
   }
 };
 
-__global__ __launch_bounds__(256) void k_decode_flat(KArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t win_all[FW_WAVES][FW_WIN + 16];
-  const int wv = (int)ufirst(threadIdx.x >> 6);  // wave-uniform (keeps per-wave state in SGPRs)
-  const int gi = blockIdx.x * FW_WAVES + wv;
-  if (gi >= a.nlist) return;
+// Keys of [v0, lim) (at most 512 values) read straight from HBM/L2 at their
+// own bit offsets — the path for key ranges whose runs or bytes exceed the
+// staged form below (very short runs).  Value j = v0 + 64 k + lane.
+__device__ void expand_direct(const KArgs &a, const ExPage &P, int page, int w, uint8_t *out, int32_t v0,
+                              int32_t lim, int32_t tfi) {
+  constexpr int R = 8;
   const int lane = lane_id();
-  const int page = ufirst(a.list[gi]);
-  if (page_status(a.status, page) != STATUS_OK) return;
-  const PageDesc d = a.pages[page];
-  if (d.dict >= 0 && page_status(a.status, d.dict) != STATUS_OK) return;
-  const ColDesc c = a.cols[d.col];
-  const PageInfo pi = a.info[page];
-  const int n = d.num_values;
-  if (n == 0) return;
-  const uint8_t *vals = body_ptr(a, d, page) + pi.val_off;
-  const int64_t vlen = pi.val_len;
-  const int w = c.width;  // 4 or 8
-  uint8_t *out = c.values + d.level_base * w;
-
-  if (d.enc == ENC_PLAIN) {
-    // a straight copy of n*w bytes (binary.Read per value, type_int32.go:23-37)
-    if ((int64_t)n * w > vlen) {
-      set_status(a.status, page, ST_VALUES, E_EOF);
-      return;
+  const uint8_t *ks = P.vals + 1;
+  const uintptr_t ks_al = (uintptr_t)ks & ~(uintptr_t)3;
+  const uint32_t ks_sh = (uint32_t)((uintptr_t)ks & 3) * 8;
+  const int32_t end_bit = (P.val_len - 1) * 8;
+  const int bw = P.bw;
+  const uint32_t mask = bw >= 32 ? 0xffffffffu : ((1u << bw) - 1);
+  RunWin W;
+  W.load(P.runs, P.nr, tfi);
+  uint32_t ko[R];
+  uint32_t rle_bits = 0;
+#pragma unroll
+  for (int k = 0; k < R; k++) {
+    ko[k] = 0;
+    const int32_t rl = v0 + 64 * k;
+    if (rl >= lim) continue;
+    const int32_t rh = min(rl + 64, lim);
+    uint64_t m = ballot(W.start <= rl);
+    while (m == ~0ull) {  // every window entry starts at or before the row: slide forward
+      W.load(P.runs, P.nr, W.wb + 63);
+      m = ballot(W.start <= rl);
     }
-    copy_bytes_wave(vals, out, (int64_t)n * w, lane);
-    return;
+    int32_t ri = max((int32_t)__popcll(m) - 1, 0);
+    int32_t ns = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, ri + 1);
+    if (ns < rh && ri > 0) {  // runs start inside the row: put the row's first run at lane 0
+      W.load(P.runs, P.nr, W.wb + ri);
+      ri = 0;
+      ns = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, 1);
+    }
+    const int32_t j = rl + lane;
+    int32_t s0 = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, ri);
+    uint32_t p0 = __builtin_amdgcn_readlane(W.prm, ri), f0 = __builtin_amdgcn_readlane(W.rle, ri);
+    for (int32_t q = ri + 1; q < 64 && ns < rh;) {  // runs that start inside this row
+      const bool mine = j >= ns;
+      const uint32_t pq = __builtin_amdgcn_readlane(W.prm, q), fq = __builtin_amdgcn_readlane(W.rle, q);
+      s0 = mine ? ns : s0;
+      p0 = mine ? pq : p0;
+      f0 = mine ? fq : f0;
+      q++;
+      ns = q < 64 ? (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, q) : 0x7fffffff;
+    }
+    ko[k] = f0 ? p0 : p0 * 8 + (uint32_t)(j - s0) * (uint32_t)bw;
+    rle_bits |= (f0 ? 1u : 0u) << k;
   }
-
-  // RLE_DICTIONARY (type_dict.go:39-59) over the hybrid key stream
-  const PageDesc *dp = d.dict >= 0 ? &a.pages[d.dict] : nullptr;
-  if (!dp) {
+  uint64_t raw[R];
+#pragma unroll
+  for (int k = 0; k < R; k++) {
+    const uint32_t t = ks_sh + (((rle_bits >> k) & 1) ? 0u : ko[k]);
+    raw[k] = gld64(ks_al + ((t >> 5) << 2));
+  }
+  uint32_t key[R];
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < R; k++) {
+    const bool act = v0 + 64 * k + lane < lim;
+    const uint32_t t = ks_sh + ko[k];
+    uint32_t kv = (uint32_t)(raw[k] >> (t & 31)) & mask;
+    const int32_t avail = end_bit - (int32_t)ko[k];
+    kv &= avail >= bw ? 0xffffffffu : avail <= 0 ? 0u : ((1u << avail) - 1);
+    kv = ((rle_bits >> k) & 1) ? ko[k] : kv;
+    bad |= act && kv >= P.dict_n;
+    key[k] = act && kv < P.dict_n ? kv : 0u;
+  }
+  if (ballot(bad)) {
     set_status(a.status, page, ST_VALUES, E_DICT);
     return;
   }
-  const uint8_t *dict = body_ptr(a, *dp, d.dict);
-  const int64_t dict_n = dp->num_values;
-  const int bw = pi.idx_bw;
-
-  LdsWin L;
-  L.lds = win_all[wv];
-  L.p = vals + 1;
-  L.len = vlen - 1;
-  L.lo = 1;
-  L.hi = 0;  // empty
-  L.ab = nullptr;
-
-  // hybrid run state (hybrid_decoder.go:82-166), wave-uniform
-  int64_t pos = 0, rem = 0, data = 0, vi = 0;
-  uint32_t rle_val = 0;
-  bool rle = false;
-  uint32_t err = E_OK;
-  const bool aligned_dict = (((uintptr_t)dict) & (w - 1)) == 0;
-
-  for (int64_t e0 = 0; e0 < n && !err; e0 += FW_STEP) {
-    const int cnt = (int)min<int64_t>(FW_STEP, n - e0);
-    uint32_t key[FW_PER_LANE];
+  const uintptr_t dict_al = (uintptr_t)P.dict & ~(uintptr_t)3;
+  const uint32_t dsh = (uint32_t)((uintptr_t)P.dict & 3);
 #pragma unroll
-    for (int k = 0; k < FW_PER_LANE; k++) key[k] = 0;
-    int got = 0;
-    if (bw > 0) {
-      while (got < cnt) {
-        if (rem == 0) {
-          // readRunHeader: uvarint from the LDS window
-          uint64_t h = 0;
-          uint32_t sh = 0;
-          for (int i = 0;; i++) {
-            if (pos >= L.len) {
-              err = E_EOF;
-              break;
-            }
-            L.ensure(pos, pos + 16);
-            uint32_t b = ufirst(L.byte(pos));
-            pos++;
-            if (b < 0x80) {
-              if (i > 9 || (i == 9 && b > 1)) err = E_RLE;
-              h |= (uint64_t)b << (sh & 63);
-              break;
-            }
-            if (sh < 64) h |= (uint64_t)(b & 0x7f) << sh;
-            sh += 7;
-          }
-          if (err) break;
-          if (h > 0x7fffffffull) {
-            err = E_RLE;
-            break;
-          }
-          if (h & 1) {
-            int64_t g = (int64_t)(h >> 1);
-            if (g == 0) {
-              err = E_RLE;
-              break;
-            }
-            rle = false;
-            rem = g * 8;
-            data = pos;
-            vi = 0;
-            pos = data + g * (int64_t)bw;
-          } else {
-            int64_t cr = (int64_t)(h >> 1);
-            if (cr == 0) {
-              err = E_RLE;
-              break;
-            }
-            int sz = (bw + 7) >> 3;
-            if (pos >= L.len || pos + sz > L.len) {
-              err = E_EOF;
-              break;
-            }
-            L.ensure(pos, pos + 16);
-            uint32_t v = 0;
-            for (int k = 0; k < sz; k++) v |= ufirst(L.byte(pos + k)) << (8 * k);
-            pos += sz;
-            if (bw < 32 && (v >> bw) != 0) {
-              err = E_RLE;
-              break;
-            }
-            rle = true;
-            rem = cr;
-            rle_val = v;
-          }
-        }
-        const int take = (int)min<int64_t>(rem, (int64_t)(cnt - got));
-        if (rle) {
-#pragma unroll
-          for (int k = 0; k < FW_PER_LANE; k++) {
-            int j = FW_PER_LANE * lane + k;
-            key[k] = (j >= got && j < got + take) ? rle_val : key[k];
-          }
-        } else {
-          const int64_t last_group = (vi + take - 1) >> 3;
-          if (data + last_group * bw >= L.len) {
-            err = E_EOF;
-            break;
-          }
-          const int64_t b_first = data + ((vi * bw) >> 3);
-          const int64_t b_last = data + (((vi + take) * (int64_t)bw + 7) >> 3);
-          L.ensure(b_first, b_last + 8);
-          // bit offset of chunk value 0 relative to lds[0] (fits 32 bits: the window is 8 KB)
-          const int32_t rbit0 = (int32_t)(((L.p + data) - L.ab) * 8 + (vi - got) * (int64_t)bw);
-          const uint32_t mask = bw == 32 ? 0xffffffffu : ((1u << bw) - 1);
-          const bool tail = b_last + 8 > L.len;  // values may touch bytes past the stream end
-          const int64_t end_bit = ((L.p + L.len) - L.ab) * 8;
-          // issue every LDS read of the lane's 16 values back to back, select afterwards
-#pragma unroll
-          for (int k = 0; k < FW_PER_LANE; k++) {
-            const int j = FW_PER_LANE * lane + k;
-            const bool in = j >= got && j < got + take;
-            const int32_t rb = in ? rbit0 + j * bw : 0;
-            const uint32_t *q = (const uint32_t *)(L.lds + ((rb >> 3) & ~3));
-            uint64_t v = ((uint64_t)q[1] << 32) | q[0];
-            uint32_t val = (uint32_t)(v >> (rb & 31)) & mask;
-            // zero-fill past the stream end (hybrid_decoder.go:133-141), branch-free
-            const int32_t avail = tail ? (int32_t)min<int64_t>(end_bit - rb, 64) : 64;
-            const uint32_t amask = avail <= 0 ? 0u : (avail >= 32 ? 0xffffffffu : ((1u << avail) - 1));
-            val &= amask;
-            key[k] = in ? val : key[k];
-          }
-          vi += take;
-        }
-        rem -= take;
-        got += take;
-      }
-      if (err) break;
-    }
-    // gather + store
-    bool bad = false;
-#pragma unroll
-    for (int k = 0; k < FW_PER_LANE; k++) bad |= (FW_PER_LANE * lane + k < cnt) && (int64_t)key[k] >= dict_n;
-    if (ballot(bad)) {
-      err = E_DICT;
-      break;
-    }
-    const int64_t s0 = e0 + FW_PER_LANE * lane;  // my first entry
-    const bool full = FW_PER_LANE * lane + FW_PER_LANE <= cnt;
+  for (int k = 0; k < R; k++) {
+    const int32_t j = v0 + 64 * k + lane;
+    if (j >= lim) continue;
+    const uintptr_t q = dict_al + (size_t)key[k] * w;
+    const uint32_t x0 = gld32(q), x1 = gld32(q + 4);
     if (w == 4) {
-      uint32_t v[FW_PER_LANE];
-#pragma unroll
-      for (int k = 0; k < FW_PER_LANE; k++) {
-        const uint8_t *src = dict + (int64_t)key[k] * 4;
-        v[k] = aligned_dict ? *(const uint32_t *)src : load_u32_unaligned(src);
-      }
-      uint32_t *o = (uint32_t *)(out + s0 * 4);
-      if (full && (((uintptr_t)o) & 15) == 0) {
-#pragma unroll
-        for (int k = 0; k < FW_PER_LANE; k += 4) *(uint4 *)(o + k) = make_uint4(v[k], v[k + 1], v[k + 2], v[k + 3]);
-      } else {
-#pragma unroll
-        for (int k = 0; k < FW_PER_LANE; k++)
-          if (FW_PER_LANE * lane + k < cnt) o[k] = v[k];
-      }
+      gst32((uintptr_t)out + 4 * (uintptr_t)j, __builtin_amdgcn_alignbyte(x1, x0, dsh));
     } else {
-      uint64_t v[FW_PER_LANE];
-#pragma unroll
-      for (int k = 0; k < FW_PER_LANE; k++) {
-        const uint8_t *src = dict + (int64_t)key[k] * 8;
-        v[k] = aligned_dict ? *(const uint64_t *)src : load_u64_unaligned(src);
-      }
-      uint64_t *o = (uint64_t *)(out + s0 * 8);
-      if (full && (((uintptr_t)o) & 15) == 0) {
-#pragma unroll
-        for (int k = 0; k < FW_PER_LANE; k += 2)
-          *(uint4 *)(o + k) = make_uint4((uint32_t)v[k], (uint32_t)(v[k] >> 32), (uint32_t)v[k + 1], (uint32_t)(v[k + 1] >> 32));
-      } else {
-#pragma unroll
-        for (int k = 0; k < FW_PER_LANE; k++)
-          if (FW_PER_LANE * lane + k < cnt) o[k] = v[k];
-      }
+      const uint32_t x2 = gld32(q + 8);
+      gst64((uintptr_t)out + 8 * (uintptr_t)j,
+            ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, dsh) << 32) | __builtin_amdgcn_alignbyte(x1, x0, dsh));
     }
   }
-  if (err) set_status(a.status, page, ST_VALUES, err);
 }
 
 // ===========================================================================
-// K5d: flat, required, fixed-width RLE_DICTIONARY pages whose key stream fits
-// in LDS — one 256-thread workgroup per page.
-//   1. the whole key stream is staged into LDS with 16-byte loads;
-//   2. wave 0 walks the run headers (hybrid_decoder.go:143-166) into an LDS
-//      run table.  The walk is speculative: after a bit-packed header it
-//      checks, one candidate per lane, whether the next 63 runs repeat the
-//      same header at the same stride (what an encoder writes for
-//      high-entropy keys) and accepts the matching prefix in one step;
-//   3. all four waves decode 1024-value steps (step s -> wave s % 4) with the
-//      run table held in registers (lane i = entry i of a 64-entry window):
-//      keys from LDS, dictionary gathers from HBM/L2, 16-byte stores.
-// A page with more runs than the table holds is processed in table-sized
-// rounds.
+// K5t: k_expand — tiled decode of flat, required, fixed-width (4 / 8 byte)
+// PLAIN and RLE_DICTIONARY pages (the hot shape of C1 / C2 / C5).
+//
+// One wave per TileJob (EX_WAVE consecutive values of one page), four jobs per
+// 256-thread workgroup.  RLE_DICTIONARY (type_dict.go:39-59):
+//   1. one round trip for the job's descriptors and its tile_info (first run
+//      and first key byte of its first tile and of the next job's);
+//   2. one round trip for the run-table window (lane i = run i) and, in
+//      parallel, the job's key bytes staged into LDS with 16-byte loads;
+//   3. rows of 256 values, four consecutive values per lane: each key is two
+//      LDS dwords and a funnel shift (or its run's RLE value), range-checked;
+//      then every dictionary gather of the job is issued back to back and
+//      each lane stores 16 / 32 contiguous bytes per row.
+// Jobs whose values span more runs or key bytes than the staged form holds
+// fall back to expand_direct.  PLAIN (type_int32.go:23-37,
+// type_int64.go:23-37) is a 16-byte copy of the job's bytes.  The grid is
+// dealt so that the jobs of one column chunk (one dictionary) share an XCD's
+// L2 (host side).
 // ===========================================================================
-constexpr int DW_RUNS = 512;  // run-table entries per round
+constexpr int EX_WAVE = EX_WAVE_VALUES;       // values per wave
+constexpr int EX_ROW = 256;                   // values per row (4 per lane)
+constexpr int EX_ROWS = EX_WAVE / EX_ROW;     // rows per wave
+static_assert(EX_WAVE % RUN_TILE == 0, "tile_info granularity");
 
-struct RunEnt {
-  int32_t start;    // first value of the run (page-relative)
-  int32_t bitpos;   // bit offset of the run's data in the staged stream; -1 for RLE
-  uint32_t rle_val;
-  int32_t pad;
-};
-
-// DW_STREAM: staged key-stream bytes per workgroup.  Three instantiations
-// (8 / 31 / 56 KB) so small pages do not pay the LDS (occupancy) of big ones;
-// the host routes each page by its body length.
-template <int DW_STREAM>
-__global__ __launch_bounds__(256) void k_decode_dict_wg(KArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t sstream[DW_STREAM + 32];
-  __shared__ __attribute__((aligned(16))) RunEnt runs[DW_RUNS + 1];
-  __shared__ int32_t s_nruns, s_cover, s_err, s_dict_err;
+template <int WIDTH>
+__global__ __launch_bounds__(256) void k_expand(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t kspan_dyn[];
+  STAMP(0);
   const int wv = (int)ufirst(threadIdx.x >> 6);
   const int lane = lane_id();
-  if ((int)blockIdx.x >= a.nlist) return;
-  const int page = ufirst(a.list[blockIdx.x]);
-  if (page_status(a.status, page) != STATUS_OK) return;
-  const PageDesc d = a.pages[page];
-  if (d.dict < 0 || page_status(a.status, d.dict) != STATUS_OK) {
-    if (d.dict < 0 && threadIdx.x == 0) atomicMin(&a.status[page], make_status(ST_VALUES, E_DICT));
-    return;
+  const int job = (int)blockIdx.x * 4 + wv;
+  if (job >= a.nlist) return;
+  const TileJob tj = a.tiles[job];
+  const int page = tj.page, dpage = tj.dict >= 0 ? tj.dict : tj.page;
+  // 1. every descriptor load is independent of the others: one round trip
+  ExPage P;
+  const int2 ti0 = a.tile_info[tj.tf], ti1 = a.tile_info[tj.tf + EX_WAVE / RUN_TILE];
+  {
+    const uint32_t st = a.status[page], dst = a.status[dpage];
+    const PageDesc *pd = &a.pages[page];
+    const PageInfo *pi = &a.info[page];
+    const PageDesc *dd = &a.pages[dpage];
+    P.n = pd->num_values;
+    P.plain = pd->enc == ENC_PLAIN;
+    P.cover = pi->cover;
+    P.nr = pi->pad;
+    P.bw = pi->idx_bw;
+    P.val_len = pi->val_len;
+    P.dict_n = (uint32_t)dd->num_values;
+    P.vals = body_of(a, pd->body_src, pd->body, pi->alias1) + pi->val_off;
+    P.dict = body_of(a, dd->body_src, dd->body, a.info[dpage].alias1);
+    P.runs = a.runs + pd->run_base;
+    P.ok = st == STATUS_OK && dst == STATUS_OK;
   }
-  const ColDesc c = a.cols[d.col];
-  const PageInfo pi = a.info[page];
-  const int n = (int)ufirst((uint32_t)d.num_values);
-  if (n == 0) return;
-  const uint8_t *vals = body_ptr(a, d, page) + pi.val_off;
-  const int64_t slen = ufirst64((int64_t)pi.val_len - 1);  // key stream after the bit-width byte
-  const uint8_t *ks = vals + 1;
-  const int w = (int)ufirst((uint32_t)c.width);
-  uint8_t *out = c.values + d.level_base * w;
-  const PageDesc dp = a.pages[d.dict];
-  const uint8_t *dict = body_ptr(a, dp, d.dict);
-  const int64_t dict_n = ufirst64(dp.num_values);
-  const int bw = (int)ufirst((uint32_t)pi.idx_bw);
-  const bool aligned_dict = (((uintptr_t)dict) & (w - 1)) == 0;
-
-  STAMP(0);
-  // 1. stage the key stream: sstream[i] = byte at address A + i, A = ks aligned down to 16
-  const uintptr_t A = (uintptr_t)ks & ~(uintptr_t)15;
-  const int32_t skew = (int32_t)ufirst((uint32_t)((uintptr_t)ks - A));
-  const int64_t nbytes = skew + slen;  // the host routes only pages that fit
-  for (int64_t off = (int64_t)threadIdx.x * 16; off < nbytes + 16; off += 256 * 16)
-    *(uint4 *)(sstream + off) = off < nbytes ? *(const uint4 *)(A + off) : make_uint4(0, 0, 0, 0);
-  if (threadIdx.x == 0) {
-    s_err = 0;
-    s_dict_err = 0;
-  }
-  __syncthreads();
+  if (!P.ok) return;
   STAMP(1);
+  const int32_t v0 = tj.v0;
+  const int32_t v1 = min(v0 + EX_WAVE, P.n);
+  if (v0 >= v1) return;
+  constexpr int w = WIDTH;
 
-  int64_t hpos = 0;        // wave 0: next header (stream offset)
-  int32_t covered = 0;     // values covered by completed rounds
-  const int64_t end_bit = (int64_t)(skew + slen) * 8;
-  const uint32_t mask = bw == 32 ? 0xffffffffu : ((1u << bw) - 1);
-
-  while (covered < n) {
-    // 2. wave 0 walks up to DW_RUNS run headers
-    if (wv == 0) {
-      int32_t nr = 0, v = covered;
-      uint32_t err = E_OK;
-      if (bw == 0) {  // hybrid_decoder.go:84-86: all zeros, nothing read
-        if (lane == 0) runs[0] = RunEnt{v, -1, 0u, 0};
-        nr = 1;
-        v = n;
-      }
-      while (v < n && nr < DW_RUNS && !err) {
-        hpos = ufirst64(hpos);
-        v = (int32_t)ufirst((uint32_t)v);
-        nr = (int32_t)ufirst((uint32_t)nr);
-        const int64_t h0 = hpos;
-        uint64_t h = 0;
-        uint32_t sh = 0;
-        for (int i = 0;; i++) {
-          if (hpos >= slen) {
-            err = E_EOF;
-            break;
-          }
-          uint32_t b = ufirst(sstream[skew + hpos]);
-          hpos++;
-          if (b < 0x80) {
-            if (i > 9 || (i == 9 && b > 1)) err = E_RLE;
-            h |= (uint64_t)b << (sh & 63);
-            break;
-          }
-          if (sh < 64) h |= (uint64_t)(b & 0x7f) << sh;
-          sh += 7;
-        }
-        if (err) break;
-        if (h > 0x7fffffffull) {
-          err = E_RLE;
-          break;
-        }
-        const int32_t hl = (int32_t)(hpos - h0);  // header length in bytes
-        if (h & 1) {
-          const int64_t g = (int64_t)(h >> 1);
-          if (g == 0) {
-            err = E_RLE;
-            break;
-          }
-          // every group the page needs must start inside the stream (:133-141)
-          int64_t need = min<int64_t>(g * 8, (int64_t)(n - v));
-          if (hpos + ((need - 1) >> 3) * bw >= slen) {
-            err = E_EOF;
-            break;
-          }
-          if (lane == 0) runs[nr] = RunEnt{v, (int32_t)((skew + hpos) * 8), 0u, 0};
-          v = (int32_t)min<int64_t>((int64_t)v + g * 8, (int64_t)n);
-          hpos += g * (int64_t)bw;
-          nr++;
-          // speculate: lane k checks for the same header again k strides ahead
-          const int64_t stride = hl + g * (int64_t)bw;
-          const int64_t cand = hpos + (int64_t)lane * stride;  // candidate header of run nr + lane
-          const int64_t cstart = (int64_t)v + (int64_t)lane * g * 8;
-          bool ok = cstart < n && nr + lane < DW_RUNS && cand + hl <= slen;
-          if (ok) {
-            for (int q = 0; q < hl; q++) ok &= sstream[skew + cand + q] == sstream[skew + h0 + q];
-            const int64_t cneed = min<int64_t>(g * 8, (int64_t)n - cstart);
-            ok &= cand + hl + ((cneed - 1) >> 3) * bw < slen;
-          }
-          const uint64_t okm = ballot(ok);
-          const int m = (int)__builtin_ctzll(~okm);  // leading accepted candidates (lanes 0..m-1)
-          if (m > 0) {
-            if (lane < m) runs[nr + lane] = RunEnt{(int32_t)cstart, (int32_t)((skew + cand + hl) * 8), 0u, 0};
-            v = (int32_t)min<int64_t>((int64_t)v + (int64_t)m * g * 8, (int64_t)n);
-            hpos += (int64_t)m * stride;
-            nr += m;
-          }
-        } else {
-          int64_t cr = (int64_t)(h >> 1);
-          if (cr == 0) {
-            err = E_RLE;
-            break;
-          }
-          int sz = (bw + 7) >> 3;
-          if (hpos >= slen || hpos + sz > slen) {
-            err = E_EOF;
-            break;
-          }
-          uint32_t val = 0;
-          for (int k = 0; k < sz; k++) val |= ufirst(sstream[skew + hpos + k]) << (8 * k);
-          hpos += sz;
-          if (bw < 32 && (val >> bw) != 0) {
-            err = E_RLE;
-            break;
-          }
-          if (lane == 0) runs[nr] = RunEnt{v, -1, val, 0};
-          v = (int32_t)min<int64_t>((int64_t)v + cr, (int64_t)n);
-          nr++;
-        }
-      }
-      if (lane == 0) {
-        runs[nr] = RunEnt{v, 0, 0u, 0};  // sentinel: end of coverage
-        s_nruns = nr;
-        s_cover = v;
-        if (err) s_err = (int32_t)err;
-      }
-    }
-    __syncthreads();
-    STAMP(2);
-    const int32_t nr = (int32_t)ufirst((uint32_t)s_nruns), cover = (int32_t)ufirst((uint32_t)s_cover);
-    // on a header error, the values before it are still decoded: a dictionary
-    // index error among them comes first in the reference (type_dict.go:45-53)
-
-    // 3. steps of 1024 values over [covered, cover); step boundaries are page-absolute.
-    // Run table window in registers: lane i holds entry wb + i (and the next start).
-    int32_t wb = -1;
-    int32_t r_start = 0, r_next = 0, r_bit = 0;
-    uint32_t r_val = 0;
-    for (int32_t e0 = (covered / FW_STEP) * FW_STEP + wv * FW_STEP; e0 < cover; e0 += FW_WAVES * FW_STEP) {
-      const int32_t lo = max(e0, covered), hi = min(e0 + FW_STEP, cover);
-      // window containing the run of `lo`: first entry with start <= lo < next start
-      while (true) {
-        if (wb < 0 || !(ufirst(__builtin_amdgcn_readlane(r_start, 0)) <= lo &&
-                        lo < (int32_t)__builtin_amdgcn_readlane(r_next, min(63, nr - 1 - wb)))) {
-          // (re)load: binary search the LDS table for the run of lo, window starts there
-          int32_t l = 0, h2 = nr - 1;
-          while (l < h2) {
-            int32_t mid = (l + h2 + 1) >> 1;
-            if ((int32_t)ufirst((uint32_t)runs[mid].start) <= lo) l = mid;
-            else h2 = mid - 1;
-          }
-          wb = l;
-          const int32_t ei = min(wb + lane, nr - 1);
-          const RunEnt re = runs[ei];
-          r_start = re.start;
-          r_bit = re.bitpos;
-          r_val = re.rle_val;
-          r_next = runs[ei + 1].start;
-        }
-        break;
-      }
-      // per-lane: run of my first value j0, found by binary search over the window lanes
-      const int32_t j0 = e0 + FW_PER_LANE * lane;
-      const int32_t wn = min(64, nr - wb);  // valid window entries
-      int32_t ri = 0;
-#pragma unroll
-      for (int stp = 32; stp >= 1; stp >>= 1) {
-        int32_t cand = ri + stp;
-        int32_t cs = (int32_t)shfl32((uint32_t)r_start, min(cand, 63));
-        if (cand < wn && cs <= j0) ri = cand;
-      }
-      int32_t my_start = (int32_t)shfl32((uint32_t)r_start, ri);
-      int32_t my_next = (int32_t)shfl32((uint32_t)r_next, ri);
-      int32_t my_bit = (int32_t)shfl32((uint32_t)r_bit, ri);
-      uint32_t my_val = shfl32(r_val, ri);
-      uint32_t key[FW_PER_LANE];
-#pragma unroll
-      for (int k = 0; k < FW_PER_LANE; k++) {
-        const int32_t j = j0 + k;
-        const bool cross = j >= my_next && ri + 1 < wn;  // crossed into the next run (rare: runs are long)
-        if (ballot(cross)) {  // wave-uniform branch: every lane takes part in the shuffles
-          ri += cross ? 1 : 0;
-          my_start = (int32_t)shfl32((uint32_t)r_start, ri);
-          my_next = (int32_t)shfl32((uint32_t)r_next, ri);
-          my_bit = (int32_t)shfl32((uint32_t)r_bit, ri);
-          my_val = shfl32(r_val, ri);
-        }
-        const bool in = j >= lo && j < hi;
-        const int32_t rb = (in && my_bit >= 0) ? my_bit + (j - my_start) * bw : 0;
-        const uint32_t *q = (const uint32_t *)(sstream + ((rb >> 3) & ~3));
-        uint64_t vv = ((uint64_t)q[1] << 32) | q[0];
-        uint32_t val = (uint32_t)(vv >> (rb & 31)) & mask;
-        const int32_t avail = (int32_t)min<int64_t>(end_bit - rb, 64);  // zero past the stream end
-        val &= avail <= 0 ? 0u : (avail >= 32 ? 0xffffffffu : ((1u << avail) - 1));
-        key[k] = my_bit < 0 ? my_val : val;
-      }
-      bool bad = false;
-#pragma unroll
-      for (int k = 0; k < FW_PER_LANE; k++) {
-        const int32_t j = j0 + k;
-        bad |= j >= lo && j < hi && (int64_t)key[k] >= dict_n;
-      }
-      if (ballot(bad)) {
-        if (lane == 0) {
-          atomicMin(&a.status[page], make_status(ST_VALUES, E_DICT));
-          s_dict_err = 1;
-        }
-        continue;
-      }
-      const bool full = j0 >= lo && j0 + FW_PER_LANE <= hi;
-      if (w == 4) {
-        uint32_t vv[FW_PER_LANE];
-#pragma unroll
-        for (int k = 0; k < FW_PER_LANE; k++) {
-          const uint8_t *sp = dict + (int64_t)(j0 + k < hi ? key[k] : 0) * 4;
-          vv[k] = aligned_dict ? *(const uint32_t *)sp : load_u32_unaligned(sp);
-        }
-        uint32_t *o = (uint32_t *)(out + (int64_t)j0 * 4);
-        if (full && (((uintptr_t)o) & 15) == 0) {
-#pragma unroll
-          for (int k = 0; k < FW_PER_LANE; k += 4) *(uint4 *)(o + k) = make_uint4(vv[k], vv[k + 1], vv[k + 2], vv[k + 3]);
-        } else {
-#pragma unroll
-          for (int k = 0; k < FW_PER_LANE; k++)
-            if (j0 + k >= lo && j0 + k < hi) o[k] = vv[k];
-        }
-      } else {
-        uint64_t vv[FW_PER_LANE];
-#pragma unroll
-        for (int k = 0; k < FW_PER_LANE; k++) {
-          const uint8_t *sp = dict + (int64_t)(j0 + k < hi ? key[k] : 0) * 8;
-          vv[k] = aligned_dict ? *(const uint64_t *)sp : load_u64_unaligned(sp);
-        }
-        uint64_t *o = (uint64_t *)(out + (int64_t)j0 * 8);
-        if (full && (((uintptr_t)o) & 15) == 0) {
-#pragma unroll
-          for (int k = 0; k < FW_PER_LANE; k += 2)
-            *(uint4 *)(o + k) = make_uint4((uint32_t)vv[k], (uint32_t)(vv[k] >> 32), (uint32_t)vv[k + 1], (uint32_t)(vv[k + 1] >> 32));
-        } else {
-#pragma unroll
-          for (int k = 0; k < FW_PER_LANE; k++)
-            if (j0 + k >= lo && j0 + k < hi) o[k] = vv[k];
-        }
-      }
-    }
-    covered = cover;
-    __syncthreads();  // the run table is rewritten next round
-    STAMP(3);
-    if (s_err) {
-      if (threadIdx.x == 0 && !s_dict_err) atomicMin(&a.status[page], make_status(ST_VALUES, (uint32_t)s_err));
+  if (P.plain) {
+    if ((int64_t)P.n * w > P.val_len) {  // binary.Read past the values section
+      set_status(a.status, page, ST_VALUES, E_EOF);
       return;
     }
-    if (s_dict_err) return;
+    copy_tile<EX_WAVE * 8 / 1024>(P.vals + (int64_t)v0 * w, tj.out + (int64_t)v0 * w, (int64_t)(v1 - v0) * w, lane);
+    return;
   }
+
+  // ---- RLE_DICTIONARY ----
+  if (tj.dict < 0) return;                  // reported by walk_runs
+  const int32_t lim = min(v1, P.cover);     // values before a key-stream header error
+  if (v0 >= lim) return;
+  const int bw = P.bw;
+  const uint8_t *ks = P.vals + 1;
+  const int64_t slen = (int64_t)P.val_len - 1;
+  // 2. window and staged key bytes, in parallel
+  RunWin W;
+  W.load(P.runs, P.nr, ti0.x);
+  const int64_t byte_lo = ti0.y, byte_hi = (v1 >= P.n ? slen : (int64_t)ti1.y) + 16;
+  const uintptr_t A = ((uintptr_t)ks + (uintptr_t)byte_lo) & ~(uintptr_t)15;
+  const int64_t nb = (int64_t)((uintptr_t)ks + (uintptr_t)byte_hi - A);
+  const int ex_lds = a.ex_lds;
+  uint32_t *kspan = kspan_dyn + wv * (ex_lds / 4);
+  const bool staged = nb <= ex_lds;
+  if (staged) {
+    constexpr int NC = EX_WAVE * 4 / 1024 + 1;  // covers 32-bit keys
+    const uintptr_t E = (uintptr_t)ks + (uintptr_t)slen;  // stream end: bytes at/after it read as zero
+    uint4 x[NC];
+#pragma unroll
+    for (int i = 0; i < NC; i++) {
+      const int64_t off = (int64_t)(lane + 64 * i) * 16;
+      const uintptr_t src = A + (uintptr_t)(off < nb ? off : 0);
+      const uint64_t lo8 = gld64(src), hi8 = gld64(src + 8);
+      x[i] = make_uint4((uint32_t)lo8, (uint32_t)(lo8 >> 32), (uint32_t)hi8, (uint32_t)(hi8 >> 32));
+    }
+#pragma unroll
+    for (int i = 0; i < NC; i++) {
+      const int64_t off = (int64_t)(lane + 64 * i) * 16;
+      if (off < nb) {
+        const uintptr_t c = A + (uintptr_t)off;
+        uint32_t v4[4] = {x[i].x, x[i].y, x[i].z, x[i].w};
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uintptr_t d0 = c + 4 * q;
+          if (d0 + 4 <= E) continue;
+          v4[q] = d0 >= E ? 0u : (v4[q] & ((1u << (8 * (uint32_t)(E - d0))) - 1));
+        }
+        *(uint4 *)(kspan + off / 4) = make_uint4(v4[0], v4[1], v4[2], v4[3]);
+      }
+    }
+  }
+  // every run meeting [v0, lim) must sit in lanes 0..62 (its end is the next lane's start),
+  // and no row of EX_ROW values may hold two run starts (rows meet at most two runs)
+  const int32_t rs = W.start > v0 && W.start < lim && ((W.start - v0) & (EX_ROW - 1)) ? (W.start - v0) / EX_ROW : -1 - lane;
+  const int32_t rs_next = (int32_t)shfl32((uint32_t)rs, min(lane + 1, 63));
+  const bool fits = staged && (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, 63) >= lim &&
+                    !ballot(lane < 63 && rs >= 0 && rs == rs_next);
+  STAMP(2);
+  if (!fits) {
+    for (int32_t c = v0; c < lim; c += 512)
+      expand_direct(a, P, page, w, tj.out, c, min(c + 512, lim), a.tile_info[tj.tf + (c - v0) / RUN_TILE].x);
+    return;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  STAMP(3);
+  const int64_t lbase = (int64_t)(A - (uintptr_t)ks) * 8;  // stream bit of kspan bit 0
+  const int64_t end_bit = slen * 8;
+  const uint32_t mask = bw >= 32 ? 0xffffffffu : ((1u << bw) - 1);
+  const uint32_t dsh = (uint32_t)((uintptr_t)P.dict & 3);
+  // 3. per half (four rows, value j = row start + 4 lane + q): keys from LDS,
+  //    range check, then the half's gathers back to back; stores trail.
+  //    Dictionary reads and output writes go through buffer resources
+  //    (32-bit offsets; a read past the dictionary returns zero).
+  const __amdgpu_buffer_rsrc_t drs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)P.dict, (short)0, (int)(P.dict_n * (uint32_t)w + 8), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ors =
+      __builtin_amdgcn_make_buffer_rsrc((void *)tj.out, (short)0, (int)((uint32_t)P.n * (uint32_t)w), 0x00020000);
+  constexpr int HR = EX_ROWS / 2;
+  const int32_t end_bit32 = (int32_t)end_bit;
+  typedef typename std::conditional<WIDTH == 4, uint32_t, uint64_t>::type VT;
+  VT val[2][HR][4];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    uint32_t key[HR][4];
+    bool bad = false;
+    uint32_t kmax = 0;  // largest key of the fast rows
+#pragma unroll
+    for (int r = 0; r < HR; r++) {
+      const int32_t rl = v0 + (h * HR + r) * EX_ROW;
+      const int32_t j0 = rl + 4 * lane;
+#pragma unroll
+      for (int q = 0; q < 4; q++) key[r][q] = 0;
+      if (rl >= lim) continue;
+      const int32_t rh = min(rl + EX_ROW, lim);
+      const uint64_t m = ballot(W.start <= rl);
+      const int32_t ri = max((int32_t)__popcll(m) - 1, 0);
+      // at most two runs meet a row (checked per wave above): the row's run and the next
+      const int32_t s0 = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, ri);
+      const uint32_t p0 = __builtin_amdgcn_readlane(W.prm, ri), f0 = __builtin_amdgcn_readlane(W.rle, ri);
+      const int32_t s1 = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, ri + 1);
+      const uint32_t p1 = __builtin_amdgcn_readlane(W.prm, ri + 1), f1 = __builtin_amdgcn_readlane(W.rle, ri + 1);
+      // staged bit of key j inside a bit-packed run: c + j * bw
+      const int32_t c0 = (int32_t)(p0 * 8) - s0 * bw - (int32_t)lbase, c1 = (int32_t)(p1 * 8) - s1 * bw - (int32_t)lbase;
+      const bool fast = !f0 && (s1 >= rh || !f1) && rh - rl == EX_ROW &&
+                        (s1 >= rh ? (int64_t)p0 * 8 + (int64_t)(rh - s0) * bw
+                                  : (int64_t)p1 * 8 + (int64_t)(rh - s1) * bw) <= end_bit;
+      if (fast) {  // full row, bit-packed runs only, nothing past the stream end
+        // the lane's four keys are consecutive in one run unless a run starts among them
+        const bool split = j0 < s1 && j0 + 3 >= s1;
+        const uint32_t lb0 = (uint32_t)((j0 >= s1 ? c1 : c0) + j0 * bw);
+        const uint32_t *dw = kspan + (lb0 >> 5);
+        if (bw <= 8) {  // all four keys inside one 32-bit window
+          const uint32_t x = __builtin_amdgcn_alignbit(dw[1], dw[0], lb0 & 31);
+#pragma unroll
+          for (int q = 0; q < 4; q++) key[r][q] = __builtin_amdgcn_ubfe(x, (uint32_t)(q * bw), (uint32_t)bw);
+        } else if (bw <= 16) {  // ... inside one 64-bit window
+          const uint32_t d2 = dw[2];
+          const uint64_t x = ((uint64_t)__builtin_amdgcn_alignbit(d2, dw[1], lb0 & 31) << 32) |
+                             __builtin_amdgcn_alignbit(dw[1], dw[0], lb0 & 31);
+#pragma unroll
+          for (int q = 0; q < 4; q++) key[r][q] = (uint32_t)(x >> (q * bw)) & mask;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            const uint32_t lb = lb0 + (uint32_t)(q * bw);
+            const uint32_t *dq = kspan + (lb >> 5);
+            key[r][q] = __builtin_amdgcn_alignbit(dq[1], dq[0], lb & 31) & mask;
+          }
+        }
+        if (split) {  // the one lane of the row where a run starts (rare)
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            const int32_t j = j0 + q;
+            const uint32_t lb = (uint32_t)((j >= s1 ? c1 : c0) + j * bw);
+            const uint32_t *dq = kspan + (lb >> 5);
+            key[r][q] = __builtin_amdgcn_alignbit(dq[1], dq[0], lb & 31) & mask;
+          }
+        }
+        kmax = max(kmax, max(max(key[r][0], key[r][1]), max(key[r][2], key[r][3])));
+        continue;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int32_t j = j0 + q;
+        const bool act = j < lim;
+        const bool sel = j >= s1;
+        const uint32_t pr = sel ? p1 : p0, fr = sel ? f1 : f0;
+        const int32_t sr = sel ? s1 : s0;
+        const int32_t bb = (int32_t)pr * 8 + (j - sr) * bw;  // stream bit of the key (pages < 256 MiB)
+        const uint32_t lb = (fr || !act) ? 0u : (uint32_t)(bb - (int32_t)lbase);
+        const uint32_t *dw = kspan + (lb >> 5);
+        uint32_t kv = __builtin_amdgcn_alignbit(dw[1], dw[0], lb & 31) & mask;
+        const int32_t avail = end_bit32 - bb;  // zero-fill past the stream end (hybrid_decoder.go:133-141)
+        kv &= avail >= bw ? 0xffffffffu : avail <= 0 ? 0u : ((1u << avail) - 1);
+        kv = fr ? pr : kv;
+        bad |= act && kv >= P.dict_n;
+        key[r][q] = act ? kv : 0u;
+      }
+    }
+    if (ballot(bad || kmax >= P.dict_n)) {
+      // dictionary index out of range (type_dict.go:51-53); it precedes any later header error
+      set_status(a.status, page, ST_VALUES, E_DICT);
+      return;
+    }
+    // gathers (an unaligned dictionary is read as aligned dwords + a funnel shift)
+    if (dsh == 0) {
+#pragma unroll
+      for (int r = 0; r < HR; r++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          if (WIDTH == 4) {
+            switch (a.gather_aux) {  // experiment: cache policy of the dictionary gathers
+              case 1: val[h][r][q] = __builtin_amdgcn_raw_buffer_load_b32(drs, key[r][q] * 4, 0, 1); break;
+              case 2: val[h][r][q] = __builtin_amdgcn_raw_buffer_load_b32(drs, key[r][q] * 4, 0, 2); break;
+              case 3: val[h][r][q] = __builtin_amdgcn_raw_buffer_load_b32(drs, key[r][q] * 4, 0, 16); break;
+              case 4: val[h][r][q] = __builtin_amdgcn_raw_buffer_load_b32(drs, key[r][q] * 4, 0, 17); break;
+              default: val[h][r][q] = __builtin_amdgcn_raw_buffer_load_b32(drs, key[r][q] * 4, 0, 0); break;
+            }
+          } else {
+            const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(drs, key[r][q] * 8, 0, 0);
+            val[h][r][q] = ((uint64_t)x.y << 32) | x.x;
+          }
+        }
+    } else {
+      const __amdgpu_buffer_rsrc_t dra = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)((uintptr_t)P.dict & ~(uintptr_t)3), (short)0, (int)(P.dict_n * (uint32_t)w + 12), 0x00020000);
+#pragma unroll
+      for (int r = 0; r < HR; r++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          if (WIDTH == 4) {
+            const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(dra, key[r][q] * 4, 0, 0);
+            val[h][r][q] = __builtin_amdgcn_alignbyte(x.y, x.x, dsh);
+          } else {
+            const u32x3 x = __builtin_amdgcn_raw_buffer_load_b96(dra, key[r][q] * 8, 0, 0);
+            val[h][r][q] = ((uint64_t)__builtin_amdgcn_alignbyte(x.z, x.y, dsh) << 32) |
+                           __builtin_amdgcn_alignbyte(x.y, x.x, dsh);
+          }
+        }
+    }
+  }
+  STAMP(4);
+  // 4. stores: 16 / 32 contiguous bytes per lane per row
+  const bool out_al = ((uintptr_t)tj.out & 15) == 0;
+#pragma unroll
+  for (int h = 0; h < 2; h++)
+#pragma unroll
+    for (int r = 0; r < HR; r++) {
+      const int32_t j0 = v0 + (h * HR + r) * EX_ROW + 4 * lane;
+      const uint32_t off = (uint32_t)j0 * (uint32_t)w;
+      if (j0 + 4 <= lim && out_al) {
+        if (WIDTH == 4) {
+          __builtin_amdgcn_raw_buffer_store_b128(
+              u32x4{(uint32_t)val[h][r][0], (uint32_t)val[h][r][1], (uint32_t)val[h][r][2], (uint32_t)val[h][r][3]},
+              ors, off, 0, 0);
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b128(
+              u32x4{(uint32_t)val[h][r][0], (uint32_t)((uint64_t)val[h][r][0] >> 32), (uint32_t)val[h][r][1],
+                    (uint32_t)((uint64_t)val[h][r][1] >> 32)},
+              ors, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(
+              u32x4{(uint32_t)val[h][r][2], (uint32_t)((uint64_t)val[h][r][2] >> 32), (uint32_t)val[h][r][3],
+                    (uint32_t)((uint64_t)val[h][r][3] >> 32)},
+              ors, off + 16, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          if (j0 + q >= lim) continue;
+          if (WIDTH == 4) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)val[h][r][q], ors, off + 4 * q, 0, 0);
+          else
+            __builtin_amdgcn_raw_buffer_store_b64(
+                u32x2{(uint32_t)val[h][r][q], (uint32_t)((uint64_t)val[h][r][q] >> 32)}, ors, off + 8 * q, 0, 0);
+        }
+      }
+    }
+  STAMP(5);
 }
 
 // level-error precedence pass: for pages that failed in k_decode at the
@@ -1792,7 +1913,14 @@ __global__ __launch_bounds__(256) void k_level_check(KArgs a) {
   if (gi >= a.nlist) return;
   const int page = ufirst(a.list[gi]);
   uint32_t st = page_status(a.status, page);
-  if (st == STATUS_OK || (st >> 16) <= ST_REP) return;
+  if (st == STATUS_OK) {
+    // a key-stream header error found by k_runs, unless a dictionary error
+    // among the values before it was reported by k_expand
+    const uint32_t we = ufirst(a.info[page].walk_err);
+    if (we) set_status(a.status, page, ST_VALUES, we);
+    return;
+  }
+  if ((st >> 16) <= ST_REP) return;
   const PageDesc d = a.pages[page];
   const ColDesc c = a.cols[d.col];
   const PageInfo pi = a.info[page];
@@ -1848,6 +1976,12 @@ struct pq_launch_args {
   const int32_t *job_base;
   const int32_t *job_owner;
   uint64_t *dbg;
+  void *runs;
+  void *tile_info;
+  const void *tiles;
+  int32_t ntiles, ntiles4;  // k_expand jobs; the first ntiles4 are of 4-byte columns
+  int32_t ex_lds;
+  int32_t gather_aux;
 };
 
 static pq::KArgs to_k(const pq_launch_args *p) {
@@ -1868,6 +2002,11 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   k.job_base = p->job_base;
   k.job_owner = p->job_owner;
   k.dbg = p->dbg;
+  k.runs = (uint2 *)p->runs;
+  k.tile_info = (int2 *)p->tile_info;
+  k.ex_lds = p->ex_lds;
+  k.gather_aux = p->gather_aux;
+  k.tiles = (const pq::TileJob *)p->tiles;
   return k;
 }
 
@@ -1880,7 +2019,21 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
   }
   if (which == 6) {  // deferred literal copies: fixed grid, the job count lives on the device
     if (k.max_jobs == 0) return 0;
-    hipLaunchKernelGGL(pq::k_copy, dim3(k.max_jobs), dim3(256), 0, s, k);
+    hipLaunchKernelGGL(pq::k_copy, dim3(k.max_jobs < 2048 ? k.max_jobs : 2048), dim3(256), 0, s, k);
+    return hipGetLastError() == hipSuccess ? 0 : 17;
+  }
+  if (which == 8) {  // k_expand: one workgroup per tile job
+    if (p->ntiles <= 0) return 0;
+    // jobs of 4-byte columns first, then 8-byte ones (p->ntiles4 of them first)
+    if (p->ntiles4 > 0) {
+      k.nlist = p->ntiles4;
+      hipLaunchKernelGGL(pq::k_expand<4>, dim3((p->ntiles4 + 3) / 4), dim3(256), (size_t)4 * p->ex_lds, s, k);
+    }
+    if (p->ntiles > p->ntiles4) {
+      k.tiles = (const pq::TileJob *)p->tiles + p->ntiles4;
+      k.nlist = p->ntiles - p->ntiles4;
+      hipLaunchKernelGGL(pq::k_expand<8>, dim3((k.nlist + 3) / 4), dim3(256), (size_t)4 * p->ex_lds, s, k);
+    }
     return hipGetLastError() == hipSuccess ? 0 : 17;
   }
   if (k.nlist <= 0) return 0;
@@ -1891,10 +2044,6 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     case 2: hipLaunchKernelGGL(pq::k_prepare, grid, block, 0, s, k); break;
     case 3: hipLaunchKernelGGL(pq::k_decode, grid, block, 0, s, k); break;
     case 5: hipLaunchKernelGGL(pq::k_level_check, grid, block, 0, s, k); break;
-    case 7: hipLaunchKernelGGL(pq::k_decode_flat, grid, block, 0, s, k); break;
-    case 8: hipLaunchKernelGGL(pq::k_decode_dict_wg<8 * 1024>, dim3(k.nlist), block, 0, s, k); break;
-    case 9: hipLaunchKernelGGL(pq::k_decode_dict_wg<31 * 1024>, dim3(k.nlist), block, 0, s, k); break;
-    case 10: hipLaunchKernelGGL(pq::k_decode_dict_wg<56 * 1024>, dim3(k.nlist), block, 0, s, k); break;
     default: return 1;
   }
   return hipGetLastError() == hipSuccess ? 0 : 17;
