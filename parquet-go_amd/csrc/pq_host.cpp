@@ -49,6 +49,8 @@ struct pq_launch_args {
   const int32_t *job_base;
   const int32_t *job_owner;
   uint64_t *dbg;
+  uint64_t *dbg2;
+  int32_t npages_dbg;
   void *runs;
   void *tile_info;
   const void *tiles;
@@ -523,6 +525,7 @@ struct pqg_batch {
   int32_t *d_job_base = nullptr, *d_job_owner = nullptr;
   uint32_t max_jobs = 0;
   uint64_t *d_dbg = nullptr;     // diagnostic stamps (PQ_STAMPS builds only)
+  uint64_t *d_dbg2 = nullptr;
   void *d_runs = nullptr;        // run tables (k_prepare's run walk -> k_expand)
   void *d_tile_info = nullptr;     // per RUN_TILE values of a tiled page: {first run, first key byte}
   int32_t ex_lds = 0;              // k_expand staged key bytes per wave
@@ -1330,6 +1333,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   }
 #ifdef PQ_STAMPS
   rc |= alloc_dev((void **)&B->d_dbg, sizeof(uint64_t) * 8 * 4 * (B->tiles.size() + 1));
+  rc |= alloc_dev((void **)&B->d_dbg2, sizeof(uint64_t) * (8 * (npages + 1) + 256));
 #endif
   if (rc) {
     pqg_batch_destroy(B);
@@ -1496,6 +1500,8 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.job_base = B->d_job_base;
   a.job_owner = B->d_job_owner;
   a.dbg = B->d_dbg;
+  a.dbg2 = B->d_dbg2;
+  a.npages_dbg = (int32_t)B->pages.size() + 1;
   a.runs = B->d_runs;
   a.tile_info = B->d_tile_info;
   a.ex_lds = B->ex_lds;
@@ -1740,6 +1746,7 @@ void pqg_batch_destroy(pqg_batch *B) {
   hipFree(B->d_job_base);
   hipFree(B->d_job_owner);
   hipFree(B->d_dbg);
+  hipFree(B->d_dbg2);
   hipFree(B->d_runs);
   hipFree(B->d_tile_info);
   hipFree(B->d_tiles);
@@ -1846,5 +1853,11 @@ extern "C" int pqg_diag_stamps(pqg_batch *B, uint64_t *out, size_t n) {
   size_t cap = 8 * 4 * (B->tiles.size() + 1);
   if (n > cap) n = cap;
   return hipMemcpy(out, B->d_dbg, n * 8, hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
+}
+extern "C" int pqg_diag_stamps2(pqg_batch *B, uint64_t *out, size_t n) {
+  hipStreamSynchronize(B->ctx->stream);
+  size_t cap = 8 * (B->pages.size() + 1) + 256;
+  if (n > cap) n = cap;
+  return hipMemcpy(out, B->d_dbg2, n * 8, hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
 }
 #endif

@@ -23,6 +23,10 @@
 
 namespace pq {
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
 struct CopyJob {  // dst[0, len) = src[0, len), both in device memory
   const uint8_t *src;
   uint8_t *dst;
@@ -45,7 +49,9 @@ struct KArgs {
   uint32_t max_jobs;      // total job slots
   const int32_t *job_base;   // per Snappy-list position: first slot of its region
   const int32_t *job_owner;  // per slot: Snappy-list position that owns it
-  uint64_t *dbg;          // diagnostic build only (-DPQ_STAMPS): per-workgroup s_memtime stamps
+  uint64_t *dbg;          // diagnostic build only (-DPQ_STAMPS): per-wave k_expand stamps
+  uint64_t *dbg2;         // diagnostic build only: per-page k_prepare stamps / values
+  uint64_t *dbg3;         // diagnostic build only: run-walk iteration stamps of page 1
   uint2 *runs;            // k_runs -> k_expand: run tables (PageDesc.run_base)
   int2 *tile_info;        // per RUN_TILE values: {first run, byte of its first key} (PageDesc.tile_base)
   int32_t ex_lds;         // k_expand: staged key bytes per wave (dynamic LDS)
@@ -60,7 +66,14 @@ struct KArgs {
     if (a.dbg && lane_id() == 0)                                                              \
       a.dbg[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+#define PSTAMP(page, i, v)                              \
+  do {                                                   \
+    if (a.dbg2 && lane_id() == 0) a.dbg2[(size_t)(page) * 8 + (i)] = (v); \
+  } while (0)
 #else
+#define PSTAMP(page, i, v) \
+  do {                     \
+  } while (0)
 #define STAMP(i) \
   do {           \
   } while (0)
@@ -610,11 +623,13 @@ struct Win1K {
   const uint8_t *ab;
   uint4 w;
   __device__ __forceinline__ void reset() { ab = nullptr; }
+  __device__ __forceinline__ void fill(const uint8_t *a) {  // window starting at a (aligned down)
+    ab = (const uint8_t *)((uintptr_t)a & ~(uintptr_t)15);
+    const u32x4 x = *(const __attribute__((address_space(1))) u32x4 *)(ab + 16 * lane_id());
+    w = make_uint4(x.x, x.y, x.z, x.w);
+  }
   __device__ __forceinline__ void at(const uint8_t *a) {  // make [a, a + 8) resident
-    if (!ab || (uint64_t)(a - ab) >= 1024 - 8) {
-      ab = (const uint8_t *)((uintptr_t)a & ~(uintptr_t)15);
-      w = ((const uint4 *)ab)[lane_id()];
-    }
+    if (!ab || (uint64_t)(a - ab) >= 1024 - 8) fill(a);
   }
   __device__ __forceinline__ uint32_t dw(uint32_t i) {  // dword i of the window
     const int l = (int)(i >> 2);
@@ -644,29 +659,161 @@ __device__ __forceinline__ void tiles_of_run(int2 *tf, int64_t s, int64_t e, int
 }
 
 // ks / slen: the key stream after the bit-width byte; n values; bw bit width
+// Run entries are collected one per lane (64 at a time) and written out in
+// one lane-parallel burst with their tiles: no store sits in the walk's
+// dependency chain (stores and loads share vmcnt on gfx950, so a store in the
+// loop would make every window read wait for it).
+struct RunBuf {
+  uint2 *runs;
+  int2 *tf;
+  int32_t base, cnt;  // entries written / buffered
+  uint2 ent;          // lane k: entry base + k
+  int32_t es, ee;     // its values [es, ee)
+  int32_t tb, tbw;    // tile key bytes: data byte and bit width (-1: RLE, tb = byte after it)
+  __device__ __forceinline__ void emit(int64_t s, int64_t e, uint32_t x, uint32_t y, int64_t b, int w) {
+    if (lane_id() == cnt) {
+      ent = make_uint2(x, y);
+      es = (int32_t)s;
+      ee = (int32_t)e;
+      tb = (int32_t)b;
+      tbw = w;
+    }
+    if (++cnt == 64) flush();
+  }
+  __device__ __forceinline__ void flush() {
+    if (lane_id() < cnt) {
+      runs[base + lane_id()] = ent;
+      tiles_of_run(tf, es, ee, base + lane_id(), tb, tbw);
+    }
+    base += cnt;
+    cnt = 0;
+  }
+};
+
+// Chain mode (streams of short runs, e.g. a bit width 1 key stream that
+// alternates RLE and short bit-packed runs): for the 1 KiB register window,
+// every byte position p gets, in parallel, the position of the header that
+// would follow a one-byte header at p (LDS table).  One lane then hops the
+// chain (one LDS read a header), collecting up to 64 header positions, and
+// the collected runs are decoded and emitted lane-parallel with a wave prefix
+// sum of their lengths.  Anything unusual (multi-byte header, an error, the
+// end of the stream) is left to the exact serial step below.
+constexpr uint32_t NX_STOP = 0xFFFFu;
+
 __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const uint8_t *ks, int64_t slen,
-                          int32_t n, int bw) {
+                          int32_t n, int bw, uint8_t *lbytes, uint16_t *lnx) {
   const int lane = lane_id();
-  uint2 *runs = a.runs + d.run_base;
-  int2 *tf = a.tile_info + d.tile_base;
+  RunBuf R;
+  R.runs = a.runs + d.run_base;
+  R.tf = a.tile_info + d.tile_base;
+  R.base = R.cnt = 0;
+  R.ent = make_uint2(0u, 0u);
+  R.es = R.ee = R.tb = R.tbw = 0;
   const int32_t cap = d.run_cap - 1;  // entries before the sentinel
 
-  int32_t nr = 0;    // runs emitted
   int64_t v = 0;     // values covered
   int64_t hpos = 0;  // next header (stream offset)
   uint32_t err = E_OK;
   Win1K W;
   W.reset();
+  int iters = 0;
   if (bw == 0) {  // hybrid_decoder.go:84-86: all zeros, nothing read
-    if (lane == 0) {
-      runs[0] = make_uint2(RUN_RLE, 0u);
-      tiles_of_run(tf, 0, n, 0, 0, 0);
-    }
-    nr = 1;
+    R.emit(0, n, RUN_RLE, 0u, 0, 0);
     v = n;
   }
+  const int sz = (bw + 7) >> 3;  // RLE value bytes
+  const uint8_t *nx_ab = nullptr;  // window the chain table was built for
+  bool chain = false;              // short runs seen lately: try chain mode
   while (v < n) {
-    if (nr >= cap) {  // cannot happen: runs <= min(n, len / 2 + 1) (host sizing)
+    // ---- chain mode ----
+    if (chain) {
+      if (!W.ab || ks + hpos < W.ab || (ks + hpos) - W.ab > 512) W.fill(ks + hpos);
+      const int64_t wbo = W.ab - ks;  // stream offset of window byte 0
+      if (W.ab != nx_ab) {
+        nx_ab = W.ab;
+        *(uint4 *)(lbytes + 16 * lane) = W.w;
+        const uint32_t wd[4] = {W.w.x, W.w.y, W.w.z, W.w.w};
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+          uint32_t two = 0;
+#pragma unroll
+          for (int k = 0; k < 2; k++) {
+            const uint32_t b = (wd[(i + k) >> 2] >> (8 * ((i + k) & 3))) & 0xffu;
+            const uint32_t r = 16 * lane + i + k, g = b >> 1;
+            uint32_t nx = NX_STOP;
+            if (b < 0x80 && g != 0) nx = min(r + 1 + ((b & 1) ? g * (uint32_t)bw : (uint32_t)sz), NX_STOP - 1);
+            two |= nx << (16 * k);
+          }
+          *(uint32_t *)(lnx + 16 * lane + i) = two;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      int32_t r = (int32_t)(hpos - wbo), cnt = 0;
+      uint32_t myr = 0;
+      while (cnt < 64 && r <= 1024 - 8 - sz && wbo + r < slen) {
+        const uint32_t nx = ufirst((uint32_t)lnx[r]);
+        if (nx == NX_STOP) break;
+        if (lane == cnt) myr = (uint32_t)r;
+        cnt++;
+        r = (int32_t)nx;
+      }
+      if (cnt >= 2) {
+        R.flush();
+        const int32_t nr0 = R.base;
+        const bool in = lane < cnt;
+        const uint32_t b = in ? lbytes[myr] : 0u;
+        const bool bp = (b & 1) != 0;
+        const uint32_t g = b >> 1;
+        const int32_t len = in ? (int32_t)(bp ? g * 8 : g) : 0;
+        uint32_t val = 0;
+        if (in && !bp)
+          for (int k = 0; k < sz; k++) val |= (uint32_t)lbytes[myr + 1 + k] << (8 * k);
+        const int32_t incl = wave_incl_scan32(len);
+        const int64_t st = v + incl - len;
+        const int64_t data = wbo + myr + 1;  // packed data / RLE value
+        bool ok = in && st < n && nr0 + lane < cap;
+        bool bad = false;
+        if (ok) {
+          if (bp) {
+            const int64_t ng = (min<int64_t>((int64_t)len, (int64_t)n - st) + 7) >> 3;
+            bad = data + (ng - 1) * bw >= slen;
+          } else {
+            bad = data + sz > slen || (bw < 32 && (val >> bw) != 0);
+          }
+        }
+        const uint64_t okm = ballot(ok), badm = ballot(ok && bad);
+        const int m = min((int)__popcll(okm), badm ? (int)__builtin_ctzll(badm) : 64);
+        if (m > 0) {
+          if (lane < m) {
+            const int64_t e = min<int64_t>(st + len, (int64_t)n);
+            R.runs[nr0 + lane] = make_uint2((uint32_t)st | (bp ? 0u : RUN_RLE), bp ? (uint32_t)data : val);
+            tiles_of_run(R.tf, st, e, nr0 + lane, bp ? data : data + sz, bp ? bw : -1);
+          }
+          const int32_t last = m - 1;
+          const uint32_t lr = __builtin_amdgcn_readlane(myr, last);
+          const uint32_t lb = __builtin_amdgcn_readlane(b, last);
+          v = min<int64_t>(v + (int64_t)__builtin_amdgcn_readlane((uint32_t)incl, last), (int64_t)n);
+          const int64_t hnext = wbo + lr + 1 + ((lb & 1) ? (int64_t)(lb >> 1) * bw : (int64_t)sz);
+          chain = hnext - hpos < 48 * (int64_t)m;  // still short runs on average
+          hpos = hnext;
+          R.base += m;
+          iters++;
+          continue;
+        }
+      }
+      chain = false;  // nothing to chain here: long runs (or an exact step is due)
+    }
+    // ---- exact serial step ----
+#ifdef PQ_STAMPS
+    if (a.dbg3 && (int)(pi - a.info) == 1 && lane == 0 && iters < 60) {
+      a.dbg3[iters * 4 + 0] = __builtin_amdgcn_s_memrealtime();
+      a.dbg3[iters * 4 + 1] = (uint64_t)hpos;
+      a.dbg3[iters * 4 + 2] = (uint64_t)v;
+      a.dbg3[iters * 4 + 3] = (uint64_t)(R.base + R.cnt);
+    }
+#endif
+    iters++;
+    if (R.base + R.cnt >= cap) {  // cannot happen: runs <= min(n, len / 2 + 1) (host sizing)
       err = E_UNSUPPORTED;
       break;
     }
@@ -704,32 +851,27 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
       // groups the page needs; each must start inside the stream (a short
       // last group is zero-filled, a group starting at the end is io.EOF)
       const int64_t ng = (min<int64_t>(g * 8, (int64_t)n - v) + 7) >> 3;
-      const int64_t have = hpos < slen ? (slen - hpos + bw - 1) / bw : 0;
-      if (have < ng) {
-        if (have > 0 && lane == 0) {
-          runs[nr] = make_uint2((uint32_t)v, (uint32_t)hpos);
-          tiles_of_run(tf, v, v + have * 8, nr, hpos, bw);
-        }
-        if (have > 0) nr++;
+      if (hpos + (ng - 1) * bw >= slen) {
+        const int64_t have = hpos < slen ? (slen - hpos + bw - 1) / bw : 0;
+        if (have > 0) R.emit(v, v + have * 8, (uint32_t)v, (uint32_t)hpos, hpos, bw);
         v += have * 8;
         err = E_EOF;
         break;
       }
       const int64_t e = min<int64_t>(v + g * 8, (int64_t)n);
-      if (lane == 0) {
-        runs[nr] = make_uint2((uint32_t)v, (uint32_t)hpos);
-        tiles_of_run(tf, v, e, nr, hpos, bw);
-      }
-      nr++;
+      R.emit(v, e, (uint32_t)v, (uint32_t)hpos, hpos, bw);
       v = e;
       hpos += g * (int64_t)bw;
       if (v >= n) break;
+      chain = hpos - h0 < 48;  // a short run: the next ones may chain
       // a train?  only if the next header repeats this one (a uvarint's bytes
       // are fixed by its value and length)
       const int64_t stride = hl + g * (int64_t)bw;
       bool same = hpos + hl <= slen;
       for (int q = 0; q < hl && same; q++) same = W.byte_at(ks + hpos + q) == hdr_byte(h, hl, q);
       if (!same) continue;
+      R.flush();
+      const int32_t nr = R.base;
       // lane k checks for the same header again k strides ahead
       const int64_t cand = hpos + (int64_t)lane * stride;  // candidate header of run nr + lane
       const int64_t cstart = v + (int64_t)lane * g * 8;
@@ -743,12 +885,12 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
       const int m = (int)__builtin_ctzll(~okm);  // leading accepted candidates (lanes 0..m-1)
       if (m > 0) {
         if (lane < m) {
-          runs[nr + lane] = make_uint2((uint32_t)cstart, (uint32_t)(cand + hl));
-          tiles_of_run(tf, cstart, min<int64_t>(cstart + g * 8, (int64_t)n), nr + lane, cand + hl, bw);
+          R.runs[nr + lane] = make_uint2((uint32_t)cstart, (uint32_t)(cand + hl));
+          tiles_of_run(R.tf, cstart, min<int64_t>(cstart + g * 8, (int64_t)n), nr + lane, cand + hl, bw);
         }
         v = min<int64_t>(v + (int64_t)m * g * 8, (int64_t)n);
         hpos += (int64_t)m * stride;
-        nr += m;
+        R.base += m;
       }
     } else {  // RLE run (readRLERunValue :116-131)
       const int64_t cr = (int64_t)(h >> 1);
@@ -756,7 +898,6 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
         err = E_RLE;
         break;
       }
-      const int sz = (bw + 7) >> 3;
       if (hpos >= slen || hpos + sz > slen) {
         err = E_EOF;
         break;
@@ -769,24 +910,25 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
         break;
       }
       const int64_t e = min<int64_t>(v + cr, (int64_t)n);
-      if (lane == 0) {
-        runs[nr] = make_uint2((uint32_t)v | RUN_RLE, val);
-        tiles_of_run(tf, v, e, nr, hpos, -1);
-      }
-      nr++;
+      R.emit(v, e, (uint32_t)v | RUN_RLE, val, hpos, -1);
       v = e;
+      chain = true;
     }
   }
+  R.flush();
+  const int32_t nr = R.base;
   const int32_t cover = (int32_t)min<int64_t>(v, (int64_t)n);
   // sentinel, and tiles past the coverage point at it
   const int64_t ntiles = ((int64_t)n + RUN_TILE - 1) / RUN_TILE;
-  for (int64_t t = (cover + RUN_TILE - 1) / RUN_TILE + lane; t < ntiles; t += 64) tf[t] = make_int2(nr, (int32_t)slen);
+  for (int64_t t = (cover + RUN_TILE - 1) / RUN_TILE + lane; t < ntiles; t += 64) R.tf[t] = make_int2(nr, (int32_t)slen);
   if (lane == 0) {
-    runs[nr] = make_uint2((uint32_t)cover, 0u);
+    R.runs[nr] = make_uint2((uint32_t)cover, 0u);
     pi->cover = cover;
     pi->walk_err = err;
     pi->pad = nr;
   }
+  PSTAMP((int)(pi - a.info), 3, (uint64_t)nr);
+  PSTAMP((int)(pi - a.info), 5, (uint64_t)iters);
 }
 
 
@@ -794,10 +936,14 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
 // K3: data page prepare
 // ===========================================================================
 __global__ __launch_bounds__(256) void k_prepare(KArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t wl_bytes[4][1024];  // run walk: window bytes
+  __shared__ __attribute__((aligned(16))) uint16_t wl_nx[4][1024];    // run walk: chain table
+  const int wv = (int)ufirst(threadIdx.x >> 6);
   const int gi = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
   if (gi >= a.nlist) return;
   const int lane = lane_id();
   const int page = ufirst(a.list[gi]);
+  PSTAMP(page, 0, __builtin_amdgcn_s_memrealtime());
   const PageDesc d = a.pages[page];
   PageInfo *pi = &a.info[page];
   if (page_status(a.status, page) != STATUS_OK) return;
@@ -845,7 +991,10 @@ __global__ __launch_bounds__(256) void k_prepare(KArgs a) {
       set_status(a.status, page, ST_VALUES, E_DICT);
       return;
     }
-    walk_runs(a, d, pi, ps.body + ps.val_off + 1, ps.val_len - 1, d.num_values, idx_bw);
+    PSTAMP(page, 1, __builtin_amdgcn_s_memrealtime());
+    walk_runs(a, d, pi, ps.body + ps.val_off + 1, ps.val_len - 1, d.num_values, idx_bw, wl_bytes[wv], wl_nx[wv]);
+    PSTAMP(page, 2, __builtin_amdgcn_s_memrealtime());
+    PSTAMP(page, 4, (uint64_t)idx_bw);
     return;
   }
   if (!(c.flags & COL_NEEDS_COUNT)) return;
@@ -1426,9 +1575,7 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
 // compiler on global_load / global_store instead of flat)
 typedef __attribute__((address_space(1))) const uint32_t g_u32;
 typedef __attribute__((address_space(1))) const uint64_t g_u64;
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ uint32_t gld32(uintptr_t p) { return *(g_u32 *)p; }
 __device__ __forceinline__ uint64_t gld64(uintptr_t p) { return *(g_u64 *)p; }
 __device__ __forceinline__ void gst32(uintptr_t p, uint32_t v) { *(__attribute__((address_space(1))) uint32_t *)p = v; }
@@ -1976,6 +2123,8 @@ struct pq_launch_args {
   const int32_t *job_base;
   const int32_t *job_owner;
   uint64_t *dbg;
+  uint64_t *dbg2;
+  int32_t npages_dbg;
   void *runs;
   void *tile_info;
   const void *tiles;
@@ -2002,6 +2151,8 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   k.job_base = p->job_base;
   k.job_owner = p->job_owner;
   k.dbg = p->dbg;
+  k.dbg2 = p->dbg2;
+  k.dbg3 = p->dbg2 ? p->dbg2 + 8 * (size_t)p->npages_dbg : nullptr;
   k.runs = (uint2 *)p->runs;
   k.tile_info = (int2 *)p->tile_info;
   k.ex_lds = p->ex_lds;
