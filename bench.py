@@ -8,9 +8,11 @@ data (seeded), written with pyarrow on the box, then planned on the host and
 uploaded to HBM once; the timed region is the whole GPU decode pipeline
 (snappy -> prepare -> scan -> decode) with every page already resident.
 
-A "step" decodes every page of the file once.  For N > 1 each rank decodes its
-own identical 100M-row shard on its own GPU (weak scaling, no collective on the
-data path); value = decoded bytes of all ranks / max-over-ranks time.
+A "step" decodes every page of the rank's shard once.  For N > 1 the file holds
+N x 100M rows and each rank decodes a contiguous, byte-balanced slice of its
+row groups (pqgpu.plan_row_group_shards) on its own GPU: weak scaling, no
+collective on the data path; value = decoded bytes of all ranks / max-over-ranks
+time.
 
 Prints ONE JSON line (rank 0).
 """
@@ -105,15 +107,18 @@ def main():
             dist.barrier()
 
     import pqgpu
+    total_rows = args.rows * world
     path = args.file or os.path.join(os.environ.get("TMPDIR", "/tmp"),
-                                     "pqgpu_bench_c2_%d_%d_%d.parquet" % (args.rows, args.rg_rows, args.bw))
+                                     "pqgpu_bench_c2_%d_%d_%d.parquet" % (total_rows, args.rg_rows, args.bw))
     if local == 0 and not os.path.exists(path):
-        make_file(path, args.rows, args.rg_rows, fixed_bw=args.bw)
+        make_file(path, total_rows, args.rg_rows, fixed_bw=args.bw)
     barrier()
 
     ctx = pqgpu.Context(local if world > 1 else 0)
     reader = pqgpu.FileReader(path, ctx=ctx)
-    batch = reader.batch()
+    sizes = [reader.RowGroupByteSize(i) for i in range(reader.RowGroupCount())]
+    rg0, rg1 = pqgpu.plan_row_group_shards(sizes, world)[rank]
+    batch = reader.batch(rg0, rg1)
     stats = batch.stats()
 
     def step():
@@ -135,15 +140,19 @@ def main():
     batch.sync()  # raises if any page failed to decode
     # per-kernel HIP-event times recorded on the decode stream during the timed steps
     kern = {k: [v] for k, v in batch.kernel_times().items()}
+    out_b, in_b = stats["output_bytes"], stats["input_bytes"]
+    job_out = out_b
     if dist is not None:
         import torch
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)  # the slowest rank sets the job time
         dt = float(t.item())
+        nb = torch.tensor([out_b], dtype=torch.float64, device="cuda")
+        dist.all_reduce(nb, op=dist.ReduceOp.SUM)  # every rank's decoded bytes
+        job_out = float(nb.item())
 
-    out_b, in_b = stats["output_bytes"], stats["input_bytes"]
     per_step = dt / args.steps
-    value = out_b * world * args.steps / dt / 1e9
+    value = job_out * args.steps / dt / 1e9
     avg = {k: float(np.mean(v)) for k, v in kern.items()}
     dom = max(avg, key=avg.get)
     # algorithmic bytes per launch of each kernel
@@ -167,7 +176,8 @@ def main():
         "data": "synthetic (seeded pyarrow writer: dictionary INT32, bit widths 1-20 across row groups, snappy, V1)",
         "config": {"workload": "C2: INT32 RLE_DICTIONARY bw 1-20, Snappy, V1, %d rows, %d-row row groups"
                                % (args.rows, args.rg_rows),
-                   "rows_per_gpu": args.rows, "pages": stats["data_pages"], "dict_pages": stats["dict_pages"],
+                   "rows_per_gpu": args.rows, "row_groups": [rg0, rg1],
+                   "pages": stats["data_pages"], "dict_pages": stats["dict_pages"],
                    "B_in": in_b, "B_out": out_b, "staged": stats["staged_bytes"],
                    "pipeline_hbm_frac": round((in_b + out_b) / per_step / 1e9 / HBM_PEAK_GBPS, 4),
                    "kernel_ms": {k: round(v, 4) for k, v in avg.items()},

@@ -179,8 +179,11 @@ int pqg_batch_column(const pqg_batch *b, int i, pqg_column_view *out);
 /* Copy one output buffer of selected column i to host memory. */
 int pqg_batch_copy(pqg_batch *b, int i, int buf_id, void *dst, size_t cap, size_t *nbytes);
 int pqg_batch_stats_get(const pqg_batch *b, pqg_batch_stats *out);
-/* Per-kernel device time (ms) of the last pqg_batch_decode, measured with HIP
- * events on the context stream.  names/ms have room for `cap` entries. */
+/* Device time (ms) per timed segment, averaged over the decodes issued since
+ * the previous call (up to 64), from HIP events on the context stream.  By
+ * default one segment brackets the decode phase (k_decode + k_expand); with
+ * PQG_SEGMENT_TIMES=1 every phase is bracketed (events add launch gaps).
+ * names/ms have room for `cap` entries; returns the number of segments. */
 int pqg_batch_kernel_times(pqg_batch *b, const char **names, float *ms, int cap);
 void pqg_batch_destroy(pqg_batch *b);
 

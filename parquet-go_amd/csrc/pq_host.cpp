@@ -56,7 +56,6 @@ struct pq_launch_args {
   const void *tiles;
   int32_t ntiles, ntiles4;
   int32_t ex_lds;
-  int32_t gather_aux;
 };
 int pq_launch(int which, const pq_launch_args *p, hipStream_t s);
 }
@@ -1505,7 +1504,6 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.runs = B->d_runs;
   a.tile_info = B->d_tile_info;
   a.ex_lds = B->ex_lds;
-  a.gather_aux = getenv("PQG_GATHER_AUX") ? atoi(getenv("PQG_GATHER_AUX")) : 0;
   a.tiles = B->d_tiles;
   a.ntiles = (int32_t)B->tiles.size();
   a.ntiles4 = B->ntiles4;

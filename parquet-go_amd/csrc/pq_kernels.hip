@@ -27,6 +27,20 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
+// global-address-space accessors for addresses held as integers (keeps the
+// compiler on global_load / global_store instead of flat)
+typedef __attribute__((address_space(1))) const uint32_t g_u32;
+typedef __attribute__((address_space(1))) const uint64_t g_u64;
+
+__device__ __forceinline__ uint32_t gld32(uintptr_t p) { return *(g_u32 *)p; }
+__device__ __forceinline__ uint64_t gld64(uintptr_t p) { return *(g_u64 *)p; }
+__device__ __forceinline__ void gst32(uintptr_t p, uint32_t v) { *(__attribute__((address_space(1))) uint32_t *)p = v; }
+__device__ __forceinline__ void gst64(uintptr_t p, uint64_t v) { *(__attribute__((address_space(1))) uint64_t *)p = v; }
+__device__ __forceinline__ void gst128(uintptr_t p, uint4 v) {
+  u32x4 x = {v.x, v.y, v.z, v.w};
+  *(__attribute__((address_space(1))) u32x4 *)p = x;
+}
+
 struct CopyJob {  // dst[0, len) = src[0, len), both in device memory
   const uint8_t *src;
   uint8_t *dst;
@@ -55,7 +69,6 @@ struct KArgs {
   uint2 *runs;            // k_runs -> k_expand: run tables (PageDesc.run_base)
   int2 *tile_info;        // per RUN_TILE values: {first run, byte of its first key} (PageDesc.tile_base)
   int32_t ex_lds;         // k_expand: staged key bytes per wave (dynamic LDS)
-  int32_t gather_aux;     // experiment knob (PQG_GATHER_AUX)
   const TileJob *tiles;   // k_expand: one workgroup per entry
 };
 
@@ -267,6 +280,7 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
   const int64_t dl = (int64_t)dlen;
   // a block that is exactly one literal is its own content: leave it in place
   if (write && lane == 0) a.info[page].alias1 = 0;
+  // (a dictionary only when 8-byte aligned: k_expand gathers aligned entries)
   if (write && dl > 0 && s < slen) {
     uint32_t tag = W.byte_at(src + s);
     if ((tag & 3) == 0) {
@@ -282,7 +296,8 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
           for (int k = 0; k < extra; k++) x |= W.byte_at(src + s + 1 + k) << (8 * k);
         }
       }
-      if (ok && (int64_t)x + 1 == dl && s + hs + dl == slen) {
+      if (ok && (int64_t)x + 1 == dl && s + hs + dl == slen &&
+          (d.kind != PAGE_DICT || ((d.src + lsize + s + hs) & 7) == 0)) {
         if (lane == 0) a.info[page].alias1 = 1 + (int64_t)(d.src + lsize + s + hs);
         return;
       }
@@ -461,42 +476,56 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
 // ===========================================================================
 // K1b: long literals deferred by k_snappy, copied by every workgroup
 // ===========================================================================
-constexpr int COPY_TILE = 4096;  // bytes per workgroup step (256 lanes x 16 B)
+constexpr int COPY_TILE = 4096;   // bytes per workgroup instruction (256 lanes x 16 B)
+constexpr int COPY_CHUNK = 4;     // tiles per work item (16 KiB)
+constexpr int COPY_ITEMS = 4;     // work items per job slot and pass (64 KiB: a google/Go snappy literal)
 
+// Work item i = (job slot i / COPY_ITEMS, chunk i % COPY_ITEMS), grid-strided;
+// a job longer than COPY_ITEMS chunks is covered in passes.  Every load of a
+// chunk is issued before its stores.
 __global__ __launch_bounds__(256) void k_copy(KArgs a) {
-  // a workgroup per job, grid-strided (google/Go snappy literals are <= 64 KB; longer ones loop)
-  for (uint32_t j = blockIdx.x; j < a.max_jobs; j += gridDim.x) {
-  const int32_t q = a.job_owner[j];
-  if ((uint32_t)(j - a.job_base[q]) >= a.njobs[q]) continue;
-  const CopyJob job = a.jobs[j];
-  const int t = threadIdx.x;
-  const uintptr_t d0 = (uintptr_t)job.dst, d1 = d0 + (uintptr_t)job.len;
-  const uintptr_t A = d0 & ~(uintptr_t)15;
-  for (uintptr_t base = A; base < d1; base += 4 * COPY_TILE) {
+  const uint32_t items = a.max_jobs * COPY_ITEMS;
+  for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
+    const uint32_t j = it / COPY_ITEMS, c = it % COPY_ITEMS;
+    const int32_t q = a.job_owner[j];
+    if ((uint32_t)(j - a.job_base[q]) >= a.njobs[q]) continue;
+    const CopyJob job = a.jobs[j];
+    const int t = threadIdx.x;
+    const uintptr_t d0 = (uintptr_t)job.dst, d1 = d0 + (uintptr_t)job.len;
+    const uintptr_t A = d0 & ~(uintptr_t)15;
+    for (uintptr_t base = A + (uintptr_t)c * COPY_CHUNK * COPY_TILE; base < d1;
+         base += (uintptr_t)COPY_ITEMS * COPY_CHUNK * COPY_TILE) {
+      uint4 x[COPY_CHUNK];
+      uint32_t x4[COPY_CHUNK];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      uintptr_t u = base + (uintptr_t)k * COPY_TILE + (uintptr_t)t * 16;
-      if (u >= d1) continue;
-      if (u >= d0 && u + 16 <= d1) {
-        const uint8_t *s = job.src + (u - d0);
-        const uint32_t skew = (uint32_t)((uintptr_t)s & 3);
-        const uint32_t *sa = (const uint32_t *)((uintptr_t)s & ~(uintptr_t)3);
-        uint4 x = *(const uint4 *)sa;
-        uint32_t x4 = sa[4];
-        uint4 o;
-        o.x = __builtin_amdgcn_alignbyte(x.y, x.x, skew);
-        o.y = __builtin_amdgcn_alignbyte(x.z, x.y, skew);
-        o.z = __builtin_amdgcn_alignbyte(x.w, x.z, skew);
-        o.w = __builtin_amdgcn_alignbyte(x4, x.w, skew);
-        *(uint4 *)u = o;
-      } else {
-        for (int b = 0; b < 16; b++) {
-          uintptr_t x = u + b;
-          if (x >= d0 && x < d1) *(uint8_t *)x = job.src[x - d0];
+      for (int k = 0; k < COPY_CHUNK; k++) {
+        const uintptr_t u = base + (uintptr_t)k * COPY_TILE + (uintptr_t)t * 16;
+        const bool whole = u >= d0 && u + 16 <= d1;
+        const uintptr_t sp = (uintptr_t)job.src + (whole ? u - d0 : 0);
+        const uintptr_t sa = sp & ~(uintptr_t)3;
+        x[k] = make_uint4(gld32(sa), gld32(sa + 4), gld32(sa + 8), gld32(sa + 12));
+        x4[k] = gld32(sa + 16);
+      }
+#pragma unroll
+      for (int k = 0; k < COPY_CHUNK; k++) {
+        const uintptr_t u = base + (uintptr_t)k * COPY_TILE + (uintptr_t)t * 16;
+        if (u >= d1) continue;
+        if (u >= d0 && u + 16 <= d1) {
+          const uint32_t skew = (uint32_t)(((uintptr_t)job.src + (u - d0)) & 3);
+          uint4 o;
+          o.x = __builtin_amdgcn_alignbyte(x[k].y, x[k].x, skew);
+          o.y = __builtin_amdgcn_alignbyte(x[k].z, x[k].y, skew);
+          o.z = __builtin_amdgcn_alignbyte(x[k].w, x[k].z, skew);
+          o.w = __builtin_amdgcn_alignbyte(x4[k], x[k].w, skew);
+          gst128(u, o);
+        } else {
+          for (int b = 0; b < 16; b++) {
+            const uintptr_t y = u + b;
+            if (y >= d0 && y < d1) *(uint8_t *)y = job.src[y - d0];
+          }
         }
       }
     }
-  }
   }
 }
 
@@ -1571,20 +1600,6 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
   if (err) set_status(a.status, page, err_stage, err);
 }
 
-// global-address-space accessors for addresses held as integers (keeps the
-// compiler on global_load / global_store instead of flat)
-typedef __attribute__((address_space(1))) const uint32_t g_u32;
-typedef __attribute__((address_space(1))) const uint64_t g_u64;
-
-__device__ __forceinline__ uint32_t gld32(uintptr_t p) { return *(g_u32 *)p; }
-__device__ __forceinline__ uint64_t gld64(uintptr_t p) { return *(g_u64 *)p; }
-__device__ __forceinline__ void gst32(uintptr_t p, uint32_t v) { *(__attribute__((address_space(1))) uint32_t *)p = v; }
-__device__ __forceinline__ void gst64(uintptr_t p, uint64_t v) { *(__attribute__((address_space(1))) uint64_t *)p = v; }
-__device__ __forceinline__ void gst128(uintptr_t p, uint4 v) {
-  u32x4 x = {v.x, v.y, v.z, v.w};
-  *(__attribute__((address_space(1))) u32x4 *)p = x;
-}
-
 // Wave copy of up to MAXC KiB, in passes of 4 KiB with every load of a pass
 // issued before its stores (16-byte aligned stores after a short head,
 // funnel-shifted dword loads).
@@ -1984,13 +1999,7 @@ __global__ __launch_bounds__(256) void k_expand(KArgs a) {
 #pragma unroll
         for (int q = 0; q < 4; q++) {
           if (WIDTH == 4) {
-            switch (a.gather_aux) {  // experiment: cache policy of the dictionary gathers
-              case 1: val[h][r][q] = __builtin_amdgcn_raw_buffer_load_b32(drs, key[r][q] * 4, 0, 1); break;
-              case 2: val[h][r][q] = __builtin_amdgcn_raw_buffer_load_b32(drs, key[r][q] * 4, 0, 2); break;
-              case 3: val[h][r][q] = __builtin_amdgcn_raw_buffer_load_b32(drs, key[r][q] * 4, 0, 16); break;
-              case 4: val[h][r][q] = __builtin_amdgcn_raw_buffer_load_b32(drs, key[r][q] * 4, 0, 17); break;
-              default: val[h][r][q] = __builtin_amdgcn_raw_buffer_load_b32(drs, key[r][q] * 4, 0, 0); break;
-            }
+            val[h][r][q] = __builtin_amdgcn_raw_buffer_load_b32(drs, key[r][q] * 4, 0, 0);
           } else {
             const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(drs, key[r][q] * 8, 0, 0);
             val[h][r][q] = ((uint64_t)x.y << 32) | x.x;
@@ -2130,7 +2139,6 @@ struct pq_launch_args {
   const void *tiles;
   int32_t ntiles, ntiles4;  // k_expand jobs; the first ntiles4 are of 4-byte columns
   int32_t ex_lds;
-  int32_t gather_aux;
 };
 
 static pq::KArgs to_k(const pq_launch_args *p) {
@@ -2156,7 +2164,6 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   k.runs = (uint2 *)p->runs;
   k.tile_info = (int2 *)p->tile_info;
   k.ex_lds = p->ex_lds;
-  k.gather_aux = p->gather_aux;
   k.tiles = (const pq::TileJob *)p->tiles;
   return k;
 }
@@ -2170,7 +2177,8 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
   }
   if (which == 6) {  // deferred literal copies: fixed grid, the job count lives on the device
     if (k.max_jobs == 0) return 0;
-    hipLaunchKernelGGL(pq::k_copy, dim3(k.max_jobs < 2048 ? k.max_jobs : 2048), dim3(256), 0, s, k);
+    const uint32_t items = k.max_jobs * pq::COPY_ITEMS;
+    hipLaunchKernelGGL(pq::k_copy, dim3(items < 4096 ? items : 4096), dim3(256), 0, s, k);
     return hipGetLastError() == hipSuccess ? 0 : 17;
   }
   if (which == 8) {  // k_expand: one workgroup per tile job

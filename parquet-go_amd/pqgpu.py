@@ -350,6 +350,10 @@ class FileReader:
     def RowGroupNumRows(self, rg=None):
         return lib().pqg_file_row_group_num_rows(self._h, self.row_group_position if rg is None else rg)
 
+    def RowGroupByteSize(self, rg):
+        """Σ total_uncompressed_size of the row group's chunks (the shard balancing weight)."""
+        return lib().pqg_file_row_group_byte_size(self._h, rg)
+
     def CurrentRowGroup(self):
         return self.row_group_position
 
@@ -402,3 +406,26 @@ class FileReader:
 
 def NewFileReader(source, *columns, **kw):
     return FileReader(source, *columns, **kw)
+
+
+def plan_row_group_shards(sizes, world):
+    """Contiguous row-group ranges [(rg0, rg1)] for `world` ranks, balanced by
+    the byte sizes `sizes` (one per row group).  Row groups are independent
+    (one dictionary per chunk, chunk_reader.go:221), so a shard needs nothing
+    from its neighbours and the decode path has no collective."""
+    n = len(sizes)
+    total = float(sum(sizes))
+    out, rg = [], 0
+    acc = 0.0
+    for r in range(world):
+        rg0 = rg
+        if r == world - 1:
+            rg = n
+        else:
+            target = total * (r + 1) / world
+            # at least one row group per rank while any remain for the ranks after
+            while rg < n - (world - 1 - r) and (rg == rg0 or acc + sizes[rg] / 2.0 <= target):
+                acc += sizes[rg]
+                rg += 1
+        out.append((rg0, rg))
+    return out

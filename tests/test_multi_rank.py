@@ -1,0 +1,99 @@
+"""N > 1 path on CPU: row-group shards over world_size 2 ranks with gloo.
+
+The decode path has no collective (row groups are independent,
+chunk_reader.go:221); what the multi-GPU bench adds is (1) the shard plan,
+(2) max-over-ranks timing and (3) whole-job aggregation of decoded bytes.
+These tests run that exact logic with 2 gloo ranks on 127.0.0.1, each rank
+decoding its shard with the CPU oracle (the checker), and check that the
+shards tile the file and that the aggregated result equals the whole-file
+decode.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_plan_row_group_shards_tiles_and_balances():
+    import pqgpu
+    sizes = [5, 1, 1, 1, 9, 2, 2, 3]
+    for world in (1, 2, 3, 4, 8, 11):
+        sh = pqgpu.plan_row_group_shards(sizes, world)
+        assert len(sh) == world
+        assert sh[0][0] == 0 and sh[-1][1] == len(sizes)
+        for (a0, a1), (b0, b1) in zip(sh, sh[1:]):
+            assert a1 == b0 and a0 <= a1
+        if world <= len(sizes):
+            assert all(b > a for a, b in sh)
+    # balanced: equal sizes split evenly
+    sh = pqgpu.plan_row_group_shards([1] * 96, 8)
+    assert [b - a for a, b in sh] == [12] * 8
+
+
+def _rank_main(rank, world, port, path, out_dir):
+    import torch
+    import torch.distributed as dist
+    sys.path[:0] = [os.path.join(ROOT, "parquet-go_amd"), os.path.join(ROOT, "oracle")]
+    import oracle
+    import pqgpu
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    data = open(path, "rb").read()
+    r = pqgpu.FileReader(data)  # host-side metadata only: no GPU needed
+    sizes = [r.RowGroupByteSize(i) for i in range(r.RowGroupCount())]
+    rg0, rg1 = pqgpu.plan_row_group_shards(sizes, world)[rank]
+    import time
+    t0 = time.perf_counter()
+    got = oracle.File(data).decode(0, rg0, rg1)
+    dt = time.perf_counter() - t0
+    vals = np.asarray(got["values"]).view(np.uint8)
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)  # the bench's max-over-ranks time
+    nb = torch.tensor([vals.size], dtype=torch.int64)
+    dist.all_reduce(nb, op=dist.ReduceOp.SUM)  # whole-job decoded bytes
+    parts = [None] * world
+    dist.all_gather_object(parts, (rg0, rg1, vals.tobytes()))
+    if rank == 0:
+        np.save(os.path.join(out_dir, "agg.npy"),
+                np.frombuffer(b"".join(p[2] for p in parts), np.uint8))
+        with open(os.path.join(out_dir, "meta.txt"), "w") as f:
+            f.write("%d %f %s\n" % (int(nb.item()), float(t.item()), ";".join("%d-%d" % p[:2] for p in parts)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo_shards_match_whole_file(tmp_path):
+    pa = pytest.importorskip("pyarrow")
+    import pyarrow.parquet as pq
+    torch = pytest.importorskip("torch")
+    import torch.multiprocessing as mp
+    import oracle
+    rng = np.random.default_rng(7)
+    n = 60000
+    path = str(tmp_path / "shards.parquet")
+    keys = rng.integers(0, 300, n)
+    dvals = rng.permutation(1 << 16)[:300].astype(np.int32)
+    pq.write_table(pa.table({"v": pa.array(dvals[keys])}), path, row_group_size=7000, compression="snappy",
+                   use_dictionary=True)
+    world = 2
+    mp.spawn(_rank_main, args=(world, _free_port(), path, str(tmp_path)), nprocs=world, join=True)
+    agg = np.load(str(tmp_path / "agg.npy"))
+    nbytes, tmax, shards = open(str(tmp_path / "meta.txt")).read().split()
+    whole = np.asarray(oracle.File(open(path, "rb").read()).decode(0)["values"]).view(np.uint8)
+    assert int(nbytes) == whole.size == agg.size
+    assert np.array_equal(agg, whole)
+    assert float(tmax) > 0
+    (a0, a1), (b0, b1) = [tuple(map(int, s.split("-"))) for s in shards.split(";")]
+    assert a0 == 0 and a1 == b0 and b1 == pq.ParquetFile(path).num_row_groups
