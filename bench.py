@@ -52,31 +52,86 @@ def make_file(path, rows, rg_rows, seed=2, fixed_bw=0):
     os.replace(tmp, path)
 
 
-def cpu_baseline(path, budget_s=10.0):
-    """The CPU oracle (a serial C port of the reference read path) on a bounded
-    sample of the same file: whole row groups until ~budget_s of CPU time."""
+def cpu_baseline(path, budget_s=10.0, threads=None):
+    """The CPU oracle (a C port of the reference read path) on a bounded sample
+    of the same file: whole row groups, one per worker thread at a time (the
+    oracle releases the GIL inside its C calls), until ~budget_s of wall time.
+    `threads` defaults to the 16-core CPU share of a GPU box."""
+    import concurrent.futures as cf
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     data = open(path, "rb").read()
     f = oracle.File(data)
     L = oracle.lib()
-    t_total, out_bytes, rows, rgs = 0.0, 0, 0, 0
-    for rg in range(f.num_row_groups):
+    threads = threads or min(16, os.cpu_count() or 1)
+
+    def one(rg):
         r = ctypes.c_void_p()
-        t0 = time.perf_counter()
         st = L.pqref_decode(f._h, 0, rg, rg + 1, ctypes.byref(r))
-        t_total += time.perf_counter() - t0
         if st != 0:
             raise RuntimeError("oracle failed on the bench file: %d" % st)
-        out_bytes += L.pqref_result_count(r, oracle.CNT_SLOTS) * 4
-        rows += L.pqref_result_count(r, oracle.CNT_SLOTS)
+        n = L.pqref_result_count(r, oracle.CNT_SLOTS)
         L.pqref_result_free(r)
-        rgs += 1
-        if t_total >= budget_s:
-            break
-    return {"value": out_bytes / t_total / 1e9, "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": "oracle/pqref.c single-thread on %d of %d row groups (%d rows) of the bench file, %.1f s"
-                      % (rgs, f.num_row_groups, rows, t_total)}
+        return n
+
+    out_bytes, rows, rgs = 0, 0, 0
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(threads) as ex:
+        rg = 0
+        while rg < f.num_row_groups and time.perf_counter() - t0 < budget_s:
+            wave = list(range(rg, min(rg + threads, f.num_row_groups)))
+            for n in ex.map(one, wave):
+                out_bytes += n * 4
+                rows += n
+            rgs += len(wave)
+            rg += len(wave)
+    t_total = time.perf_counter() - t0
+    return {"value": out_bytes / t_total / 1e9, "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": "oracle/pqref.c on %d threads, %d of %d row groups (%d rows) of the bench file, %.1f s wall"
+                      % (threads, rgs, f.num_row_groups, rows, t_total)}
+
+
+def pmc_traffic(args, kernels=("k_expand", "k_decode")):
+    """HBM bytes per launch of the decode phase from rocprofv3 PMC counters,
+    collected in separate passes (FETCH_SIZE, then WRITE_SIZE) over a short
+    child run of this same bench; MI355X_MICROARCH.md: on gfx950 FETCH_SIZE
+    reports half of a wide streaming read, so it is doubled.  None when the
+    profiler is unavailable or a pass fails."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    if not shutil.which("rocprofv3"):
+        return None
+    base = [sys.executable, os.path.abspath(__file__), "--no-cpu", "--no-pmc", "--steps", "3", "--warmup", "1",
+            "--rows", str(args.rows), "--rg-rows", str(args.rg_rows), "--bw", str(args.bw)]
+    if args.file:
+        base += ["--file", args.file]
+    per = {}
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            out = os.path.join(td, ctr)
+            cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", ctr, "--output-format", "csv",
+                   "-d", out, "-o", "run", "--"] + base
+            try:
+                subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, check=True, timeout=150)
+            except Exception:
+                return None
+            vals = {}
+            for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+                for r in csv.DictReader(open(f)):
+                    if any(k in r["Kernel_Name"] for k in kernels) and r["Counter_Name"] == ctr:
+                        vals.setdefault(r["Dispatch_Id"], 0.0)
+                        vals[r["Dispatch_Id"]] += float(r["Counter_Value"])
+            if not vals:
+                return None
+            per[ctr] = sorted(vals.values())
+    # kilobytes per dispatch; one launch of the phase may be several dispatches (k_expand<4>, <8>, k_decode)
+    n_launch = 4  # 1 warmup + 3 timed steps of the child run
+    fetch = sum(per["FETCH_SIZE"]) / n_launch * 1024 * 2
+    write = sum(per["WRITE_SIZE"]) / n_launch * 1024
+    return fetch + write
 
 
 def main():
@@ -89,6 +144,7 @@ def main():
     ap.add_argument("--file", default=None)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes behind roofline.traffic")
     ap.add_argument("--bw", type=int, default=0, help="analysis: one dictionary bit width for every row group")
     args = ap.parse_args()
 
@@ -187,6 +243,10 @@ def main():
     }
     if rank == 0 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(path, args.cpu_budget)
+    if rank == 0 and world == 1 and not args.no_pmc:
+        tr = pmc_traffic(args)
+        line["roofline"]["traffic"] = None if tr is None else round(tr / 1e6, 1)
+        line["roofline"]["traffic_unit"] = "MB per launch (FETCH_SIZE x 2 + WRITE_SIZE)"
     if rank == 0:
         print(json.dumps(line), flush=True)
     batch.close()
