@@ -65,6 +65,8 @@ struct PageDesc {
   int64_t run_base;      // tiled RLE_DICTIONARY page: first entry of its run table (k_runs -> k_expand)
   int32_t run_cap;       // run-table entries reserved for the page (runs + sentinel)
   int32_t tile_base;     // tiled page: first entry of its tile -> first-run index table
+  int32_t job_base;      // tiled page: first entry of its job -> position table (page_jobs)
+  int32_t pad1;
 };
 
 // Tiled flat decode (k_prepare's run walk + k_expand).  The run walk records,
@@ -81,6 +83,25 @@ struct TileJob {         // one k_expand workgroup (host-built, XCD-affine order
   int32_t width;         // value bytes (4 / 8)
   int32_t pad;
 };
+// What k_expand needs about one job, written by k_prepare at the job's
+// position in the launch order (one 64-byte scalar load).  A record is
+// current only when `epoch` matches the decode's epoch: a page that failed
+// before k_prepare leaves stale records, which k_expand skips.
+struct ExRec {
+  const uint8_t *vals;   // values section (PLAIN values; RLE_DICTIONARY: bit-width byte, then keys)
+  const uint8_t *dict;   // dictionary values
+  const uint2 *runs;     // the page's run table
+  int32_t v0, lim;       // decode values [v0, lim) of the page (lim <= v0: nothing)
+  int32_t bw;            // key bit width; -1: PLAIN
+  int32_t nr;            // run entries (the sentinel is entry nr)
+  int32_t first_run;     // run holding value v0
+  int32_t byte_lo, byte_hi;  // key-stream bytes holding keys [v0, lim) (byte_hi exclusive, before slack)
+  uint32_t dict_n;       // dictionary entries
+  uint32_t epoch;
+  int32_t val_len;       // values section bytes
+};
+static_assert(sizeof(ExRec) == 64, "one scalar load");
+
 // One RLE/bit-packed run of a key stream (hybrid_decoder.go:143-166), as
 // written by k_runs: x = first value (page-relative) | RUN_RLE for an RLE run;
 // y = the repeated value (RLE) or the byte offset of the run's packed data in

@@ -56,6 +56,9 @@ struct pq_launch_args {
   const void *tiles;
   int32_t ntiles, ntiles4;
   int32_t ex_lds;
+  void *recs;
+  const int32_t *page_jobs;
+  uint32_t epoch;
 };
 int pq_launch(int which, const pq_launch_args *p, hipStream_t s);
 }
@@ -529,6 +532,10 @@ struct pqg_batch {
   void *d_tile_info = nullptr;     // per RUN_TILE values of a tiled page: {first run, first key byte}
   int32_t ex_lds = 0;              // k_expand staged key bytes per wave
   int32_t ntiles4 = 0;             // k_expand jobs of 4-byte columns (they come first)
+  void *d_recs = nullptr;          // k_expand job records (k_prepare writes them every decode)
+  int32_t *d_page_jobs = nullptr;  // per tiled page: positions of its jobs in the launch order
+  int64_t page_job_entries = 0;
+  uint32_t epoch = 0;
   TileJob *d_tiles = nullptr;
   uint32_t *h_status = nullptr;  // pinned mirror
   std::vector<ColDesc> hcols;
@@ -1059,6 +1066,7 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
     const PageHeader &h = w.h;
     PageDesc d;
     memset(&d, 0, sizeof(d));
+    d.job_base = -1;  // not a tiled page
     d.col = ci;
     d.rg = rg;
     d.ord = w.ord;
@@ -1248,6 +1256,8 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
     }
     const int32_t n = std::max(d.num_values, 0);
     const int32_t nt = (n + RUN_TILE - 1) / RUN_TILE;
+    d.job_base = (int32_t)B->page_job_entries;
+    B->page_job_entries += (n + EX_WAVE_VALUES - 1) / EX_WAVE_VALUES;
     d.tile_base = (int32_t)B->tile_entries;
     B->tile_entries += nt;
     if (d.enc == ENC_RLE_DICT) {
@@ -1312,8 +1322,21 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   rc |= alloc_dev((void **)&B->d_lists, sizeof(int32_t) * nl);
   rc |= alloc_dev(&B->d_runs, 8 * (size_t)(B->run_entries + 64));
   rc |= alloc_dev(&B->d_tile_info, 8 * (size_t)(B->tile_entries + EX_WAVE_VALUES / RUN_TILE + 1));
-  B->ex_lds = (B->ex_lds + 255) & ~255;
+  B->ex_lds = (B->ex_lds + 1023) & ~1023;  // whole 1 KiB LDS-DMA chunks
   rc |= alloc_dev((void **)&B->d_tiles, sizeof(TileJob) * (B->tiles.size() + 1));
+  rc |= alloc_dev(&B->d_recs, sizeof(ExRec) * (B->tiles.size() + 1));
+  rc |= alloc_dev((void **)&B->d_page_jobs, sizeof(int32_t) * (size_t)(B->page_job_entries + 1));
+  if (!rc) {
+    // positions of every page's jobs in the launch order; records start stale (epoch 0)
+    std::vector<int32_t> pj((size_t)B->page_job_entries + 1, 0);
+    for (size_t p = 0; p < B->tiles.size(); p++) {
+      const TileJob &tj = B->tiles[p];
+      if (tj.page < 0) continue;
+      pj[(size_t)B->pages[(size_t)tj.page].job_base + (size_t)(tj.v0 / EX_WAVE_VALUES)] = (int32_t)p;
+    }
+    hipMemcpy(B->d_page_jobs, pj.data(), sizeof(int32_t) * pj.size(), hipMemcpyHostToDevice);
+    hipMemset(B->d_recs, 0, sizeof(ExRec) * (B->tiles.size() + 1));
+  }
   // per Snappy page a region of job slots: at most body_len / 16 KB literals are long enough to defer
   std::vector<int32_t> job_base(B->snappy_list.size() + 1), job_owner;
   for (size_t q = 0; q < B->snappy_list.size(); q++) {
@@ -1504,6 +1527,9 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.runs = B->d_runs;
   a.tile_info = B->d_tile_info;
   a.ex_lds = B->ex_lds;
+  a.recs = B->d_recs;
+  a.page_jobs = B->d_page_jobs;
+  a.epoch = ++B->epoch;
   a.tiles = B->d_tiles;
   a.ntiles = (int32_t)B->tiles.size();
   a.ntiles4 = B->ntiles4;
@@ -1748,6 +1774,8 @@ void pqg_batch_destroy(pqg_batch *B) {
   hipFree(B->d_runs);
   hipFree(B->d_tile_info);
   hipFree(B->d_tiles);
+  hipFree(B->d_recs);
+  hipFree(B->d_page_jobs);
   if (B->h_status) hipHostFree(B->h_status);
   for (int k = 0; k < pqg_batch::kRing; k++)
     for (int i = 0; i < 8; i++)

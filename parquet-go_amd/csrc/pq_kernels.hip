@@ -69,6 +69,9 @@ struct KArgs {
   uint2 *runs;            // k_runs -> k_expand: run tables (PageDesc.run_base)
   int2 *tile_info;        // per RUN_TILE values: {first run, byte of its first key} (PageDesc.tile_base)
   int32_t ex_lds;         // k_expand: staged key bytes per wave (dynamic LDS)
+  ExRec *recs;            // k_prepare -> k_expand: one record per job (launch order)
+  const int32_t *page_jobs;  // per tiled page (PageDesc.job_base): positions of its jobs
+  uint32_t epoch;         // this decode's record epoch
   const TileJob *tiles;   // k_expand: one workgroup per entry
 };
 
@@ -730,7 +733,7 @@ struct RunBuf {
 constexpr uint32_t NX_STOP = 0xFFFFu;
 
 __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const uint8_t *ks, int64_t slen,
-                          int32_t n, int bw, uint8_t *lbytes, uint16_t *lnx) {
+                          int32_t n, int bw, uint8_t *lbytes, uint16_t *lnx, const uint8_t *dict, uint32_t dict_n) {
   const int lane = lane_id();
   RunBuf R;
   R.runs = a.runs + d.run_base;
@@ -956,8 +959,31 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
     pi->walk_err = err;
     pi->pad = nr;
   }
+  // k_expand records, lane k = job k (read back this wave's own tile stores)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int32_t njobs = (n + EX_WAVE_VALUES - 1) / EX_WAVE_VALUES;
+  for (int32_t k = lane; k < njobs; k += 64) {
+    const int32_t v0 = k * EX_WAVE_VALUES, v1 = min(v0 + EX_WAVE_VALUES, n);
+    const int2 t0 = R.tf[v0 / RUN_TILE];
+    ExRec rc;
+    rc.vals = ks - 1;
+    rc.dict = dict;
+    rc.runs = R.runs;
+    rc.v0 = v0;
+    rc.lim = min(v1, cover);
+    rc.bw = bw;
+    rc.nr = nr;
+    rc.first_run = t0.x;
+    rc.byte_lo = t0.y;
+    rc.byte_hi = v1 >= n ? (int32_t)slen : R.tf[v1 / RUN_TILE].y;
+    rc.dict_n = dict_n;
+    rc.epoch = a.epoch;
+    rc.val_len = (int32_t)slen + 1;
+    a.recs[a.page_jobs[d.job_base + k]] = rc;
+  }
   PSTAMP((int)(pi - a.info), 3, (uint64_t)nr);
   PSTAMP((int)(pi - a.info), 5, (uint64_t)iters);
+  (void)iters;
 }
 
 
@@ -1021,9 +1047,34 @@ __global__ __launch_bounds__(256) void k_prepare(KArgs a) {
       return;
     }
     PSTAMP(page, 1, __builtin_amdgcn_s_memrealtime());
-    walk_runs(a, d, pi, ps.body + ps.val_off + 1, ps.val_len - 1, d.num_values, idx_bw, wl_bytes[wv], wl_nx[wv]);
+    const PageDesc dp = a.pages[d.dict];
+    walk_runs(a, d, pi, ps.body + ps.val_off + 1, ps.val_len - 1, d.num_values, idx_bw, wl_bytes[wv], wl_nx[wv],
+              body_ptr(a, dp, d.dict), (uint32_t)dp.num_values);
     PSTAMP(page, 2, __builtin_amdgcn_s_memrealtime());
     PSTAMP(page, 4, (uint64_t)idx_bw);
+    return;
+  }
+  if (d.job_base >= 0 && d.enc == ENC_PLAIN) {  // tiled PLAIN page: k_expand records
+    const int32_t n = d.num_values;
+    if ((int64_t)n * c.width > ps.val_len) {  // binary.Read past the values section
+      set_status(a.status, page, ST_VALUES, E_EOF);
+      return;
+    }
+    const int32_t njobs = (n + EX_WAVE_VALUES - 1) / EX_WAVE_VALUES;
+    for (int32_t k = lane; k < njobs; k += 64) {
+      ExRec rc;
+      rc.vals = ps.body + ps.val_off;
+      rc.dict = nullptr;
+      rc.runs = nullptr;
+      rc.v0 = k * EX_WAVE_VALUES;
+      rc.lim = min(rc.v0 + EX_WAVE_VALUES, n);
+      rc.bw = -1;
+      rc.nr = rc.first_run = rc.byte_lo = rc.byte_hi = 0;
+      rc.dict_n = 0;
+      rc.epoch = a.epoch;
+      rc.val_len = (int32_t)ps.val_len;
+      a.recs[a.page_jobs[d.job_base + k]] = rc;
+    }
     return;
   }
   if (!(c.flags & COL_NEEDS_COUNT)) return;
@@ -1790,6 +1841,32 @@ constexpr int EX_ROW = 256;                   // values per row (4 per lane)
 constexpr int EX_ROWS = EX_WAVE / EX_ROW;     // rows per wave
 static_assert(EX_WAVE % RUN_TILE == 0, "tile_info granularity");
 
+// The four keys of a lane whose first key sits at staged bit lb0, all in one
+// bit-packed run: CLS 0 (bw <= 8) one 32-bit window, 1 (bw <= 16) one 64-bit
+// window, 2 a dword pair per key.
+template <int CLS>
+__device__ __forceinline__ void row_keys(const uint32_t *kspan, uint32_t lb0, int bw, uint32_t mask, uint32_t (&k)[4]) {
+  const uint32_t *dw = kspan + (lb0 >> 5);
+  const uint32_t sh = lb0 & 31;
+  if (CLS == 0) {
+    const uint32_t x = __builtin_amdgcn_alignbit(dw[1], dw[0], sh);
+#pragma unroll
+    for (int q = 0; q < 4; q++) k[q] = __builtin_amdgcn_ubfe(x, (uint32_t)(q * bw), (uint32_t)bw);
+  } else if (CLS == 1) {
+    const uint32_t d1 = dw[1];
+    const uint64_t x = ((uint64_t)__builtin_amdgcn_alignbit(dw[2], d1, sh) << 32) | __builtin_amdgcn_alignbit(d1, dw[0], sh);
+#pragma unroll
+    for (int q = 0; q < 4; q++) k[q] = (uint32_t)(x >> (q * bw)) & mask;
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t lb = lb0 + (uint32_t)(q * bw);
+      const uint32_t *dq = kspan + (lb >> 5);
+      k[q] = __builtin_amdgcn_alignbit(dq[1], dq[0], lb & 31) & mask;
+    }
+  }
+}
+
 template <int WIDTH>
 __global__ __launch_bounds__(256) void k_expand(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t kspan_dyn[];
@@ -1799,85 +1876,46 @@ __global__ __launch_bounds__(256) void k_expand(KArgs a) {
   const int job = (int)blockIdx.x * 4 + wv;
   if (job >= a.nlist) return;
   const TileJob tj = a.tiles[job];
-  const int page = tj.page, dpage = tj.dict >= 0 ? tj.dict : tj.page;
-  // 1. every descriptor load is independent of the others: one round trip
-  ExPage P;
-  const int2 ti0 = a.tile_info[tj.tf], ti1 = a.tile_info[tj.tf + EX_WAVE / RUN_TILE];
-  {
-    const uint32_t st = a.status[page], dst = a.status[dpage];
-    const PageDesc *pd = &a.pages[page];
-    const PageInfo *pi = &a.info[page];
-    const PageDesc *dd = &a.pages[dpage];
-    P.n = pd->num_values;
-    P.plain = pd->enc == ENC_PLAIN;
-    P.cover = pi->cover;
-    P.nr = pi->pad;
-    P.bw = pi->idx_bw;
-    P.val_len = pi->val_len;
-    P.dict_n = (uint32_t)dd->num_values;
-    P.vals = body_of(a, pd->body_src, pd->body, pi->alias1) + pi->val_off;
-    P.dict = body_of(a, dd->body_src, dd->body, a.info[dpage].alias1);
-    P.runs = a.runs + pd->run_base;
-    P.ok = st == STATUS_OK && dst == STATUS_OK;
-  }
-  if (!P.ok) return;
+  const ExRec rc = a.recs[job];  // written by this decode's k_prepare, or stale (epoch)
+  const int page = tj.page;
+  if (rc.epoch != a.epoch) return;  // the page failed before k_prepare finished it
   STAMP(1);
-  const int32_t v0 = tj.v0;
-  const int32_t v1 = min(v0 + EX_WAVE, P.n);
-  if (v0 >= v1) return;
+  const int32_t v0 = rc.v0, lim = rc.lim;
+  if (v0 >= lim) return;
   constexpr int w = WIDTH;
-
-  if (P.plain) {
-    if ((int64_t)P.n * w > P.val_len) {  // binary.Read past the values section
-      set_status(a.status, page, ST_VALUES, E_EOF);
-      return;
-    }
-    copy_tile<EX_WAVE * 8 / 1024>(P.vals + (int64_t)v0 * w, tj.out + (int64_t)v0 * w, (int64_t)(v1 - v0) * w, lane);
+  if (rc.bw < 0) {  // PLAIN (type_int32.go:23-37, type_int64.go:23-37): a copy of the job's bytes
+    copy_tile<EX_WAVE * 8 / 1024>(rc.vals + (int64_t)v0 * w, tj.out + (int64_t)v0 * w, (int64_t)(lim - v0) * w, lane);
     return;
   }
-
   // ---- RLE_DICTIONARY ----
-  if (tj.dict < 0) return;                  // reported by walk_runs
-  const int32_t lim = min(v1, P.cover);     // values before a key-stream header error
-  if (v0 >= lim) return;
+  ExPage P;
+  P.nr = rc.nr;
+  P.bw = rc.bw;
+  P.val_len = rc.val_len;
+  P.dict_n = rc.dict_n;
+  P.vals = rc.vals;
+  P.dict = rc.dict;
+  P.runs = rc.runs;
   const int bw = P.bw;
   const uint8_t *ks = P.vals + 1;
   const int64_t slen = (int64_t)P.val_len - 1;
   // 2. window and staged key bytes, in parallel
   RunWin W;
-  W.load(P.runs, P.nr, ti0.x);
-  const int64_t byte_lo = ti0.y, byte_hi = (v1 >= P.n ? slen : (int64_t)ti1.y) + 16;
+  W.load(P.runs, P.nr, rc.first_run);
+  const int64_t byte_lo = rc.byte_lo, byte_hi = (int64_t)rc.byte_hi + 16;
   const uintptr_t A = ((uintptr_t)ks + (uintptr_t)byte_lo) & ~(uintptr_t)15;
   const int64_t nb = (int64_t)((uintptr_t)ks + (uintptr_t)byte_hi - A);
   const int ex_lds = a.ex_lds;
   uint32_t *kspan = kspan_dyn + wv * (ex_lds / 4);
   const bool staged = nb <= ex_lds;
   if (staged) {
-    constexpr int NC = EX_WAVE * 4 / 1024 + 1;  // covers 32-bit keys
-    const uintptr_t E = (uintptr_t)ks + (uintptr_t)slen;  // stream end: bytes at/after it read as zero
-    uint4 x[NC];
-#pragma unroll
-    for (int i = 0; i < NC; i++) {
-      const int64_t off = (int64_t)(lane + 64 * i) * 16;
-      const uintptr_t src = A + (uintptr_t)(off < nb ? off : 0);
-      const uint64_t lo8 = gld64(src), hi8 = gld64(src + 8);
-      x[i] = make_uint4((uint32_t)lo8, (uint32_t)(lo8 >> 32), (uint32_t)hi8, (uint32_t)(hi8 >> 32));
-    }
-#pragma unroll
-    for (int i = 0; i < NC; i++) {
-      const int64_t off = (int64_t)(lane + 64 * i) * 16;
-      if (off < nb) {
-        const uintptr_t c = A + (uintptr_t)off;
-        uint32_t v4[4] = {x[i].x, x[i].y, x[i].z, x[i].w};
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const uintptr_t d0 = c + 4 * q;
-          if (d0 + 4 <= E) continue;
-          v4[q] = d0 >= E ? 0u : (v4[q] & ((1u << (8 * (uint32_t)(E - d0))) - 1));
-        }
-        *(uint4 *)(kspan + off / 4) = make_uint4(v4[0], v4[1], v4[2], v4[3]);
-      }
-    }
+    // LDS-DMA: lane l's 16 bytes of chunk i land at kspan + 1024 i + 16 l.  Bytes
+    // past the stream end are never used as key bits (fast rows stay inside it,
+    // the general path masks them), so they are staged as they are.
+    const uintptr_t src = A + 16 * (uintptr_t)lane;
+    for (int32_t off = 0; off < nb; off += 1024)
+      __builtin_amdgcn_global_load_lds((const void *)(src + off),
+                                       (__attribute__((address_space(3))) void *)(kspan + off / 4), 16, 0, 0);
   }
   // every run meeting [v0, lim) must sit in lanes 0..62 (its end is the next lane's start),
   // and no row of EX_ROW values may hold two run starts (rows meet at most two runs)
@@ -1891,12 +1929,18 @@ __global__ __launch_bounds__(256) void k_expand(KArgs a) {
       expand_direct(a, P, page, w, tj.out, c, min(c + 512, lim), a.tile_info[tj.tf + (c - v0) / RUN_TILE].x);
     return;
   }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the staged bytes (LDS-DMA) and the window
   STAMP(3);
   const int64_t lbase = (int64_t)(A - (uintptr_t)ks) * 8;  // stream bit of kspan bit 0
   const int64_t end_bit = slen * 8;
   const uint32_t mask = bw >= 32 ? 0xffffffffu : ((1u << bw) - 1);
   const uint32_t dsh = (uint32_t)((uintptr_t)P.dict & 3);
+  // per window lane (run): the staged bit of its key j is c + j * bw, and okm
+  // marks bit-packed runs whose keys all lie inside the stream (the fast rows)
+  const int32_t w_end = (int32_t)shfl32((uint32_t)W.start, min(lane + 1, 63));
+  const int32_t w_c = (int32_t)(W.prm * 8) - W.start * bw - (int32_t)lbase;
+  const uint64_t okm = ballot(!W.rle && W.start != 0x7fffffff &&
+                              (int64_t)W.prm * 8 + (int64_t)(min(w_end, lim) - W.start) * bw <= end_bit);
   // 3. per half (four rows, value j = row start + 4 lane + q): keys from LDS,
   //    range check, then the half's gathers back to back; stores trail.
   //    Dictionary reads and output writes go through buffer resources
@@ -1904,9 +1948,10 @@ __global__ __launch_bounds__(256) void k_expand(KArgs a) {
   const __amdgpu_buffer_rsrc_t drs =
       __builtin_amdgcn_make_buffer_rsrc((void *)P.dict, (short)0, (int)(P.dict_n * (uint32_t)w + 8), 0x00020000);
   const __amdgpu_buffer_rsrc_t ors =
-      __builtin_amdgcn_make_buffer_rsrc((void *)tj.out, (short)0, (int)((uint32_t)P.n * (uint32_t)w), 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void *)tj.out, (short)0, (int)((uint32_t)lim * (uint32_t)w), 0x00020000);
   constexpr int HR = EX_ROWS / 2;
   const int32_t end_bit32 = (int32_t)end_bit;
+  const int cls = bw <= 8 ? 0 : bw <= 16 ? 1 : 2;
   typedef typename std::conditional<WIDTH == 4, uint32_t, uint64_t>::type VT;
   VT val[2][HR][4];
 #pragma unroll
@@ -1925,39 +1970,25 @@ __global__ __launch_bounds__(256) void k_expand(KArgs a) {
       const uint64_t m = ballot(W.start <= rl);
       const int32_t ri = max((int32_t)__popcll(m) - 1, 0);
       // at most two runs meet a row (checked per wave above): the row's run and the next
-      const int32_t s0 = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, ri);
-      const uint32_t p0 = __builtin_amdgcn_readlane(W.prm, ri), f0 = __builtin_amdgcn_readlane(W.rle, ri);
       const int32_t s1 = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, ri + 1);
-      const uint32_t p1 = __builtin_amdgcn_readlane(W.prm, ri + 1), f1 = __builtin_amdgcn_readlane(W.rle, ri + 1);
-      // staged bit of key j inside a bit-packed run: c + j * bw
-      const int32_t c0 = (int32_t)(p0 * 8) - s0 * bw - (int32_t)lbase, c1 = (int32_t)(p1 * 8) - s1 * bw - (int32_t)lbase;
-      const bool fast = !f0 && (s1 >= rh || !f1) && rh - rl == EX_ROW &&
-                        (s1 >= rh ? (int64_t)p0 * 8 + (int64_t)(rh - s0) * bw
-                                  : (int64_t)p1 * 8 + (int64_t)(rh - s1) * bw) <= end_bit;
+      const int32_t c0 = (int32_t)__builtin_amdgcn_readlane((uint32_t)w_c, ri);
+      const bool one = s1 >= rh;  // the whole row inside run ri
+      const bool fast = ((okm >> ri) & 1) && (one || ((okm >> (ri + 1)) & 1)) && rh - rl == EX_ROW;
       if (fast) {  // full row, bit-packed runs only, nothing past the stream end
-        // the lane's four keys are consecutive in one run unless a run starts among them
-        const bool split = j0 < s1 && j0 + 3 >= s1;
-        const uint32_t lb0 = (uint32_t)((j0 >= s1 ? c1 : c0) + j0 * bw);
-        const uint32_t *dw = kspan + (lb0 >> 5);
-        if (bw <= 8) {  // all four keys inside one 32-bit window
-          const uint32_t x = __builtin_amdgcn_alignbit(dw[1], dw[0], lb0 & 31);
-#pragma unroll
-          for (int q = 0; q < 4; q++) key[r][q] = __builtin_amdgcn_ubfe(x, (uint32_t)(q * bw), (uint32_t)bw);
-        } else if (bw <= 16) {  // ... inside one 64-bit window
-          const uint32_t d2 = dw[2];
-          const uint64_t x = ((uint64_t)__builtin_amdgcn_alignbit(d2, dw[1], lb0 & 31) << 32) |
-                             __builtin_amdgcn_alignbit(dw[1], dw[0], lb0 & 31);
-#pragma unroll
-          for (int q = 0; q < 4; q++) key[r][q] = (uint32_t)(x >> (q * bw)) & mask;
+        uint32_t lb0;
+        if (one) {
+          lb0 = (uint32_t)(c0 + j0 * bw);
         } else {
-#pragma unroll
-          for (int q = 0; q < 4; q++) {
-            const uint32_t lb = lb0 + (uint32_t)(q * bw);
-            const uint32_t *dq = kspan + (lb >> 5);
-            key[r][q] = __builtin_amdgcn_alignbit(dq[1], dq[0], lb & 31) & mask;
-          }
+          const int32_t c1 = (int32_t)__builtin_amdgcn_readlane((uint32_t)w_c, ri + 1);
+          lb0 = (uint32_t)((j0 >= s1 ? c1 : c0) + j0 * bw);
         }
-        if (split) {  // the one lane of the row where a run starts (rare)
+        switch (cls) {
+          case 0: row_keys<0>(kspan, lb0, bw, mask, key[r]); break;
+          case 1: row_keys<1>(kspan, lb0, bw, mask, key[r]); break;
+          default: row_keys<2>(kspan, lb0, bw, mask, key[r]); break;
+        }
+        if (!one && j0 < s1 && j0 + 3 >= s1) {  // the one lane of the row where a run starts
+          const int32_t c1 = (int32_t)__builtin_amdgcn_readlane((uint32_t)w_c, ri + 1);
 #pragma unroll
           for (int q = 0; q < 4; q++) {
             const int32_t j = j0 + q;
@@ -1969,6 +2000,9 @@ __global__ __launch_bounds__(256) void k_expand(KArgs a) {
         kmax = max(kmax, max(max(key[r][0], key[r][1]), max(key[r][2], key[r][3])));
         continue;
       }
+      const int32_t s0 = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, ri);
+      const uint32_t p0 = __builtin_amdgcn_readlane(W.prm, ri), f0 = __builtin_amdgcn_readlane(W.rle, ri);
+      const uint32_t p1 = __builtin_amdgcn_readlane(W.prm, ri + 1), f1 = __builtin_amdgcn_readlane(W.rle, ri + 1);
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const int32_t j = j0 + q;
@@ -2139,6 +2173,9 @@ struct pq_launch_args {
   const void *tiles;
   int32_t ntiles, ntiles4;  // k_expand jobs; the first ntiles4 are of 4-byte columns
   int32_t ex_lds;
+  void *recs;
+  const int32_t *page_jobs;
+  uint32_t epoch;
 };
 
 static pq::KArgs to_k(const pq_launch_args *p) {
@@ -2164,6 +2201,9 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   k.runs = (uint2 *)p->runs;
   k.tile_info = (int2 *)p->tile_info;
   k.ex_lds = p->ex_lds;
+  k.recs = (pq::ExRec *)p->recs;
+  k.page_jobs = p->page_jobs;
+  k.epoch = p->epoch;
   k.tiles = (const pq::TileJob *)p->tiles;
   return k;
 }
@@ -2190,6 +2230,7 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     }
     if (p->ntiles > p->ntiles4) {
       k.tiles = (const pq::TileJob *)p->tiles + p->ntiles4;
+      k.recs = (pq::ExRec *)p->recs + p->ntiles4;
       k.nlist = p->ntiles - p->ntiles4;
       hipLaunchKernelGGL(pq::k_expand<8>, dim3((k.nlist + 3) / 4), dim3(256), (size_t)4 * p->ex_lds, s, k);
     }
