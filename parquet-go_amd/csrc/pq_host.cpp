@@ -59,6 +59,7 @@ struct pq_launch_args {
   void *recs;
   const int32_t *page_jobs;
   uint32_t epoch;
+  int32_t knob;
 };
 int pq_launch(int which, const pq_launch_args *p, hipStream_t s);
 }
@@ -1530,6 +1531,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.recs = B->d_recs;
   a.page_jobs = B->d_page_jobs;
   a.epoch = ++B->epoch;
+  a.knob = getenv("PQG_KNOB") ? atoi(getenv("PQG_KNOB")) : 0;
   a.tiles = B->d_tiles;
   a.ntiles = (int32_t)B->tiles.size();
   a.ntiles4 = B->ntiles4;

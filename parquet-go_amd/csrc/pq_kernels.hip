@@ -72,6 +72,7 @@ struct KArgs {
   ExRec *recs;            // k_prepare -> k_expand: one record per job (launch order)
   const int32_t *page_jobs;  // per tiled page (PageDesc.job_base): positions of its jobs
   uint32_t epoch;         // this decode's record epoch
+  int32_t knob;           // analysis only (PQG_KNOB): 1 no gathers, 2 no stores, 3 neither
   const TileJob *tiles;   // k_expand: one workgroup per entry
 };
 
@@ -1879,6 +1880,10 @@ __global__ __launch_bounds__(256) void k_expand(KArgs a) {
   const ExRec rc = a.recs[job];  // written by this decode's k_prepare, or stale (epoch)
   const int page = tj.page;
   if (rc.epoch != a.epoch) return;  // the page failed before k_prepare finished it
+  if (a.knob == 5) {  // analysis: record only
+    if (rc.v0 == 0x7fffffff) a.status[0] = 0;
+    return;
+  }
   STAMP(1);
   const int32_t v0 = rc.v0, lim = rc.lim;
   if (v0 >= lim) return;
@@ -1931,6 +1936,10 @@ __global__ __launch_bounds__(256) void k_expand(KArgs a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the staged bytes (LDS-DMA) and the window
   STAMP(3);
+  if (a.knob == 4) {  // analysis: record + window + staging only
+    if (W.start == 0x7fffffe || kspan[lane] == 0x12345u) a.status[0] = 0;
+    return;
+  }
   const int64_t lbase = (int64_t)(A - (uintptr_t)ks) * 8;  // stream bit of kspan bit 0
   const int64_t end_bit = slen * 8;
   const uint32_t mask = bw >= 32 ? 0xffffffffu : ((1u << bw) - 1);
@@ -1959,6 +1968,61 @@ __global__ __launch_bounds__(256) void k_expand(KArgs a) {
     uint32_t key[HR][4];
     bool bad = false;
     uint32_t kmax = 0;  // largest key of the fast rows
+    // scalar plan of the half's rows: the run of the row start (ri), the next
+    // run's start (s1) and the staged-bit constants of both; `fast` rows are
+    // full, bit-packed only and inside the stream
+    int32_t rs1[HR], rc0[HR], rc1[HR];
+    bool all_fast = true;
+#pragma unroll
+    for (int r = 0; r < HR; r++) {
+      const int32_t rl = v0 + (h * HR + r) * EX_ROW;
+      const int32_t rh = min(rl + EX_ROW, lim);
+      const uint64_t m = ballot(W.start <= rl);
+      const int32_t ri = max((int32_t)__popcll(m) - 1, 0);
+      rs1[r] = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, ri + 1);
+      rc0[r] = (int32_t)__builtin_amdgcn_readlane((uint32_t)w_c, ri);
+      rc1[r] = (int32_t)__builtin_amdgcn_readlane((uint32_t)w_c, ri + 1);
+      all_fast &= rl < lim && rh - rl == EX_ROW && ((okm >> ri) & 1) && (rs1[r] >= rh || ((okm >> (ri + 1)) & 1));
+    }
+    if (all_fast) {
+      // straight-line: every row's LDS reads go out together.  The four keys of
+      // a lane are taken from the run of its first key; the one lane per row
+      // where a run starts among them is fixed up below.
+      uint32_t lb0[HR];
+#pragma unroll
+      for (int r = 0; r < HR; r++) {
+        const int32_t j0 = v0 + (h * HR + r) * EX_ROW + 4 * lane;
+        lb0[r] = (uint32_t)(j0 >= rs1[r] ? rc1[r] : rc0[r]) + __umul24((uint32_t)j0, (uint32_t)bw);
+      }
+      switch (cls) {
+        case 0:
+#pragma unroll
+          for (int r = 0; r < HR; r++) row_keys<0>(kspan, lb0[r], bw, mask, key[r]);
+          break;
+        case 1:
+#pragma unroll
+          for (int r = 0; r < HR; r++) row_keys<1>(kspan, lb0[r], bw, mask, key[r]);
+          break;
+        default:
+#pragma unroll
+          for (int r = 0; r < HR; r++) row_keys<2>(kspan, lb0[r], bw, mask, key[r]);
+          break;
+      }
+#pragma unroll
+      for (int r = 0; r < HR; r++) {
+        const int32_t j0 = v0 + (h * HR + r) * EX_ROW + 4 * lane;
+        if (j0 < rs1[r] && j0 + 3 >= rs1[r]) {
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            const int32_t j = j0 + q;
+            const uint32_t lb = (uint32_t)((j >= rs1[r] ? rc1[r] : rc0[r]) + j * bw);
+            const uint32_t *dq = kspan + (lb >> 5);
+            key[r][q] = __builtin_amdgcn_alignbit(dq[1], dq[0], lb & 31) & mask;
+          }
+        }
+        kmax = max(kmax, max(max(key[r][0], key[r][1]), max(key[r][2], key[r][3])));
+      }
+    } else {
 #pragma unroll
     for (int r = 0; r < HR; r++) {
       const int32_t rl = v0 + (h * HR + r) * EX_ROW;
@@ -2021,13 +2085,19 @@ __global__ __launch_bounds__(256) void k_expand(KArgs a) {
         key[r][q] = act ? kv : 0u;
       }
     }
+    }
     if (ballot(bad || kmax >= P.dict_n)) {
       // dictionary index out of range (type_dict.go:51-53); it precedes any later header error
       set_status(a.status, page, ST_VALUES, E_DICT);
       return;
     }
     // gathers (an unaligned dictionary is read as aligned dwords + a funnel shift)
-    if (dsh == 0) {
+    if (a.knob & 1) {
+#pragma unroll
+      for (int r = 0; r < HR; r++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) val[h][r][q] = key[r][q];
+    } else if (dsh == 0) {
 #pragma unroll
       for (int r = 0; r < HR; r++)
 #pragma unroll
@@ -2058,6 +2128,17 @@ __global__ __launch_bounds__(256) void k_expand(KArgs a) {
     }
   }
   STAMP(4);
+  if (a.knob & 2) {  // analysis: keep the values live, store one word
+    uint32_t acc = 0;
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+      for (int r = 0; r < HR; r++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) acc ^= (uint32_t)val[h][r][q];
+    if (acc == 0x12345678u) __builtin_amdgcn_raw_buffer_store_b32(acc, ors, 0, 0, 0);
+    return;
+  }
   // 4. stores: 16 / 32 contiguous bytes per lane per row
   const bool out_al = ((uintptr_t)tj.out & 15) == 0;
 #pragma unroll
@@ -2176,6 +2257,7 @@ struct pq_launch_args {
   void *recs;
   const int32_t *page_jobs;
   uint32_t epoch;
+  int32_t knob;
 };
 
 static pq::KArgs to_k(const pq_launch_args *p) {
@@ -2204,6 +2286,7 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   k.recs = (pq::ExRec *)p->recs;
   k.page_jobs = p->page_jobs;
   k.epoch = p->epoch;
+  k.knob = p->knob;
   k.tiles = (const pq::TileJob *)p->tiles;
   return k;
 }
