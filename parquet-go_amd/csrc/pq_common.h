@@ -74,6 +74,19 @@ struct PageDesc {
 // workgroup takes 4 waves x EX_WAVE_VALUES consecutive values of one page.
 constexpr int RUN_TILE = 512;
 constexpr int EX_WAVE_VALUES = 2048;
+// k_expand_ld: one workgroup per group of consecutive jobs of one column
+// chunk, whose dictionary it holds in LDS (host-built)
+constexpr int LD_WAVES_H = 4;             // waves of a k_expand_mix workgroup
+constexpr int LD_LDS_MAX = 160 * 1024;    // LDS of one CU (gfx950)
+constexpr int LD_MIX_MAX = 32 * 1024;     // k_expand_mix LDS per workgroup with a dictionary (default)
+struct LdsGroup {
+  int32_t job0, njobs;   // jobs [job0, job0 + njobs) of the launch order
+  int32_t dpage;         // the chunk's dictionary page; -1: one job per wave, L1/L2 gathers
+  int32_t dict_bytes;    // LDS bytes reserved for the dictionary (16-byte multiple)
+  int32_t kspan;         // LDS bytes of staged key bytes per wave (1 KiB multiple)
+  int32_t pad[3];
+};
+
 struct TileJob {         // one k_expand workgroup (host-built, XCD-affine order)
   uint8_t *out;          // the page's first output value
   int32_t page;          // PageDesc index

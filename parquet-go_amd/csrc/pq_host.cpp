@@ -60,6 +60,10 @@ struct pq_launch_args {
   const int32_t *page_jobs;
   uint32_t epoch;
   int32_t knob;
+  const void *lgroups;
+  int32_t ldn[6];   // k_expand_ld groups per (width 4, 8) x LDS class, in that order
+  int32_t ldl[6];   // dynamic LDS bytes of each
+  int32_t ld_sel;   // the class pq_launch(9) launches (both widths)
 };
 int pq_launch(int which, const pq_launch_args *p, hipStream_t s);
 }
@@ -538,6 +542,10 @@ struct pqg_batch {
   int64_t page_job_entries = 0;
   uint32_t epoch = 0;
   TileJob *d_tiles = nullptr;
+  int32_t ntiles_g = 0;              // k_expand jobs (the LDS-dictionary groups' jobs follow them)
+  std::vector<LdsGroup> lgroups;     // k_expand_ld groups, 4-byte columns first
+  LdsGroup *d_lgroups = nullptr;
+  int32_t ldn[6] = {}, ldl[6] = {};  // groups and LDS bytes per (width 4, 8) x LDS class
   uint32_t *h_status = nullptr;  // pinned mirror
   std::vector<ColDesc> hcols;
   // timing: a ring of event sets, one per decode, harvested by pqg_batch_kernel_times
@@ -1243,6 +1251,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   // route data pages: flat required fixed-width PLAIN / RLE_DICTIONARY pages
   // take the tiled path (run walk in k_prepare + k_expand), everything else k_decode
   std::vector<std::vector<TileJob>> chunk_tiles;  // tiles grouped by column chunk (one dictionary)
+  std::vector<int32_t> page_need(npages, 0);      // staged key bytes per job of a tiled RLE page
   int32_t last_chunk_key = -1;
   for (int32_t pi : B->data_list) {
     PageDesc &d = B->pages[(size_t)pi];
@@ -1271,7 +1280,8 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
       // denser spots fall back to direct loads
       if (n > 0) {
         const int64_t need = ((int64_t)d.body_len * EX_WAVE_VALUES + n - 1) / n + 96;
-        B->ex_lds = (int32_t)std::max<int64_t>(B->ex_lds, std::min<int64_t>(need, EX_WAVE_VALUES * 4 + 256));
+        page_need[(size_t)pi] = (int32_t)std::min<int64_t>(need, EX_WAVE_VALUES * 4 + 256);
+        B->ex_lds = std::max(B->ex_lds, page_need[(size_t)pi]);
       }
     }
     const int32_t key = d.dict >= 0 ? d.dict : -2 - d.col * 1000003 - d.rg;
@@ -1283,31 +1293,111 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   }
   for (auto &cp : B->cols) B->any_count |= (cp.flags & COL_NEEDS_COUNT) != 0;
   // 4-byte columns' jobs first (k_expand<4>), then 8-byte ones (k_expand<8>).
-  // XCD affinity (speed only, never correctness): workgroups b and b + 8 share an
-  // XCD's L2 under round-robin dispatch, so deal whole chunks (one dictionary
-  // each) to the 8 block residues, balanced by job count, then interleave four
-  // jobs (one workgroup) at a time.
-  auto is4 = [&](const std::vector<TileJob> &ct) {
-    return ct.empty() || B->cols[(size_t)B->pages[(size_t)ct[0].page].col].info.value_width == 4;
-  };
-  auto mid = std::stable_partition(chunk_tiles.begin(), chunk_tiles.end(), is4);
-  auto deal = [&](std::vector<std::vector<TileJob>>::iterator b, std::vector<std::vector<TileJob>>::iterator e) {
-    std::vector<std::vector<TileJob>> x(8);
-    for (auto it = b; it != e; ++it) {
-      size_t best = 0;
-      for (size_t q = 1; q < 8; q++)
-        if (x[q].size() < x[best].size()) best = q;
-      x[best].insert(x[best].end(), it->begin(), it->end());
+  // k_expand_mix blocks (512 threads, eight waves), per value width:
+  //  * LDS groups: chunks whose dictionary fits in LDS beside four waves'
+  //    staged keys (within LD_MIX_MAX) and whose jobs amortise copying it
+  //    (the copy at most a quarter of the output) -> groups of consecutive jobs;
+  //  * global blocks: every other job, one per wave, gathering through L1/L2.
+  //    (Workgroups of four waves: a workgroup holds its slot until its last
+  //    wave ends, and jobs vary in length.)
+  //    XCD affinity (speed only, never correctness): blocks b and b + 8 share
+  //    an XCD's L2 under round-robin dispatch, so whole chunks (one dictionary
+  //    each) are dealt to the 8 block residues, balanced by job count.
+  // Blocks are emitted in rounds of 8 (one per residue), global and LDS rounds
+  // interleaved by job count so that L2-bound gathers and LDS-bound ones share
+  // the machine for the whole launch.
+  B->ex_lds = (B->ex_lds + 1023) & ~1023;  // whole 1 KiB LDS-DMA chunks
+  const bool ld_off = getenv("PQG_NO_LDS_DICT") != nullptr;
+  std::vector<TileJob> slot_tiles, ld_tiles;
+  const int64_t ld_max = getenv("PQG_LD_MAX_KB") ? 1024 * (int64_t)atoi(getenv("PQG_LD_MAX_KB")) : LD_MIX_MAX;
+  for (int ws = 0; ws < 2; ws++) {
+    const int32_t W = ws == 0 ? 4 : 8;
+    struct LdG {
+      const std::vector<TileJob> *ct;
+      int64_t j0, j1;
+      int32_t dict_bytes, kspan;
+    };
+    std::vector<LdG> ldg;
+    std::vector<std::vector<TileJob>> bins(8);
+    for (const auto &ct : chunk_tiles) {
+      if (ct.empty() || B->cols[(size_t)B->pages[(size_t)ct[0].page].col].info.value_width != W) continue;
+      bool ld = false;
+      if (!ld_off && ct[0].dict >= 0) {
+        const int64_t dbytes = ((int64_t)std::max(B->pages[(size_t)ct[0].dict].num_values, 0) * W + 15) & ~15;
+        int32_t ks = 0;
+        for (const TileJob &tj : ct) ks = std::max(ks, page_need[(size_t)tj.page]);
+        ks = (ks + 1023) & ~1023;
+        const int64_t J = (int64_t)ct.size();
+        if (dbytes > 0 && ks > 0 && dbytes + (int64_t)LD_WAVES_H * ks <= ld_max &&
+            dbytes * 4 <= J * EX_WAVE_VALUES * W) {
+          int64_t G = (dbytes * 4 + (int64_t)EX_WAVE_VALUES * W - 1) / ((int64_t)EX_WAVE_VALUES * W);
+          G = std::min<int64_t>(std::max<int64_t>((G + LD_WAVES_H - 1) / LD_WAVES_H * LD_WAVES_H, 2 * LD_WAVES_H), 128);
+          const int64_t ng = (J + G - 1) / G;
+          for (int64_t q = 0; q < ng; q++) ldg.push_back({&ct, q * J / ng, (q + 1) * J / ng, (int32_t)dbytes, ks});
+          ld = true;
+        }
+      }
+      if (!ld) {
+        size_t best = 0;
+        for (size_t q = 1; q < 8; q++)
+          if (bins[q].size() < bins[best].size()) best = q;
+        bins[best].insert(bins[best].end(), ct.begin(), ct.end());
+      }
     }
-    size_t maxlen = 0;
-    for (auto &v : x) maxlen = std::max(maxlen, v.size());
-    for (size_t r = 0; r < maxlen; r += 4)
-      for (size_t q = 0; q < 8; q++)
-        for (size_t k = r; k < r + 4 && k < x[q].size(); k++) B->tiles.push_back(x[q][k]);
-  };
-  deal(chunk_tiles.begin(), mid);
-  B->ntiles4 = (int32_t)B->tiles.size();
-  deal(mid, chunk_tiles.end());
+    size_t maxlen = 0, gjobs = 0, ljobs = 0;
+    for (auto &v : bins) maxlen = std::max(maxlen, v.size()), gjobs += v.size();
+    for (auto &g : ldg) ljobs += (size_t)(g.j1 - g.j0);
+    const size_t ngr = (maxlen + LD_WAVES_H - 1) / LD_WAVES_H, nlr = (ldg.size() + 7) / 8;
+    size_t gr = 0, lr = 0, gdone = 0, ldone = 0;
+    const int32_t nb0 = (int32_t)B->lgroups.size();
+    const TileJob none = {nullptr, -1, -1, 0, 0, 0, 0};
+    while (gr < ngr || lr < nlr) {
+      // the round kind that is behind in its share of the jobs goes next
+      const bool take_g = lr >= nlr || (gr < ngr && (double)gdone * (double)std::max<size_t>(ljobs, 1) <=
+                                                        (double)ldone * (double)std::max<size_t>(gjobs, 1));
+      for (size_t q = 0; q < 8; q++) {
+        // every block owns LD_WAVES_H job slots (wave w: slot 4 b + w), so a
+        // global block's waves load their jobs without waiting for the block's
+        // descriptor; LDS groups keep their jobs past the slots (ld_tiles)
+        LdsGroup g = {};
+        g.job0 = (int32_t)slot_tiles.size();
+        g.dpage = -1;
+        if (take_g) {
+          const size_t k0 = gr * LD_WAVES_H, k1 = std::min(k0 + LD_WAVES_H, bins[q].size());
+          for (size_t k = k0; k < k1; k++) slot_tiles.push_back(bins[q][k]);
+          g.njobs = (int32_t)(k1 > k0 ? k1 - k0 : 0);
+          g.kspan = B->ex_lds;
+          gdone += (size_t)g.njobs;
+          if (g.njobs) B->ldl[ws] = std::max(B->ldl[ws], LD_WAVES_H * B->ex_lds);
+        } else if (lr * 8 + q < ldg.size()) {
+          const LdG &l = ldg[lr * 8 + q];
+          g.job0 = -1 - (int32_t)ld_tiles.size();  // rebased below
+          for (int64_t j = l.j0; j < l.j1; j++) ld_tiles.push_back((*l.ct)[(size_t)j]);
+          g.njobs = (int32_t)(l.j1 - l.j0);
+          g.dpage = (*l.ct)[0].dict;
+          g.dict_bytes = l.dict_bytes;
+          g.kspan = l.kspan;
+          ldone += (size_t)g.njobs;
+          B->ldl[ws] = std::max(B->ldl[ws], l.dict_bytes + LD_WAVES_H * l.kspan);
+        }
+        while (slot_tiles.size() < (size_t)(B->lgroups.size() + 1) * LD_WAVES_H) slot_tiles.push_back(none);
+        B->lgroups.push_back(g);
+      }
+      if (take_g) gr++;
+      else lr++;
+    }
+    B->ldn[ws] = (int32_t)B->lgroups.size() - nb0;
+  }
+  // job indices are relative to the launch's first slot (the 8-byte launch
+  // starts at block ldn[0])
+  for (size_t b = 0; b < B->lgroups.size(); b++) {
+    LdsGroup &g = B->lgroups[b];
+    if (g.job0 < 0) g.job0 = (int32_t)slot_tiles.size() + (-1 - g.job0);
+    if (b >= (size_t)B->ldn[0]) g.job0 -= B->ldn[0] * LD_WAVES_H;
+  }
+  B->tiles = std::move(slot_tiles);
+  B->tiles.insert(B->tiles.end(), ld_tiles.begin(), ld_tiles.end());
+  B->ntiles_g = 0;  // every job runs in k_expand_mix
 
   // device buffers
   int rc = 0;
@@ -1323,10 +1413,12 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   rc |= alloc_dev((void **)&B->d_lists, sizeof(int32_t) * nl);
   rc |= alloc_dev(&B->d_runs, 8 * (size_t)(B->run_entries + 64));
   rc |= alloc_dev(&B->d_tile_info, 8 * (size_t)(B->tile_entries + EX_WAVE_VALUES / RUN_TILE + 1));
-  B->ex_lds = (B->ex_lds + 1023) & ~1023;  // whole 1 KiB LDS-DMA chunks
   rc |= alloc_dev((void **)&B->d_tiles, sizeof(TileJob) * (B->tiles.size() + 1));
   rc |= alloc_dev(&B->d_recs, sizeof(ExRec) * (B->tiles.size() + 1));
   rc |= alloc_dev((void **)&B->d_page_jobs, sizeof(int32_t) * (size_t)(B->page_job_entries + 1));
+  rc |= alloc_dev((void **)&B->d_lgroups, sizeof(LdsGroup) * (B->lgroups.size() + 1));
+  if (!rc && !B->lgroups.empty())
+    hipMemcpy(B->d_lgroups, B->lgroups.data(), sizeof(LdsGroup) * B->lgroups.size(), hipMemcpyHostToDevice);
   if (!rc) {
     // positions of every page's jobs in the launch order; records start stale (epoch 0)
     std::vector<int32_t> pj((size_t)B->page_job_entries + 1, 0);
@@ -1483,6 +1575,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
     HIPCHK(hipMemcpy(B->d_cols, B->hcols.data(), sizeof(ColDesc) * B->cols.size(), hipMemcpyHostToDevice));
   // k_expand jobs: output pointers now that the outputs exist
   for (TileJob &tj : B->tiles) {
+    if (tj.page < 0) continue;  // an unused slot
     const PageDesc &d = B->pages[(size_t)tj.page];
     const ColDesc &c = B->hcols[(size_t)d.col];
     tj.width = c.width;
@@ -1533,8 +1626,13 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.epoch = ++B->epoch;
   a.knob = getenv("PQG_KNOB") ? atoi(getenv("PQG_KNOB")) : 0;
   a.tiles = B->d_tiles;
-  a.ntiles = (int32_t)B->tiles.size();
+  a.ntiles = B->ntiles_g;
   a.ntiles4 = B->ntiles4;
+  a.lgroups = B->d_lgroups;
+  for (int i = 0; i < 6; i++) {
+    a.ldn[i] = B->ldn[i];
+    a.ldl[i] = B->ldl[i];
+  }
   const int32_t ns = (int32_t)B->snappy_list.size(), nd = (int32_t)B->dict_list.size(),
                 ndata = (int32_t)B->data_list.size(), ngen = (int32_t)B->general_list.size();
   int e = 0;
@@ -1566,7 +1664,8 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     a.nlist = ngen;
     e |= pq_launch(3, &a, s);
     a.nlist = (int32_t)B->tiles.size();
-    e |= pq_launch(8, &a, s);  // k_expand
+    a.ld_sel = getenv("PQG_OLD_EXPAND") && getenv("PQG_NO_LDS_DICT") ? 1 : 0;
+    e |= pq_launch(9, &a, s);  // k_expand_mix (tiled pages)
     mark(true);
     a.list = B->d_lists + ns + nd;
     a.nlist = ndata;
@@ -1778,6 +1877,7 @@ void pqg_batch_destroy(pqg_batch *B) {
   hipFree(B->d_tiles);
   hipFree(B->d_recs);
   hipFree(B->d_page_jobs);
+  hipFree(B->d_lgroups);
   if (B->h_status) hipHostFree(B->h_status);
   for (int k = 0; k < pqg_batch::kRing; k++)
     for (int i = 0; i < 8; i++)

@@ -74,6 +74,7 @@ struct KArgs {
   uint32_t epoch;         // this decode's record epoch
   int32_t knob;           // analysis only (PQG_KNOB): 1 no gathers, 2 no stores, 3 neither
   const TileJob *tiles;   // k_expand: one workgroup per entry
+  const LdsGroup *lgroups;  // k_expand_ld: one workgroup per entry
 };
 
 #ifdef PQ_STAMPS
@@ -1868,22 +1869,29 @@ __device__ __forceinline__ void row_keys(const uint32_t *kspan, uint32_t lb0, in
   }
 }
 
-template <int WIDTH>
-__global__ __launch_bounds__(256) void k_expand(KArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t kspan_dyn[];
-  STAMP(0);
-  const int wv = (int)ufirst(threadIdx.x >> 6);
+// A wave-uniform load through the scalar cache (constant address space): for
+// data written by an earlier launch and read-only in this one (job records,
+// tile jobs, groups), so the compiler never falls back to vector loads.
+template <class T>
+__device__ __forceinline__ T sload(const T *p) {
+  static_assert(sizeof(T) % 16 == 0, "whole 16-byte pieces");
+  union {
+    T t;
+    u32x4 v[sizeof(T) / 16];
+  } u;
+  const __attribute__((address_space(4))) u32x4 *q = (const __attribute__((address_space(4))) u32x4 *)p;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 16); i++) u.v[i] = q[i];
+  return u.t;
+}
+
+// One job (EX_WAVE values of one page) by one wave.  kspan: this wave's
+// staging area (ex_lds bytes); sdict: the dictionary resident in LDS, or null.
+template <int WIDTH, bool LD>
+__device__ __forceinline__ void expand_job(const KArgs &a, const TileJob &tj, const ExRec &rc, uint32_t *kspan,
+                                           int ex_lds, const uint32_t *sdict) {
   const int lane = lane_id();
-  const int job = (int)blockIdx.x * 4 + wv;
-  if (job >= a.nlist) return;
-  const TileJob tj = a.tiles[job];
-  const ExRec rc = a.recs[job];  // written by this decode's k_prepare, or stale (epoch)
   const int page = tj.page;
-  if (rc.epoch != a.epoch) return;  // the page failed before k_prepare finished it
-  if (a.knob == 5) {  // analysis: record only
-    if (rc.v0 == 0x7fffffff) a.status[0] = 0;
-    return;
-  }
   STAMP(1);
   const int32_t v0 = rc.v0, lim = rc.lim;
   if (v0 >= lim) return;
@@ -1910,8 +1918,6 @@ __global__ __launch_bounds__(256) void k_expand(KArgs a) {
   const int64_t byte_lo = rc.byte_lo, byte_hi = (int64_t)rc.byte_hi + 16;
   const uintptr_t A = ((uintptr_t)ks + (uintptr_t)byte_lo) & ~(uintptr_t)15;
   const int64_t nb = (int64_t)((uintptr_t)ks + (uintptr_t)byte_hi - A);
-  const int ex_lds = a.ex_lds;
-  uint32_t *kspan = kspan_dyn + wv * (ex_lds / 4);
   const bool staged = nb <= ex_lds;
   if (staged) {
     // LDS-DMA: lane l's 16 bytes of chunk i land at kspan + 1024 i + 16 l.  Bytes
@@ -1960,7 +1966,11 @@ __global__ __launch_bounds__(256) void k_expand(KArgs a) {
       __builtin_amdgcn_make_buffer_rsrc((void *)tj.out, (short)0, (int)((uint32_t)lim * (uint32_t)w), 0x00020000);
   constexpr int HR = EX_ROWS / 2;
   const int32_t end_bit32 = (int32_t)end_bit;
+#ifdef PQ_ONECLS
+  const int cls = 2;
+#else
   const int cls = bw <= 8 ? 0 : bw <= 16 ? 1 : 2;
+#endif
   typedef typename std::conditional<WIDTH == 4, uint32_t, uint64_t>::type VT;
   VT val[2][HR][4];
 #pragma unroll
@@ -2092,7 +2102,15 @@ __global__ __launch_bounds__(256) void k_expand(KArgs a) {
       return;
     }
     // gathers (an unaligned dictionary is read as aligned dwords + a funnel shift)
-    if (a.knob & 1) {
+    if (LD) {  // ds_read: the dictionary is resident in this workgroup's LDS
+#pragma unroll
+      for (int r = 0; r < HR; r++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          if (WIDTH == 4) val[h][r][q] = sdict[key[r][q]];
+          else val[h][r][q] = ((const uint64_t *)sdict)[key[r][q]];
+        }
+    } else if (a.knob & 1) {
 #pragma unroll
       for (int r = 0; r < HR; r++)
 #pragma unroll
@@ -2174,6 +2192,86 @@ __global__ __launch_bounds__(256) void k_expand(KArgs a) {
       }
     }
   STAMP(5);
+}
+
+template <int WIDTH>
+__global__ __launch_bounds__(256) void k_expand(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t kspan_dyn[];
+  STAMP(0);
+  const int wv = (int)ufirst(threadIdx.x >> 6);
+  const int job = (int)blockIdx.x * 4 + wv;
+  if (job >= a.nlist) return;
+  const TileJob tj = sload(a.tiles + job);
+  const ExRec rc = sload(a.recs + job);  // written by this decode's k_prepare, or stale (epoch)
+  if (rc.epoch != a.epoch) return;  // the page failed before k_prepare finished it
+  if (a.knob == 5) {  // analysis: record only
+    if (rc.v0 == 0x7fffffff) a.status[0] = 0;
+    return;
+  }
+  expand_job<WIDTH, false>(a, tj, rc, kspan_dyn + wv * (a.ex_lds / 4), a.ex_lds, nullptr);
+}
+
+
+// ===========================================================================
+// K5m: k_expand_mix — the tiled decode in 256-thread workgroups, one per
+// LdsGroup (host-built, see the planner in pq_host.cpp):
+//  * dpage >= 0: consecutive jobs of one column chunk whose dictionary fits in
+//    LDS.  The dictionary is copied into LDS once (aligned dwords; an
+//    unaligned page is funnel-shifted), then the four waves take the jobs in
+//    turn and gather with ds_read instead of L1/L2 requests, which bound the
+//    random gathers of dictionaries past the L1 (tools/gather_bench.hip);
+//  * dpage < 0: one job per wave, gathers through L1/L2 (dictionaries too
+//    large for LDS, PLAIN pages).
+// Both kinds share one launch, so L2-bound and LDS-bound blocks overlap.
+// ===========================================================================
+constexpr int LD_WAVES = LD_WAVES_H;
+
+// the two block kinds as separate (non-inlined) functions: each keeps the
+// register allocation and schedule it gets on its own
+template <int WIDTH>
+__device__ __forceinline__ void mix_global(const KArgs &a, const LdsGroup &g, uint32_t *lds_dyn) {
+  const int wv = (int)ufirst(threadIdx.x >> 6);
+  const int j = (int)blockIdx.x * LD_WAVES + wv;
+  const TileJob tj = sload(a.tiles + j);
+  const ExRec rc = sload(a.recs + j);
+  if (rc.epoch != a.epoch) return;  // an unused slot, or the page failed before k_prepare finished it
+  expand_job<WIDTH, false>(a, tj, rc, lds_dyn + wv * (g.kspan / 4), g.kspan, nullptr);
+}
+
+template <int WIDTH>
+__device__ __forceinline__ void mix_lds(const KArgs &a, const LdsGroup &g, uint32_t *lds_dyn) {
+  const int wv = (int)ufirst(threadIdx.x >> 6);
+  if (page_status(a.status, g.dpage) != STATUS_OK) return;  // no record of the chunk was written
+  const PageDesc dp = a.pages[g.dpage];
+  const uint8_t *dict = body_ptr(a, dp, g.dpage);
+  const uint32_t nbytes = min((uint32_t)max(dp.num_values, 0) * (uint32_t)WIDTH, (uint32_t)g.dict_bytes);
+  const uint32_t dsh = (uint32_t)((uintptr_t)dict & 3);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)((uintptr_t)dict & ~(uintptr_t)3), (short)0, (int)(nbytes + dsh), 0x00020000);
+  const uint32_t n16 = (nbytes + 15) / 16;
+  for (uint32_t i = threadIdx.x; i < n16; i += LD_WAVES * 64) {
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * i, 0, 0);
+    const uint32_t y = dsh ? __builtin_amdgcn_raw_buffer_load_b32(rs, 16 * i + 16, 0, 0) : 0u;
+    *(u32x4 *)(lds_dyn + 4 * i) =
+        u32x4{__builtin_amdgcn_alignbyte(x.y, x.x, dsh), __builtin_amdgcn_alignbyte(x.z, x.y, dsh),
+              __builtin_amdgcn_alignbyte(x.w, x.z, dsh), __builtin_amdgcn_alignbyte(y, x.w, dsh)};
+  }
+  __syncthreads();
+  uint32_t *kspan = lds_dyn + g.dict_bytes / 4 + wv * (g.kspan / 4);
+  for (int j = g.job0 + wv; j < g.job0 + g.njobs; j += LD_WAVES) {
+    const TileJob tj = sload(a.tiles + j);
+    const ExRec rc = sload(a.recs + j);
+    if (rc.epoch != a.epoch) continue;  // the page failed before k_prepare finished it
+    expand_job<WIDTH, true>(a, tj, rc, kspan, g.kspan, lds_dyn);
+  }
+}
+
+template <int WIDTH>
+__global__ __launch_bounds__(LD_WAVES_H * 64) void k_expand_mix(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
+  const LdsGroup g = sload(a.lgroups + blockIdx.x);
+  if (g.dpage < 0) mix_global<WIDTH>(a, g, lds_dyn);
+  else mix_lds<WIDTH>(a, g, lds_dyn);
 }
 
 // level-error precedence pass: for pages that failed in k_decode at the
@@ -2258,6 +2356,10 @@ struct pq_launch_args {
   const int32_t *page_jobs;
   uint32_t epoch;
   int32_t knob;
+  const void *lgroups;
+  int32_t ldn[6];   // k_expand_mix blocks of 4-byte, 8-byte columns ([0], [1])
+  int32_t ldl[6];   // their dynamic LDS bytes
+  int32_t ld_sel;
 };
 
 static pq::KArgs to_k(const pq_launch_args *p) {
@@ -2288,6 +2390,7 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   k.epoch = p->epoch;
   k.knob = p->knob;
   k.tiles = (const pq::TileJob *)p->tiles;
+  k.lgroups = (const pq::LdsGroup *)p->lgroups;
   return k;
 }
 
@@ -2316,6 +2419,32 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
       k.recs = (pq::ExRec *)p->recs + p->ntiles4;
       k.nlist = p->ntiles - p->ntiles4;
       hipLaunchKernelGGL(pq::k_expand<8>, dim3((k.nlist + 3) / 4), dim3(256), (size_t)4 * p->ex_lds, s, k);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : 17;
+  }
+  if (which == 9) {  // k_expand_mix: one 512-thread workgroup per LdsGroup (absolute job indices)
+    static bool attr = false;
+    if (!attr) {
+      hipFuncSetAttribute((const void *)pq::k_expand_mix<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      hipFuncSetAttribute((const void *)pq::k_expand_mix<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+    const dim3 blk(pq::LD_WAVES_H * 64);
+    if (p->ld_sel == 1) {  // analysis (PQG_OLD_EXPAND, no LDS groups): the one-job-per-wave kernel on the same slots
+      k.nlist = p->ldn[0] * pq::LD_WAVES_H;
+      if (p->ldn[0] > 0) hipLaunchKernelGGL(pq::k_expand<4>, dim3(p->ldn[0]), blk, (size_t)p->ldl[0], s, k);
+      k.tiles = (const pq::TileJob *)p->tiles + (size_t)p->ldn[0] * pq::LD_WAVES_H;
+      k.recs = (pq::ExRec *)p->recs + (size_t)p->ldn[0] * pq::LD_WAVES_H;
+      k.nlist = p->ldn[1] * pq::LD_WAVES_H;
+      if (p->ldn[1] > 0) hipLaunchKernelGGL(pq::k_expand<8>, dim3(p->ldn[1]), blk, (size_t)p->ldl[1], s, k);
+      return hipGetLastError() == hipSuccess ? 0 : 17;
+    }
+    if (p->ldn[0] > 0) hipLaunchKernelGGL(pq::k_expand_mix<4>, dim3(p->ldn[0]), blk, (size_t)p->ldl[0], s, k);
+    if (p->ldn[1] > 0) {
+      k.lgroups = (const pq::LdsGroup *)p->lgroups + p->ldn[0];
+      k.tiles = (const pq::TileJob *)p->tiles + (size_t)p->ldn[0] * pq::LD_WAVES_H;  // slots and job indices
+      k.recs = (pq::ExRec *)p->recs + (size_t)p->ldn[0] * pq::LD_WAVES_H;           // are launch-relative
+      hipLaunchKernelGGL(pq::k_expand_mix<8>, dim3(p->ldn[1]), blk, (size_t)p->ldl[1], s, k);
     }
     return hipGetLastError() == hipSuccess ? 0 : 17;
   }

@@ -1,0 +1,8 @@
+#!/bin/bash
+# GPU tests, then the C2 bench under planner variants (k_expand_mix)
+TAG=${1:-mx}
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1 || exit 1
+for v in "" "PQG_NO_LDS_DICT=1" "PQG_LD_MAX_KB=26" "PQG_LD_MAX_KB=40" "PQG_LD_MAX_KB=53"; do
+  n=$(echo "x$v" | tr -c 'a-zA-Z0-9\n' '_')
+  env $v timeout -k 10 120 python -u bench.py --steps 10 --warmup 2 --no-cpu --no-pmc > gpurun_out/${TAG}_bench$n.json 2>&1 || exit 1
+done

@@ -1,0 +1,6 @@
+#!/bin/bash
+TAG=${1:-mx}
+for v in "PQG_NO_LDS_DICT=1" "PQG_NO_LDS_DICT=1 PQG_OLD_EXPAND=1" "PQG_LD_MAX_KB=32"; do
+  n=$(echo "x$v" | tr -c 'a-zA-Z0-9\n' '_')
+  env $v timeout -k 10 120 python -u bench.py --steps 10 --warmup 2 --no-cpu --no-pmc > gpurun_out/${TAG}_bench$n.json 2>&1 || exit 1
+done
