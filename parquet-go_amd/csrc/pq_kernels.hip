@@ -992,7 +992,7 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
 // ===========================================================================
 // K3: data page prepare
 // ===========================================================================
-__global__ __launch_bounds__(256) void k_prepare(KArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_prepare(KArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t wl_bytes[4][1024];  // run walk: window bytes
   __shared__ __attribute__((aligned(16))) uint16_t wl_nx[4][1024];    // run walk: chain table
   const int wv = (int)ufirst(threadIdx.x >> 6);
