@@ -221,3 +221,78 @@ def test_generated_lists():
     t = pa.table({"l": pa.array(lists, pa.list_(pa.int32())), "ls": pa.array(strs, pa.list_(pa.string()))})
     check_file(_pq_bytes(t, compression="snappy", row_group_size=25000), "lists v1")
     check_file(_pq_bytes(t, compression="snappy", row_group_size=25000, data_page_version="2.0"), "lists v2")
+
+
+def _req_table(cols):
+    pa = pytest.importorskip("pyarrow")
+    return pa.table({k: pa.array(v) for k, v in cols.items()},
+                    schema=pa.schema([pa.field(k, pa.array(v).type, nullable=False) for k, v in cols.items()]))
+
+
+@pytest.mark.parametrize("bw", [1, 4, 12, 15])
+def test_tiled_int64_dictionary(bw):
+    """k_expand_mix<8>: required INT64 dictionary columns (LDS groups for the
+    small dictionaries, L1/L2 blocks for the large), beside an INT32 one."""
+    rng = np.random.default_rng(100 + bw)
+    K = 1 << bw
+    rows = max(2 * K, 60000)
+    d64 = rng.permutation(K).astype(np.int64) * 0x12345679 - (1 << 40)
+    d32 = rng.permutation(K).astype(np.int32) - 3
+    t = _req_table({"a": d64[rng.integers(0, K, rows)], "b": d32[rng.integers(0, K, rows)]})
+    check_file(_pq_bytes(t, compression="snappy", dictionary_pagesize_limit=1 << 30, row_group_size=1 << 16),
+               "int64 dict bw%d" % bw)
+
+
+def test_tiled_dictionary_fallback_to_plain():
+    """A chunk whose dictionary overflows mid-way: RLE_DICTIONARY pages, then
+    PLAIN pages with the same dictionary page in the chunk (LDS groups run both)."""
+    rng = np.random.default_rng(21)
+    rows = 400000
+    t = _req_table({"v": rng.integers(-(1 << 31), 1 << 31, rows, dtype=np.int64).astype(np.int32),
+                    "w": rng.integers(0, 1 << 40, rows, dtype=np.int64)})
+    check_file(_pq_bytes(t, compression="snappy", dictionary_pagesize_limit=64 << 10, row_group_size=1 << 18),
+               "dict fallback")
+
+
+def test_tiled_rle_heavy_keys():
+    """Bit width 1 and 2 key streams that alternate RLE and short bit-packed
+    runs (the run walk's chain mode; k_expand's general rows)."""
+    rng = np.random.default_rng(22)
+    rows = 300000
+    runs = np.repeat(rng.integers(0, 2, rows // 4), rng.integers(1, 12, rows // 4))[:rows]
+    runs4 = np.repeat(rng.integers(0, 4, rows // 3), rng.integers(1, 20, rows // 3))[:rows]
+    t = _req_table({"a": (runs * 7 - 1).astype(np.int32), "b": (runs4 * 11 + 5).astype(np.int32),
+                    "c": (runs4 * 3).astype(np.int64)})
+    check_file(_pq_bytes(t, compression="snappy", row_group_size=100000), "rle heavy")
+
+
+def test_tiled_corrupted_key_streams_match_oracle():
+    """Seeded corruption of uncompressed dictionary data pages (bytes after the
+    page headers): whatever the oracle reports — a clean decode, an index out
+    of range (type_dict.go:51-53) or a run-header error — the GPU reports the
+    same, or decodes the same bytes."""
+    pq = pytest.importorskip("pyarrow.parquet")
+    rng = np.random.default_rng(23)
+    K = 5  # bit width 3: keys 5..7 are out of range
+    rows = 40000
+    d = np.array([11, -4, 90, 7, 123456], np.int32)
+    t = _req_table({"v": d[rng.integers(0, K, rows)]})
+    base = _pq_bytes(t, compression="none", row_group_size=rows, data_page_size=8 << 10)
+    md = pq.ParquetFile(io.BytesIO(base)).metadata
+    cc = md.row_group(0).column(0)
+    start = cc.dictionary_page_offset if cc.has_dictionary_page else cc.data_page_offset
+    lo, hi = cc.data_page_offset, start + cc.total_compressed_size  # the data pages
+    outcomes = set()
+    for trial in range(24):
+        data = bytearray(base)
+        for _ in range(int(rng.integers(1, 4))):
+            p = int(rng.integers(lo + 32, hi))
+            data[p] ^= int(rng.integers(1, 256))
+        check_file(bytes(data), "corrupt %d" % trial)
+        o = oracle.File(bytes(data))
+        try:
+            o.decode(0)
+            outcomes.add(0)
+        except oracle.OracleError as e:
+            outcomes.add(e.code)
+    assert len(outcomes) >= 2, outcomes  # the corruptions reach more than one outcome
