@@ -66,7 +66,7 @@ struct PageDesc {
   int32_t run_cap;       // run-table entries reserved for the page (runs + sentinel)
   int32_t tile_base;     // tiled page: first entry of its tile -> first-run index table
   int32_t job_base;      // tiled page: first entry of its job -> position table (page_jobs)
-  int32_t pad1;
+  int32_t alias_any;     // dictionary page: k_snappy may alias it at any alignment (LDS-group chunks)
 };
 
 // Tiled flat decode (k_prepare's run walk + k_expand).  The run walk records,

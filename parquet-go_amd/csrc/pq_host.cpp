@@ -51,6 +51,8 @@ struct pq_launch_args {
   uint64_t *dbg;
   uint64_t *dbg2;
   int32_t npages_dbg;
+  uint32_t *copy_cnt;
+  int32_t *copy_idx;
   void *runs;
   void *tile_info;
   const void *tiles;
@@ -531,6 +533,8 @@ struct pqg_batch {
   uint32_t *d_njobs = nullptr;   // per Snappy page: jobs written
   int32_t *d_job_base = nullptr, *d_job_owner = nullptr;
   uint32_t max_jobs = 0;
+  uint32_t *d_copy_cnt = nullptr;  // deferred literals registered per decode (two, by epoch parity)
+  int32_t *d_copy_idx = nullptr;   // their job slots, compact
   uint64_t *d_dbg = nullptr;     // diagnostic stamps (PQ_STAMPS builds only)
   uint64_t *d_dbg2 = nullptr;
   void *d_runs = nullptr;        // run tables (k_prepare's run walk -> k_expand)
@@ -1335,6 +1339,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
           const int64_t ng = (J + G - 1) / G;
           for (int64_t q = 0; q < ng; q++) ldg.push_back({&ct, q * J / ng, (q + 1) * J / ng, (int32_t)dbytes, ks});
           ld = true;
+          B->pages[(size_t)ct[0].dict].alias_any = 1;  // copied into LDS with a funnel shift anyway
         }
       }
       if (!ld) {
@@ -1442,7 +1447,10 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   rc |= alloc_dev((void **)&B->d_njobs, 4 * (B->snappy_list.size() + 1));
   rc |= alloc_dev((void **)&B->d_job_base, 4 * job_base.size());
   rc |= alloc_dev((void **)&B->d_job_owner, 4 * (job_owner.size() + 1));
+  rc |= alloc_dev((void **)&B->d_copy_cnt, 16);
+  rc |= alloc_dev((void **)&B->d_copy_idx, 4 * (job_owner.size() + 1));
   if (!rc) {
+    hipMemset(B->d_copy_cnt, 0, 16);
     hipMemcpy(B->d_job_base, job_base.data(), 4 * job_base.size(), hipMemcpyHostToDevice);
     if (!job_owner.empty()) hipMemcpy(B->d_job_owner, job_owner.data(), 4 * job_owner.size(), hipMemcpyHostToDevice);
   }
@@ -1615,6 +1623,8 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.max_jobs = B->max_jobs;
   a.job_base = B->d_job_base;
   a.job_owner = B->d_job_owner;
+  a.copy_cnt = B->d_copy_cnt;
+  a.copy_idx = B->d_copy_idx;
   a.dbg = B->d_dbg;
   a.dbg2 = B->d_dbg2;
   a.npages_dbg = (int32_t)B->pages.size() + 1;
@@ -1870,6 +1880,8 @@ void pqg_batch_destroy(pqg_batch *B) {
   hipFree(B->d_njobs);
   hipFree(B->d_job_base);
   hipFree(B->d_job_owner);
+  hipFree(B->d_copy_cnt);
+  hipFree(B->d_copy_idx);
   hipFree(B->d_dbg);
   hipFree(B->d_dbg2);
   hipFree(B->d_runs);
@@ -1909,6 +1921,11 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
   rc |= alloc_dev((void **)&d_njobs, 16);
   rc |= alloc_dev((void **)&d_jb, 16);
   rc |= alloc_dev((void **)&d_jo, 4 * (size_t)(max_jobs + 1));
+  uint32_t *d_cc = nullptr;
+  int32_t *d_ci = nullptr;
+  rc |= alloc_dev((void **)&d_cc, 16);
+  rc |= alloc_dev((void **)&d_ci, 4 * (size_t)(max_jobs + 1));
+  if (!rc) hipMemset(d_cc, 0, 16);
   if (!rc) {
     int32_t zero4[4] = {0, 0, 0, 0};
     hipMemcpy(d_jb, zero4, 16, hipMemcpyHostToDevice);
@@ -1941,6 +1958,8 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
     a.max_jobs = max_jobs;
     a.job_base = d_jb;
     a.job_owner = d_jo;
+    a.copy_cnt = d_cc;
+    a.copy_idx = d_ci;
     a.dbg = nullptr;
     PageInfo *d_info = nullptr;
     rc |= alloc_dev((void **)&d_info, sizeof(PageInfo));
@@ -1965,6 +1984,8 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
   hipFree(d_list);
   hipFree(d_jobs);
   hipFree(d_njobs);
+  hipFree(d_cc);
+  hipFree(d_ci);
   hipFree(d_jb);
   hipFree(d_jo);
   if (rc) {

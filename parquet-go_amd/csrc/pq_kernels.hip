@@ -73,6 +73,8 @@ struct KArgs {
   const int32_t *page_jobs;  // per tiled page (PageDesc.job_base): positions of its jobs
   uint32_t epoch;         // this decode's record epoch
   int32_t knob;           // analysis only (PQG_KNOB): 1 no gathers, 2 no stores, 3 neither
+  uint32_t *copy_cnt;     // deferred literals registered this decode: [epoch & 1] (the other is reset)
+  int32_t *copy_idx;      // their job slots, compact (k_snappy -> k_copy)
   const TileJob *tiles;   // k_expand: one workgroup per entry
   const LdsGroup *lgroups;  // k_expand_ld: one workgroup per entry
 };
@@ -241,6 +243,7 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
   const int lane = lane_id();
   const int wv = (int)ufirst(threadIdx.x >> 6);  // wave-uniform (keeps per-wave state in SGPRs)
   const int gi = blockIdx.x * SNAPPY_WAVES + wv;
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.copy_cnt[(a.epoch + 1) & 1] = 0;  // the next decode's list
   if (gi >= a.nlist) return;
   const int page = ufirst(a.list[gi]);
   const PageDesc d = a.pages[page];
@@ -285,7 +288,8 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
   const int64_t dl = (int64_t)dlen;
   // a block that is exactly one literal is its own content: leave it in place
   if (write && lane == 0) a.info[page].alias1 = 0;
-  // (a dictionary only when 8-byte aligned: k_expand gathers aligned entries)
+  // (a dictionary page only when 8-byte aligned — L1/L2 gathers read aligned
+  // entries — unless its chunk copies it into LDS, which funnel-shifts)
   if (write && dl > 0 && s < slen) {
     uint32_t tag = W.byte_at(src + s);
     if ((tag & 3) == 0) {
@@ -302,7 +306,7 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
         }
       }
       if (ok && (int64_t)x + 1 == dl && s + hs + dl == slen &&
-          (d.kind != PAGE_DICT || ((d.src + lsize + s + hs) & 7) == 0)) {
+          (d.kind != PAGE_DICT || d.alias_any || ((d.src + lsize + s + hs) & 7) == 0)) {
         if (lane == 0) a.info[page].alias1 = 1 + (int64_t)(d.src + lsize + s + hs);
         return;
       }
@@ -475,6 +479,12 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
   if (err == E_OK && dpos != dl) err = E_SNAPPY;
   if (err == E_OK && !write) err = E_SIZE;  // compress.go:117-119
   if (a.max_jobs > 0 && lane == 0) a.njobs[gi] = err ? 0u : (uint32_t)ndefer;
+  if (!err && ndefer > 0) {  // register the page's deferred literals in the compact list
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&a.copy_cnt[a.epoch & 1], (uint32_t)ndefer);
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (lane < ndefer) a.copy_idx[base + lane] = a.job_base[gi] + lane;
+  }
   if (err) set_status(a.status, page, ST_DECOMPRESS, err);
 }
 
@@ -489,12 +499,10 @@ constexpr int COPY_ITEMS = 4;     // work items per job slot and pass (64 KiB: a
 // a job longer than COPY_ITEMS chunks is covered in passes.  Every load of a
 // chunk is issued before its stores.
 __global__ __launch_bounds__(256) void k_copy(KArgs a) {
-  const uint32_t items = a.max_jobs * COPY_ITEMS;
+  const uint32_t items = a.copy_cnt[a.epoch & 1] * COPY_ITEMS;  // registered by k_snappy
   for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
-    const uint32_t j = it / COPY_ITEMS, c = it % COPY_ITEMS;
-    const int32_t q = a.job_owner[j];
-    if ((uint32_t)(j - a.job_base[q]) >= a.njobs[q]) continue;
-    const CopyJob job = a.jobs[j];
+    const uint32_t c = it % COPY_ITEMS;
+    const CopyJob job = a.jobs[a.copy_idx[it / COPY_ITEMS]];
     const int t = threadIdx.x;
     const uintptr_t d0 = (uintptr_t)job.dst, d1 = d0 + (uintptr_t)job.len;
     const uintptr_t A = d0 & ~(uintptr_t)15;
@@ -2247,7 +2255,7 @@ __device__ __forceinline__ void mix_lds(const KArgs &a, const LdsGroup &g, uint3
   const uint32_t nbytes = min((uint32_t)max(dp.num_values, 0) * (uint32_t)WIDTH, (uint32_t)g.dict_bytes);
   const uint32_t dsh = (uint32_t)((uintptr_t)dict & 3);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      (void *)((uintptr_t)dict & ~(uintptr_t)3), (short)0, (int)(nbytes + dsh), 0x00020000);
+      (void *)((uintptr_t)dict & ~(uintptr_t)3), (short)0, (int)((nbytes + dsh + 3) & ~3u), 0x00020000);
   const uint32_t n16 = (nbytes + 15) / 16;
   for (uint32_t i = threadIdx.x; i < n16; i += LD_WAVES * 64) {
     const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * i, 0, 0);
@@ -2347,6 +2355,8 @@ struct pq_launch_args {
   uint64_t *dbg;
   uint64_t *dbg2;
   int32_t npages_dbg;
+  uint32_t *copy_cnt;
+  int32_t *copy_idx;
   void *runs;
   void *tile_info;
   const void *tiles;
@@ -2379,6 +2389,8 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   k.max_jobs = p->max_jobs;
   k.job_base = p->job_base;
   k.job_owner = p->job_owner;
+  k.copy_cnt = p->copy_cnt;
+  k.copy_idx = p->copy_idx;
   k.dbg = p->dbg;
   k.dbg2 = p->dbg2;
   k.dbg3 = p->dbg2 ? p->dbg2 + 8 * (size_t)p->npages_dbg : nullptr;
