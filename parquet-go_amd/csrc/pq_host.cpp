@@ -1178,7 +1178,14 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
     B->status0.push_back(st);
     if (d.kind == PAGE_DICT) {
       dict_idx = my_index;
-      B->dict_list.push_back(my_index);
+      if (L.physical_type == T_BYTE_ARRAY) {
+        B->dict_list.push_back(my_index);  // k_dict_prepare: the length-prefix walk
+      } else if ((int64_t)std::max(d.num_values, 0) * L.value_width > (int64_t)d.body_len &&
+                 B->status0.back() == STATUS_OK) {
+        // fixed width: the only check is the size (page_dict.go:54-61 reading
+        // num_values values), known here from the header
+        B->status0.back() = make_status(ST_DICT_VALUES, (uint32_t)PQG_ERR_EOF);
+      }
     } else {
       B->data_list.push_back(my_index);
       level_base += d.num_values;
