@@ -886,7 +886,8 @@ static int value_width(const pqref_leaf *L) {
     case PQR_INT64: case PQR_DOUBLE: return 8;
     case PQR_INT96: return 12;
     case PQR_FLBA: return L->type_length;
-    default: return 0; /* BYTE_ARRAY: variable, BOOLEAN: unsupported */
+    case PQR_BOOLEAN: return 1; /* one byte (0 / 1) per value */
+    default: return 0; /* BYTE_ARRAY: variable */
   }
 }
 
@@ -1108,8 +1109,8 @@ static int supported_value_encoding(const pqref_leaf *L, int enc, int has_dict) 
     case PQR_INT32:
     case PQR_INT64:
       return enc == ENC_PLAIN || enc == ENC_RLE_DICT || enc == ENC_DELTA_BP ? 0 : PQR_ERR_ENCODING;
-    case PQR_BOOLEAN:
-      return enc == ENC_PLAIN || enc == ENC_RLE || enc == ENC_RLE_DICT ? PQR_ERR_UNSUPPORTED : PQR_ERR_ENCODING;
+    case PQR_BOOLEAN: /* getBooleanValuesDecoder chunk_reader.go:58-69; dictionaries of booleans are not built */
+      return enc == ENC_PLAIN || enc == ENC_RLE ? 0 : enc == ENC_RLE_DICT ? PQR_ERR_UNSUPPORTED : PQR_ERR_ENCODING;
   }
   return PQR_ERR_ENCODING;
 }
@@ -1135,6 +1136,17 @@ static int values_init(page_reader *p, const pqref_leaf *L) {
     return 0;
   }
   if (enc == ENC_DELTA_BP) return delta_init(p, L->physical_type == PQR_INT32);
+  if (enc == ENC_RLE && L->physical_type == PQR_BOOLEAN) {
+    /* booleanRLEDecoder.init type_boolean.go:101-104: hybridDecoder(1).initSize
+       (hybrid_decoder.go:57-67): u32 LE size, then a LimitReader over the rest */
+    uint8_t lb[4];
+    if (rd_full(&p->vr, lb, 4)) return PQR_ERR_EOF;
+    size_t sz = le32(lb);
+    size_t take = p->vr.n - p->vr.pos < sz ? p->vr.n - p->vr.pos : sz;
+    hy_new(&p->keys, 1);
+    hy_init(&p->keys, p->vr.p + p->vr.pos, take);
+    return 0;
+  }
   return 0; /* PLAIN decoders just keep the reader */
 }
 
@@ -1178,6 +1190,29 @@ static int values_decode(page_reader *p, const pqref_leaf *L, const dictionary *
         bb_put(&dp->vals, &v32, 4);
       } else {
         bb_put(&dp->vals, &v, 8);
+      }
+    }
+    return 0;
+  }
+  if (L->physical_type == PQR_BOOLEAN) {
+    if (enc == ENC_RLE) { /* booleanRLEDecoder.decodeValues type_boolean.go:106-117 */
+      for (int64_t i = 0; i < count; i++) {
+        int32_t b;
+        int e = hy_next(&p->keys, &b);
+        if (e) return e;
+        uint8_t v = b == 1;
+        bb_put(&dp->vals, &v, 1);
+      }
+      return 0;
+    }
+    /* booleanPlainDecoder.decodeValues type_boolean.go:43-68: one byte per 8
+       values, LSB first (unpack8int32_1), read only while values remain */
+    for (int64_t i = 0; i < count; i += 8) {
+      uint8_t byte;
+      if (rd_full(&p->vr, &byte, 1)) return PQR_ERR_EOF;
+      for (int j = 0; j < 8 && i + j < count; j++) {
+        uint8_t v = (byte >> j) & 1;
+        bb_put(&dp->vals, &v, 1);
       }
     }
     return 0;
@@ -1248,7 +1283,7 @@ static int read_dict_page(const pqref_file *f, const pqref_leaf *L, const page_h
     dict->str_bytes = bytes.p;
   } else {
     int w = value_width(L);
-    if (w <= 0) e = PQR_ERR_UNSUPPORTED;
+    if (w <= 0 || L->physical_type == PQR_BOOLEAN) e = PQR_ERR_UNSUPPORTED; /* boolean dictionaries: not built */
     else if ((size_t)n * (size_t)w > blen) e = PQR_ERR_EOF;
     else {
       dict->fixed = (uint8_t *)malloc((size_t)n * (size_t)w + 1);
@@ -1395,10 +1430,6 @@ int pqref_decode(const pqref_file *f, int leaf, int rg0, int rg1, pqref_result *
   const pqref_leaf *L = &f->leaves[leaf];
   int w = value_width(L);
   int is_ba = L->physical_type == PQR_BYTE_ARRAY;
-  if (L->physical_type == PQR_BOOLEAN) {
-    set_err(R, PQR_ERR_UNSUPPORTED, rg0, -1, "BOOLEAN columns are outside the oracle scope");
-    return R->status;
-  }
   R->counts[PQR_CNT_VALUE_WIDTH] = is_ba ? 0 : w;
 
   /* gather dense per-page results for all row groups */

@@ -395,6 +395,7 @@ int value_width(int ptype, int type_length) {
     case T_INT64: case T_DOUBLE: return 8;
     case T_INT96: return 12;
     case T_FLBA: return type_length;
+    case T_BOOLEAN: return 1;  // one byte (0 / 1) per value
     default: return 0;
   }
 }
@@ -969,8 +970,8 @@ static int supported_encoding(int ptype, int enc) {
       return enc == ENC_PLAIN || enc == ENC_RLE_DICT ? 0 : PQG_ERR_ENCODING;
     case T_INT32: case T_INT64:
       return enc == ENC_PLAIN || enc == ENC_RLE_DICT || enc == ENC_DELTA_BP ? 0 : PQG_ERR_ENCODING;
-    case T_BOOLEAN:
-      return enc == ENC_PLAIN || enc == ENC_RLE || enc == ENC_RLE_DICT ? PQG_ERR_UNSUPPORTED : PQG_ERR_ENCODING;
+    case T_BOOLEAN:  // getBooleanValuesDecoder chunk_reader.go:58-69 (boolean dictionaries are not built)
+      return enc == ENC_PLAIN || enc == ENC_RLE ? 0 : enc == ENC_RLE_DICT ? PQG_ERR_UNSUPPORTED : PQG_ERR_ENCODING;
   }
   return PQG_ERR_ENCODING;
 }
@@ -1097,7 +1098,6 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
       d.num_values = h.dict_num_values;
       if (!h.has_dict || h.dict_num_values < 0) fail(ST_HEADER, PQG_ERR_PAGE);
       if (L.physical_type == T_FLBA && L.type_length <= 0) fail(ST_HEADER, PQG_ERR_SCHEMA);
-      if (L.physical_type == T_BOOLEAN) fail(ST_HEADER, PQG_ERR_UNSUPPORTED);
       if (h.dict_encoding != ENC_PLAIN && h.dict_encoding != ENC_PLAIN_DICT) fail(ST_V2_ENC, PQG_ERR_ENCODING);
       comp = h.compressed;
       body = h.uncompressed;
@@ -1180,6 +1180,8 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
       dict_idx = my_index;
       if (L.physical_type == T_BYTE_ARRAY) {
         B->dict_list.push_back(my_index);  // k_dict_prepare: the length-prefix walk
+      } else if (L.physical_type == T_BOOLEAN) {
+        if (B->status0.back() == STATUS_OK) B->status0.back() = make_status(ST_DICT_VALUES, (uint32_t)PQG_ERR_UNSUPPORTED);
       } else if ((int64_t)std::max(d.num_values, 0) * L.value_width > (int64_t)d.body_len &&
                  B->status0.back() == STATUS_OK) {
         // fixed width: the only check is the size (page_dict.go:54-61 reading

@@ -1040,6 +1040,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
       set_status(a.status, page, ST_VAL_INIT, e);
       return;
     }
+  } else if (d.enc == ENC_RLE && c.ptype == T_BOOLEAN) {  // hybridDecoder(1).initSize: the u32 size
+    if (ps.val_len < 4) {
+      set_status(a.status, page, ST_VAL_INIT, E_EOF);
+      return;
+    }
   }
   if (lane == 0) {
     pi->rep_off = (int32_t)ps.rep_off;
@@ -1335,6 +1340,11 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
   } else if (d.enc == ENC_DELTA_BP) {
     dz.init(vals, vlen, c.ptype == T_INT32);
     delta_prev = (uint64_t)dz.first;
+  } else if (d.enc == ENC_RLE && c.ptype == T_BOOLEAN) {
+    // booleanRLEDecoder (type_boolean.go:97-117): u32 size, then a bit width 1
+    // hybrid stream limited to it (checked >= 4 bytes in k_prepare)
+    const uint32_t sz = load_u32_unaligned(vals);
+    keys.init(vals + 4, min<int64_t>((int64_t)sz, vlen - 4), 1);
   }
   Win SW;  // string-length window (PLAIN BYTE_ARRAY)
   SW.reset();
@@ -1407,7 +1417,39 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
     int64_t soff[4] = {0, 0, 0, 0}, slen[4] = {0, 0, 0, 0};
     const uint8_t *sbase_ptr = nullptr;
     if (m > 0) {
-      if (d.enc == ENC_PLAIN && !is_ba) {
+      if (c.ptype == T_BOOLEAN) {
+        uint32_t bv[4] = {0, 0, 0, 0};
+        if (d.enc == ENC_RLE) {  // type_boolean.go:106-117
+          uint32_t kk[4];
+          err = keys.next4(m, kk);
+          if (err) {
+            err_stage = ST_VALUES;
+            break;
+          }
+          int vi = 0;
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            bv[k] = dense ? kk[k] : pick4(kk, valid[k] ? vbase + vi : 0);
+            vi += valid[k];
+          }
+        } else {  // PLAIN, type_boolean.go:43-68: a byte per 8 values, LSB first
+          if ((nn_run + m + 7) >> 3 > vlen) {
+            err = E_EOF;
+            err_stage = ST_VALUES;
+            break;
+          }
+          int vi = 0;
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+            if (valid[k]) {
+              const int64_t jv = nn_run + vbase + vi;
+              bv[k] = (vals[jv >> 3] >> (jv & 7)) & 1u;
+              vi++;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = bv[k] == 1;
+      } else if (d.enc == ENC_PLAIN && !is_ba) {
         if ((nn_run + m) * (int64_t)w > vlen) {
           err = E_EOF;
           err_stage = ST_VALUES;
@@ -1602,7 +1644,8 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
       for (int k = 0; k < 4; k++) {
         if (slot[k]) {
           int64_t sl = slot_base + slot_run + sbase + si;
-          if (w == 4) *(uint32_t *)(c.values + sl * 4) = valid[k] ? (uint32_t)v[k] : 0u;
+          if (c.ptype == T_BOOLEAN) c.values[sl] = valid[k] ? (uint8_t)v[k] : (uint8_t)0;
+          else if (w == 4) *(uint32_t *)(c.values + sl * 4) = valid[k] ? (uint32_t)v[k] : 0u;
           else if (w == 8) *(uint64_t *)(c.values + sl * 8) = valid[k] ? v[k] : 0ull;
           else {
             uint8_t *op = c.values + sl * (int64_t)w;

@@ -79,7 +79,7 @@ def canon_flat(arr, width=None):
         out["values"] = np.frombuffer(b"".join(bs), np.uint8)
     else:
         np_t = {8: None}
-        filled = arr.fill_null(0) if arr.null_count else arr
+        filled = arr.fill_null(False if pa.types.is_boolean(t) else 0) if arr.null_count else arr
         v = np.asarray(filled.to_numpy(zero_copy_only=False))
         out["values"] = np.ascontiguousarray(v).view(np.uint8).ravel()
     return out
@@ -235,6 +235,21 @@ def fixtures():
     np.savez_compressed(os.path.join(HERE, "flba_decimal.npz"), c0_values=vals.ravel(), c0_validity=_bits(valid),
                         c0_slots=np.int64(len(dec)))
     manifest["flba_decimal"] = {"file": "flba_decimal.parquet", "columns": {"c0": {"leaf": 0, "kind": "flat"}}}
+
+    # BOOLEAN: PLAIN bit-packed (V1) and RLE (V2)
+    rng = np.random.default_rng(13)
+    n = 30000
+    t = pa.table({"b": pa.array(rng.random(n) < 0.3, mask=rng.random(n) < 0.1),
+                  "r": pa.array(rng.random(n) < 0.5)},
+                 schema=pa.schema([pa.field("b", pa.bool_()), pa.field("r", pa.bool_(), nullable=False)]))
+    record("bool_v1_plain", t, [("b", "flat"), ("r", "flat")], compression="snappy", data_page_version="1.0",
+           use_dictionary=False, row_group_size=16384)
+    runs = np.repeat(rng.random(n // 12) < 0.4, rng.integers(1, 24, n // 12))[:n]
+    t = pa.table({"b": pa.array(runs[:n], mask=rng.random(len(runs[:n])) < 0.2),
+                  "r": pa.array(rng.random(len(runs[:n])) < 0.5)},
+                 schema=pa.schema([pa.field("b", pa.bool_()), pa.field("r", pa.bool_(), nullable=False)]))
+    record("bool_v2_rle", t, [("b", "flat"), ("r", "flat")], compression="none", data_page_version="2.0",
+           use_dictionary=False, column_encoding={"b": "RLE", "r": "RLE"}, row_group_size=16384)
 
     # ---- reference-rejected files (defects D3 / D4 in SURVEY.md Appendix) ----
     # D3: DELTA page whose value count is 1 + 256k -> lookahead reads a missing block header

@@ -296,3 +296,49 @@ def test_tiled_corrupted_key_streams_match_oracle():
         except oracle.OracleError as e:
             outcomes.add(e.code)
     assert len(outcomes) >= 2, outcomes  # the corruptions reach more than one outcome
+
+
+def test_boolean_columns_generated():
+    """BOOLEAN (type_boolean.go): PLAIN bit-packed and RLE pages, nullable,
+    required and inside lists, V1 and V2."""
+    pa = pytest.importorskip("pyarrow")
+    rng = np.random.default_rng(31)
+    n = 70000
+    runs = np.repeat(rng.random(n // 5) < 0.5, rng.integers(1, 20, n // 5))[:n]
+    lists = [None if rng.random() < 0.05 else [bool(x) if rng.random() > 0.1 else None
+                                                for x in rng.random(rng.poisson(3)) < 0.5] for _ in range(n // 4)]
+    t = pa.table({"b": pa.array(rng.random(n) < 0.3, mask=rng.random(n) < 0.1),
+                  "r": pa.array(runs)})
+    tl = pa.table({"l": pa.array(lists, pa.list_(pa.bool_()))})
+    for ver, comp, enc in (("1.0", "snappy", None), ("1.0", "none", "RLE"), ("2.0", "none", None),
+                           ("2.0", "none", "PLAIN")):
+        kw = dict(compression=comp, data_page_version=ver, use_dictionary=False, row_group_size=30000)
+        if enc:
+            kw["column_encoding"] = {"b": enc, "r": enc}
+        check_file(_pq_bytes(t, **kw), "bool %s %s %s" % (ver, comp, enc))
+        kw.pop("column_encoding", None)
+        if enc:
+            kw["column_encoding"] = {"l": enc}
+        check_file(_pq_bytes(tl, **kw), "bool list %s %s %s" % (ver, comp, enc))
+
+
+def test_boolean_corrupted_pages_match_oracle():
+    """Seeded byte corruption of uncompressed BOOLEAN pages (PLAIN V1 and RLE
+    V2): the GPU reports the oracle's first error or decodes the same bytes."""
+    pq = pytest.importorskip("pyarrow.parquet")
+    pa = pytest.importorskip("pyarrow")
+    rng = np.random.default_rng(32)
+    n = 20000
+    runs = np.repeat(rng.random(n // 4) < 0.5, rng.integers(1, 16, n // 4))[:n]
+    t = pa.table({"r": pa.array(runs)}, schema=pa.schema([pa.field("r", pa.bool_(), nullable=False)]))
+    for ver, enc in (("1.0", "PLAIN"), ("2.0", "RLE")):
+        base = _pq_bytes(t, compression="none", data_page_version=ver, use_dictionary=False,
+                         column_encoding={"r": enc}, row_group_size=n, data_page_size=1 << 10)
+        cc = pq.ParquetFile(io.BytesIO(base)).metadata.row_group(0).column(0)
+        lo, hi = cc.data_page_offset, cc.data_page_offset + cc.total_compressed_size
+        for trial in range(16):
+            data = bytearray(base)
+            for _ in range(int(rng.integers(1, 4))):
+                p = int(rng.integers(lo + 8, hi))
+                data[p] ^= int(rng.integers(1, 256))
+            check_file(bytes(data), "bool corrupt %s %d" % (enc, trial))
