@@ -935,6 +935,10 @@ typedef struct {
     int64_t group[8];
     int is32;
   } dl_state;
+  /* DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY (type_bytearray.go:98-240) */
+  int32_t *pre, *suf;     /* prefix lengths (DELTA_BYTE_ARRAY), suffix / value lengths */
+  int32_t npre, nsuf, lpos;
+  bytebuf prev;           /* previous value (DELTA_BYTE_ARRAY) */
 } page_reader;
 
 /* ---- DELTA_BINARY_PACKED: deltabp_decoder.go:14-334 ---- */
@@ -1034,6 +1038,35 @@ static int delta_next(page_reader *p, int64_t *out) { /* :273-334 */
   return 0;
 }
 
+/* decodeInt32 over a fresh deltaBitPackDecoder32 on the page reader
+   (helpers.go:119-129, deltabp_decoder.go:14-175): every valuesCount value is
+   decoded, the reader left where the decoder's reads and padding skips leave it */
+static int delta_lengths(page_reader *p, int32_t **out, int32_t *count) {
+  *out = NULL;
+  *count = 0;
+  int e = delta_init(p, 1);
+  if (e) return e;
+  int32_t vc = p->dl_state.values_count;
+  size_t cap = 0;
+  int32_t *a = NULL;
+  for (int32_t i = 0; i < vc; i++) {
+    int64_t v;
+    e = delta_next(p, &v);
+    if (e) {
+      free(a);
+      return e;
+    }
+    if ((size_t)i >= cap) { /* grown as decoded: a corrupt count fails before a huge allocation */
+      cap = cap ? 2 * cap : 1024;
+      a = (int32_t *)realloc(a, cap * sizeof(int32_t));
+    }
+    a[i] = (int32_t)v;
+  }
+  *out = a;
+  *count = vc;
+  return 0;
+}
+
 /* ------------------------------------------------------------------------ */
 /* page reading (phase 1) and decoding (phase 2)                             */
 /* ------------------------------------------------------------------------ */
@@ -1099,7 +1132,7 @@ static int supported_value_encoding(const pqref_leaf *L, int enc, int has_dict) 
   if (enc == ENC_PLAIN_DICT) enc = ENC_RLE_DICT; /* chunk_reader.go:145-147 */
   switch (L->physical_type) {
     case PQR_BYTE_ARRAY:
-      return enc == ENC_PLAIN || enc == ENC_RLE_DICT ? 0 : (enc == ENC_DELTA_LBA || enc == ENC_DELTA_BA) ? PQR_ERR_UNSUPPORTED : PQR_ERR_ENCODING;
+      return enc == ENC_PLAIN || enc == ENC_RLE_DICT || enc == ENC_DELTA_LBA || enc == ENC_DELTA_BA ? 0 : PQR_ERR_ENCODING;
     case PQR_FLBA:
       return enc == ENC_PLAIN || enc == ENC_RLE_DICT ? 0 : enc == ENC_DELTA_BA ? PQR_ERR_UNSUPPORTED : PQR_ERR_ENCODING;
     case PQR_FLOAT:
@@ -1136,6 +1169,20 @@ static int values_init(page_reader *p, const pqref_leaf *L) {
     return 0;
   }
   if (enc == ENC_DELTA_BP) return delta_init(p, L->physical_type == PQR_INT32);
+  if ((enc == ENC_DELTA_LBA || enc == ENC_DELTA_BA) && L->physical_type == PQR_BYTE_ARRAY) {
+    /* byteArrayDeltaDecoder.init :186-209 (prefix lengths, then the suffixes'
+       DELTA_LENGTH stream); byteArrayDeltaLengthDecoder.init :98-108 */
+    int e;
+    if (enc == ENC_DELTA_BA) {
+      e = delta_lengths(p, &p->pre, &p->npre);
+      if (e) return e;
+    }
+    e = delta_lengths(p, &p->suf, &p->nsuf);
+    if (e) return e;
+    if (enc == ENC_DELTA_BA && p->npre != p->nsuf) return PQR_ERR_BYTE_ARRAY; /* "different number of suffixes and prefixes" */
+    p->lpos = 0;
+    return 0;
+  }
   if (enc == ENC_RLE && L->physical_type == PQR_BOOLEAN) {
     /* booleanRLEDecoder.init type_boolean.go:101-104: hybridDecoder(1).initSize
        (hybrid_decoder.go:57-67): u32 LE size, then a LimitReader over the rest */
@@ -1214,6 +1261,38 @@ static int values_decode(page_reader *p, const pqref_leaf *L, const dictionary *
         uint8_t v = (byte >> j) & 1;
         bb_put(&dp->vals, &v, 1);
       }
+    }
+    return 0;
+  }
+  if (enc == ENC_DELTA_LBA || enc == ENC_DELTA_BA) {
+    for (int64_t i = 0; i < count; i++) {
+      /* byteArrayDeltaLengthDecoder.next :111-123 */
+      if (p->lpos >= p->nsuf) return PQR_ERR_EOF;
+      int32_t size = p->suf[p->lpos];
+      if (size < 0) return PQR_ERR_BYTE_ARRAY; /* the reference panics in make([]byte, size) */
+      if (p->vr.n - p->vr.pos < (size_t)size) return PQR_ERR_EOF; /* io.ReadFull: "there is no byte left" */
+      const uint8_t *suffix = p->vr.p + p->vr.pos;
+      p->vr.pos += (size_t)size;
+      p->lpos++;
+      int64_t len;
+      if (enc == ENC_DELTA_LBA) {
+        len = size;
+        bb_put(&dp->lens, &len, 8);
+        bb_put(&dp->vals, suffix, (size_t)size);
+        continue;
+      }
+      /* byteArrayDeltaDecoder.decodeValues :211-240 */
+      int32_t pl = p->pre[p->lpos - 1];
+      if ((int64_t)pl + size < 0) return PQR_ERR_BYTE_ARRAY; /* make with a negative capacity panics */
+      if ((int64_t)p->prev.n < (int64_t)pl) return PQR_ERR_BYTE_ARRAY; /* "invalid prefix len" */
+      bytebuf v = {0};
+      if (pl > 0) bb_put(&v, p->prev.p, (size_t)pl);
+      bb_put(&v, suffix, (size_t)size);
+      len = (int64_t)v.n;
+      bb_put(&dp->lens, &len, 8);
+      bb_put(&dp->vals, v.p, v.n);
+      free(p->prev.p);
+      p->prev = v;
     }
     return 0;
   }
@@ -1563,8 +1642,12 @@ int pqref_decode(const pqref_file *f, int leaf, int rg0, int rg1, pqref_result *
       data_idx++;
     }
     total_pages += npages;
-    for (int i = 0; i < npages; i++)
+    for (int i = 0; i < npages; i++) {
       if (pages[i].own_body) free(pages[i].body);
+      free(pages[i].pre);
+      free(pages[i].suf);
+      free(pages[i].prev.p);
+    }
     free(pages);
     free(dict.fixed);
     free(dict.str_off);

@@ -67,6 +67,7 @@ struct PageDesc {
   int32_t tile_base;     // tiled page: first entry of its tile -> first-run index table
   int32_t job_base;      // tiled page: first entry of its job -> position table (page_jobs)
   int32_t alias_any;     // dictionary page: k_snappy may alias it at any alignment (LDS-group chunks)
+  int64_t lens_base;     // DELTA_(LENGTH_)BYTE_ARRAY page: its 2 x num_values length scratch (-1: none)
 };
 
 // Tiled flat decode (k_prepare's run walk + k_expand).  The run walk records,
@@ -151,6 +152,8 @@ struct PageInfo {
   int32_t cover;      // k_runs: values decodable before the first key-stream header error (n when none)
   uint32_t walk_err;  // k_runs: that header error (0: none); applied by k_level_check unless a
                       // dictionary error among the first `cover` values came first
+  int32_t str_data;   // DELTA string pages: values-section offset of the first suffix byte
+  int32_t str_cnt;    // DELTA string pages: decoded length entries (valuesCount)
 };
 
 }  // namespace pq

@@ -446,4 +446,52 @@ struct Delta {
   }
 };
 
+// decodeInt32 over a deltaBitPackDecoder32 that reads the values section from
+// offset `pos` (helpers.go:119-129, deltabp_decoder.go:14-175), as the
+// DELTA_(LENGTH_)BYTE_ARRAY decoders do at init (type_bytearray.go:98-108,
+// :186-209): every one of the stream's valuesCount values is decoded (errors
+// are init errors), the first `cap` are stored to `out`, and `pos` is left
+// where the reference's reader is left — the end of the last miniblock started
+// (the padding read of :150-155), then the skips of the remaining miniblocks
+// at the width of miniblock currentMiniBlock (:156-163, D5), clamped to the
+// section (io.ReadFull errors ignored).
+__device__ inline uint32_t delta_len_stream(const uint8_t *p, int64_t len, int64_t &pos, int32_t *out, int32_t cap,
+                                            int32_t &count) {
+  Delta dz;
+  uint32_t e = dz.init(p + pos, len - pos, true);
+  if (e) return e;
+  count = dz.total;
+  uint32_t prev = (uint32_t)dz.first;
+  const int lane = lane_id();
+  for (int32_t v0 = 0; v0 < count; v0 += 256) {
+    const int m = min(256, count - v0);
+    uint64_t dv[4];
+    e = dz.next4(m, dv);
+    if (e) return e;
+    // value j = first + the (wrapping int32) deltas before it
+    const uint32_t loc = (uint32_t)dv[0] + (uint32_t)dv[1] + (uint32_t)dv[2] + (uint32_t)dv[3];
+    uint32_t incl = loc;  // wrapping inclusive scan over lanes
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = shfl32(incl, lane >= d ? lane - d : lane);
+      if (lane >= d) incl += o;
+    }
+    uint32_t val = prev + (incl - loc);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int32_t j = v0 + 4 * lane + k;
+      if (4 * lane + k < m && j < cap) out[j] = (int32_t)val;
+      val += (uint32_t)dv[k];
+    }
+    prev += (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+  }
+  int64_t fin = dz.pos;
+  if (count > 0 && dz.cur_mb < dz.mb_count) {
+    const int32_t w = (int32_t)__builtin_amdgcn_readlane(dz.widths, dz.cur_mb);
+    fin += (int64_t)(dz.mb_count - dz.cur_mb) * (dz.mbvc >> 3) * w;
+  }
+  pos += min<int64_t>(fin, len - pos);
+  return E_OK;
+}
+
 }  // namespace pq

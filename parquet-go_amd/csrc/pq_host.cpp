@@ -53,6 +53,7 @@ struct pq_launch_args {
   int32_t npages_dbg;
   uint32_t *copy_cnt;
   int32_t *copy_idx;
+  int32_t *lens;
   void *runs;
   void *tile_info;
   const void *tiles;
@@ -517,6 +518,7 @@ struct pqg_batch {
   std::vector<uint32_t> status0;  // host-side initial status per page
   std::vector<int32_t> snappy_list, dict_list, data_list;
   std::vector<int32_t> general_list;  // data pages for k_decode (wave per page)
+  std::vector<int32_t> dba_list;      // DELTA_BYTE_ARRAY pages: value bytes by k_dba
   std::vector<TileJob> tiles;         // k_expand work list (XCD-affine order)
   int64_t run_entries = 0, tile_entries = 0;
   bool any_count = false;
@@ -536,6 +538,8 @@ struct pqg_batch {
   uint32_t max_jobs = 0;
   uint32_t *d_copy_cnt = nullptr;  // deferred literals registered per decode (two, by epoch parity)
   int32_t *d_copy_idx = nullptr;   // their job slots, compact
+  int32_t *d_lens = nullptr;       // DELTA string pages: length scratch
+  int64_t lens_entries = 0;
   uint64_t *d_dbg = nullptr;     // diagnostic stamps (PQ_STAMPS builds only)
   uint64_t *d_dbg2 = nullptr;
   void *d_runs = nullptr;        // run tables (k_prepare's run walk -> k_expand)
@@ -961,8 +965,7 @@ static int supported_encoding(int ptype, int enc) {
   if (enc == ENC_PLAIN_DICT) enc = ENC_RLE_DICT;  // chunk_reader.go:145-147
   switch (ptype) {
     case T_BYTE_ARRAY:
-      if (enc == ENC_PLAIN || enc == ENC_RLE_DICT) return 0;
-      return enc == ENC_DELTA_LBA || enc == ENC_DELTA_BA ? PQG_ERR_UNSUPPORTED : PQG_ERR_ENCODING;
+      return enc == ENC_PLAIN || enc == ENC_RLE_DICT || enc == ENC_DELTA_LBA || enc == ENC_DELTA_BA ? 0 : PQG_ERR_ENCODING;
     case T_FLBA:
       if (enc == ENC_PLAIN || enc == ENC_RLE_DICT) return 0;
       return enc == ENC_DELTA_BA ? PQG_ERR_UNSUPPORTED : PQG_ERR_ENCODING;
@@ -1081,6 +1084,7 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
     PageDesc d;
     memset(&d, 0, sizeof(d));
     d.job_base = -1;  // not a tiled page
+    d.lens_base = -1;
     d.col = ci;
     d.rg = rg;
     d.ord = w.ord;
@@ -1191,6 +1195,10 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
     } else {
       B->data_list.push_back(my_index);
       level_base += d.num_values;
+      if (L.physical_type == T_BYTE_ARRAY && (d.enc == ENC_DELTA_LBA || d.enc == ENC_DELTA_BA)) {
+        B->pages.back().lens_base = B->lens_entries;  // suffix lengths, then prefix lengths
+        B->lens_entries += 2 * (int64_t)std::max(d.num_values, 0);
+      }
     }
     if (needs_device_codec) B->snappy_list.push_back(my_index);
   }
@@ -1275,6 +1283,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
                  (d.enc == ENC_PLAIN || d.enc == ENC_RLE_DICT);
     if (!tiled) {
       B->general_list.push_back(pi);
+      if (L.physical_type == T_BYTE_ARRAY && d.enc == ENC_DELTA_BA) B->dba_list.push_back(pi);
       continue;
     }
     const int32_t n = std::max(d.num_values, 0);
@@ -1423,7 +1432,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   rc |= alloc_dev((void **)&B->d_status, sizeof(uint32_t) * npages);
   rc |= alloc_dev((void **)&B->d_cols, sizeof(ColDesc) * B->cols.size());
   rc |= alloc_dev((void **)&B->d_dict, sizeof(uint64_t) * (size_t)B->dict_entries);
-  size_t nl = B->snappy_list.size() + B->dict_list.size() + 2 * B->data_list.size() + 16;
+  size_t nl = B->snappy_list.size() + B->dict_list.size() + 3 * B->data_list.size() + 16;
   rc |= alloc_dev((void **)&B->d_lists, sizeof(int32_t) * nl);
   rc |= alloc_dev(&B->d_runs, 8 * (size_t)(B->run_entries + 64));
   rc |= alloc_dev(&B->d_tile_info, 8 * (size_t)(B->tile_entries + EX_WAVE_VALUES / RUN_TILE + 1));
@@ -1458,6 +1467,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   rc |= alloc_dev((void **)&B->d_job_owner, 4 * (job_owner.size() + 1));
   rc |= alloc_dev((void **)&B->d_copy_cnt, 16);
   rc |= alloc_dev((void **)&B->d_copy_idx, 4 * (job_owner.size() + 1));
+  rc |= alloc_dev((void **)&B->d_lens, 4 * (size_t)(B->lens_entries + 1));
   if (!rc) {
     hipMemset(B->d_copy_cnt, 0, 16);
     hipMemcpy(B->d_job_base, job_base.data(), 4 * job_base.size(), hipMemcpyHostToDevice);
@@ -1504,6 +1514,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
     lists.insert(lists.end(), B->dict_list.begin(), B->dict_list.end());
     lists.insert(lists.end(), B->data_list.begin(), B->data_list.end());
     lists.insert(lists.end(), B->general_list.begin(), B->general_list.end());
+    lists.insert(lists.end(), B->dba_list.begin(), B->dba_list.end());
     if (!lists.empty()) HIPCHK(hipMemcpy(B->d_lists, lists.data(), sizeof(int32_t) * lists.size(), hipMemcpyHostToDevice));
   }
   memcpy(B->h_status, B->status0.data(), sizeof(uint32_t) * npages);
@@ -1634,6 +1645,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.job_owner = B->d_job_owner;
   a.copy_cnt = B->d_copy_cnt;
   a.copy_idx = B->d_copy_idx;
+  a.lens = B->d_lens;
   a.dbg = B->d_dbg;
   a.dbg2 = B->d_dbg2;
   a.npages_dbg = (int32_t)B->pages.size() + 1;
@@ -1682,6 +1694,11 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     a.list = B->d_lists + ns + nd + ndata;
     a.nlist = ngen;
     e |= pq_launch(3, &a, s);
+    if (!B->dba_list.empty()) {  // DELTA_BYTE_ARRAY value bytes (after k_decode's offsets)
+      a.list = B->d_lists + ns + nd + ndata + ngen;
+      a.nlist = (int32_t)B->dba_list.size();
+      e |= pq_launch(10, &a, s);
+    }
     a.nlist = (int32_t)B->tiles.size();
     a.ld_sel = getenv("PQG_OLD_EXPAND") && getenv("PQG_NO_LDS_DICT") ? 1 : 0;
     e |= pq_launch(9, &a, s);  // k_expand_mix (tiled pages)
@@ -1891,6 +1908,7 @@ void pqg_batch_destroy(pqg_batch *B) {
   hipFree(B->d_job_owner);
   hipFree(B->d_copy_cnt);
   hipFree(B->d_copy_idx);
+  hipFree(B->d_lens);
   hipFree(B->d_dbg);
   hipFree(B->d_dbg2);
   hipFree(B->d_runs);

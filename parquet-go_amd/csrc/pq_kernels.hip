@@ -75,6 +75,7 @@ struct KArgs {
   int32_t knob;           // analysis only (PQG_KNOB): 1 no gathers, 2 no stores, 3 neither
   uint32_t *copy_cnt;     // deferred literals registered this decode: [epoch & 1] (the other is reset)
   int32_t *copy_idx;      // their job slots, compact (k_snappy -> k_copy)
+  int32_t *lens;          // DELTA string pages: suffix lengths [0, nv), prefix lengths [nv, 2 nv)
   const TileJob *tiles;   // k_expand: one workgroup per entry
   const LdsGroup *lgroups;  // k_expand_ld: one workgroup per entry
 };
@@ -1046,6 +1047,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
       return;
     }
   }
+  // DELTA_(LENGTH_)BYTE_ARRAY: every length stream is decoded at init
+  // (type_bytearray.go:98-108, :186-209); lengths go to the page's scratch
+  int32_t dstr_data = 0, dstr_cnt = 0;
+  const bool dstr = c.ptype == T_BYTE_ARRAY && (d.enc == ENC_DELTA_LBA || d.enc == ENC_DELTA_BA) && d.lens_base >= 0;
+  if (dstr) {
+    const int32_t nvp = max(d.num_values, 0);
+    int32_t *S = a.lens + d.lens_base, *P = S + nvp;
+    const uint8_t *vp = ps.body + ps.val_off;
+    int64_t pos = 0;
+    int32_t cp = 0, cs = 0;
+    if (d.enc == ENC_DELTA_BA) {
+      e = delta_len_stream(vp, ps.val_len, pos, P, nvp, cp);  // prefix lengths
+      if (e) {
+        set_status(a.status, page, ST_VAL_INIT, e);
+        return;
+      }
+    }
+    e = delta_len_stream(vp, ps.val_len, pos, S, nvp, cs);  // suffix (value) lengths
+    if (e) {
+      set_status(a.status, page, ST_VAL_INIT, e);
+      return;
+    }
+    if (d.enc == ENC_DELTA_BA && cp != cs) {  // "different number of suffixes and prefixes"
+      set_status(a.status, page, ST_VAL_INIT, E_BYTE_ARRAY);
+      return;
+    }
+    dstr_data = (int32_t)pos;
+    dstr_cnt = cs;
+    if (lane == 0) {
+      pi->str_data = dstr_data;
+      pi->str_cnt = dstr_cnt;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the counts below read the lengths back
+  }
   if (lane == 0) {
     pi->rep_off = (int32_t)ps.rep_off;
     pi->rep_len = (int32_t)ps.rep_len;
@@ -1183,6 +1218,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         acc = (int64_t)ufirst64((int64_t)shfl64((uint64_t)acc, 63));
       }
       sbytes = acc;
+    } else if (dstr) {
+      // byteArrayDeltaLengthDecoder.next (:111-123) and, for DELTA_BYTE_ARRAY,
+      // the prefix checks of decodeValues (:211-240), in value order
+      const int32_t nvp = max(d.num_values, 0);
+      const int32_t *S = a.lens + d.lens_base, *P = S + nvp;
+      const int64_t vlen = ps.val_len;
+      int64_t acc_s = 0, acc_v = 0;
+      int64_t prevlen = 0;  // the previous value's length (the first value follows an empty one)
+      for (int64_t k0 = 0; k0 < nn; k0 += 64) {
+        const int cnt = (int)min<int64_t>(64, nn - k0);
+        const int64_t i = k0 + lane;
+        const bool act = lane < cnt;
+        uint32_t code = 0;
+        int64_t s = 0, pl = 0;
+        if (act) {
+          if (i >= dstr_cnt) code = E_EOF;  // position >= len(lens)
+          else {
+            s = S[i];
+            if (s < 0) code = E_BYTE_ARRAY;  // make([]byte, size) panics in the reference
+            if (d.enc == ENC_DELTA_BA) pl = P[i];
+          }
+        }
+        const int64_t s_ok = act && !code ? s : 0;
+        const int64_t sincl = wave_incl_scan64(s_ok);
+        if (act && !code && dstr_data + acc_s + sincl > vlen) code = E_EOF;  // io.ReadFull
+        int64_t vl = s;  // value length
+        if (d.enc == ENC_DELTA_BA) {
+          vl = (pl > 0 ? pl : 0) + s;
+          const int64_t pv = (int64_t)shfl64((uint64_t)vl, lane > 0 ? lane - 1 : 0);
+          const int64_t plen_prev = lane == 0 ? prevlen : pv;
+          if (act && !code && (pl + s < 0 || plen_prev < pl)) code = E_BYTE_ARRAY;  // "invalid prefix len"
+        }
+        const uint64_t bad = ballot(act && code != 0);
+        if (bad) {
+          set_status(a.status, page, ST_VALUES, __builtin_amdgcn_readlane(code, __builtin_ctzll(bad)));
+          return;
+        }
+        acc_s += (int64_t)shfl64((uint64_t)sincl, 63);
+        acc_v += (int64_t)shfl64((uint64_t)wave_incl_scan64(act ? vl : 0), 63);
+        prevlen = (int64_t)shfl64((uint64_t)vl, cnt - 1);
+      }
+      sbytes = acc_v;
     } else {
       set_status(a.status, page, ST_VALUES, E_UNSUPPORTED);
       return;
@@ -1349,6 +1426,11 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
   Win SW;  // string-length window (PLAIN BYTE_ARRAY)
   SW.reset();
   int64_t spos = 0;
+  // DELTA strings: lengths decoded and validated by k_prepare (scratch); suffix
+  // bytes start at str_data.  DELTA_BYTE_ARRAY bytes are written by k_dba.
+  const bool dstr = is_ba && (d.enc == ENC_DELTA_LBA || d.enc == ENC_DELTA_BA) && d.lens_base >= 0;
+  const bool defer_bytes = dstr && d.enc == ENC_DELTA_BA;
+  int64_t dpos = pi.str_data;
 
   const int64_t slot_base = flat ? d.level_base : pi.slot_base;
   int64_t e0 = 0, slot_run = 0, row_run = 0, nn_run = 0, str_run = pi.str_base;
@@ -1544,6 +1626,46 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
 #pragma unroll
         for (int k = 0; k < 4; k++)
           if (c.ptype == T_INT32) v[k] &= 0xffffffffull;
+      } else if (dstr) {
+        // value j -> lane j>>2, element j&3: suffix lengths S, prefix lengths P
+        const int32_t nvp = max(n, 0);
+        const int32_t *S = a.lens + d.lens_base, *P = S + nvp;
+        uint32_t eo[4] = {0, 0, 0, 0}, el[4] = {0, 0, 0, 0};
+        int64_t sl4[4];
+        int64_t loc = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int t = 4 * lane + k;
+          const int64_t i = nn_run + t;
+          sl4[k] = t < m ? (int64_t)S[i] : 0;
+          int64_t vl = sl4[k];
+          if (d.enc == ENC_DELTA_BA && t < m) {
+            const int32_t pl = P[i];
+            vl += pl > 0 ? pl : 0;
+          }
+          el[k] = (uint32_t)vl;
+          loc += sl4[k];
+        }
+        const int64_t incl = wave_incl_scan64(loc);
+        int64_t o = dpos + (incl - loc);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          eo[k] = (uint32_t)o;
+          o += sl4[k];
+        }
+        dpos += (int64_t)shfl64((uint64_t)incl, 63);
+        int vi = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          int j = valid[k] ? vbase + vi : 0;
+          uint32_t oo = dense ? eo[k] : pick4(eo, j), ll = dense ? el[k] : pick4(el, j);
+          if (valid[k]) {
+            soff[k] = oo;
+            slen[k] = ll;
+          }
+          vi += valid[k];
+        }
+        sbase_ptr = vals;
       } else if (d.enc == ENC_PLAIN && is_ba) {
         // serial length walk (type_bytearray.go:24-45); value j -> lane j>>2, element j&3
         uint32_t eo[4] = {0, 0, 0, 0}, el[4] = {0, 0, 0, 0};
@@ -1609,7 +1731,7 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
         if (slot[k]) {
           start += ll[k];
           c.str_offsets[slot_base + slot_run + sbase + si + 1] = start;
-          if (valid[k]) {
+          if (valid[k] && !defer_bytes) {
             const uint8_t *sp = sbase_ptr + soff[k];
             uint8_t *op = c.values + start - ll[k];
             for (int64_t b = 0; b < ll[k]; b++) op[b] = sp[b];
@@ -2325,6 +2447,62 @@ __global__ __launch_bounds__(LD_WAVES_H * 64) void k_expand_mix(KArgs a) {
   else mix_lds<WIDTH>(a, g, lds_dyn);
 }
 
+// ===========================================================================
+// K5b: k_dba — DELTA_BYTE_ARRAY value bytes (type_bytearray.go:211-240): value
+// i = previous value[:prefix_i] + suffix_i, rebuilt in value order by one wave
+// per page over an LDS copy of the previous value (updated in place: only the
+// suffix is written).  Lengths were decoded and validated by k_prepare, and the
+// string offsets / validity written by k_decode; a batch's suffix bytes are
+// contiguous in the page and staged in LDS when they fit.  Values longer than
+// DBA_PREV bytes are reported PQG_ERR_UNSUPPORTED (a documented limit).
+// ===========================================================================
+constexpr int DBA_PREV = 16384, DBA_STAGE = 8192;  // per wave: 96 KiB of LDS per workgroup
+
+__global__ __launch_bounds__(256) void k_dba(KArgs a) {
+  __shared__ uint8_t prev_all[4][DBA_PREV];
+  __shared__ uint8_t stage_all[4][DBA_STAGE];
+  const int wv = (int)ufirst(threadIdx.x >> 6);
+  const int gi = blockIdx.x * 4 + wv;
+  if (gi >= a.nlist) return;
+  const int lane = lane_id();
+  const int page = ufirst(a.list[gi]);
+  if (page_status(a.status, page) != STATUS_OK) return;
+  const PageDesc d = a.pages[page];
+  const ColDesc c = a.cols[d.col];
+  const PageInfo pi = a.info[page];
+  const int64_t nn = pi.non_null;
+  const uint8_t *data = body_ptr(a, d, page) + pi.val_off + pi.str_data;
+  const int32_t nvp = max(d.num_values, 0);
+  const int32_t *S = a.lens + d.lens_base, *P = S + nvp;
+  uint8_t *prev = prev_all[wv], *stage = stage_all[wv];
+  uint8_t *out = c.values + pi.str_base;
+  int64_t soff = 0, ooff = 0;
+  for (int64_t i0 = 0; i0 < nn; i0 += 64) {
+    const int cnt = (int)min<int64_t>(64, nn - i0);
+    const int32_t s_l = lane < cnt ? S[i0 + lane] : 0;
+    const int32_t p_l = lane < cnt ? P[i0 + lane] : 0;
+    int32_t stot;
+    const int32_t sexcl = wave_excl_scan32(s_l, &stot);
+    const bool staged = stot <= DBA_STAGE;
+    if (staged)
+      for (int32_t b = lane; b < stot; b += 64) stage[b] = data[soff + b];
+    for (int t = 0; t < cnt; t++) {
+      const int32_t s = (int32_t)__builtin_amdgcn_readlane((uint32_t)s_l, t);
+      const int32_t pl = (int32_t)__builtin_amdgcn_readlane((uint32_t)p_l, t);
+      const int32_t so = (int32_t)__builtin_amdgcn_readlane((uint32_t)sexcl, t);
+      const int32_t plen = pl > 0 ? pl : 0, vl = plen + s;
+      if (vl > DBA_PREV) {
+        set_status(a.status, page, ST_VALUES, E_UNSUPPORTED);
+        return;
+      }
+      for (int32_t b = lane; b < s; b += 64) prev[plen + b] = staged ? stage[so + b] : data[soff + so + b];
+      for (int32_t b = lane; b < vl; b += 64) out[ooff + b] = prev[b];
+      ooff += vl;
+    }
+    soff += stot;
+  }
+}
+
 // level-error precedence pass: for pages that failed in k_decode at the
 // values or def stage, finish decoding the earlier level streams to see if
 // the reference would have failed there first.
@@ -2400,6 +2578,7 @@ struct pq_launch_args {
   int32_t npages_dbg;
   uint32_t *copy_cnt;
   int32_t *copy_idx;
+  int32_t *lens;
   void *runs;
   void *tile_info;
   const void *tiles;
@@ -2434,6 +2613,7 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   k.job_owner = p->job_owner;
   k.copy_cnt = p->copy_cnt;
   k.copy_idx = p->copy_idx;
+  k.lens = p->lens;
   k.dbg = p->dbg;
   k.dbg2 = p->dbg2;
   k.dbg3 = p->dbg2 ? p->dbg2 + 8 * (size_t)p->npages_dbg : nullptr;
@@ -2511,6 +2691,7 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     case 2: hipLaunchKernelGGL(pq::k_prepare, grid, block, 0, s, k); break;
     case 3: hipLaunchKernelGGL(pq::k_decode, grid, block, 0, s, k); break;
     case 5: hipLaunchKernelGGL(pq::k_level_check, grid, block, 0, s, k); break;
+    case 10: hipLaunchKernelGGL(pq::k_dba, grid, block, 0, s, k); break;
     default: return 1;
   }
   return hipGetLastError() == hipSuccess ? 0 : 17;

@@ -251,6 +251,17 @@ def fixtures():
     record("bool_v2_rle", t, [("b", "flat"), ("r", "flat")], compression="none", data_page_version="2.0",
            use_dictionary=False, column_encoding={"b": "RLE", "r": "RLE"}, row_group_size=16384)
 
+    # DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY strings:
+    # sorted words (shared prefixes), nulls, several pages and row groups
+    rng = np.random.default_rng(14)
+    n = 45000
+    words = sorted("k%05d/%s" % (rng.integers(0, 4000), "ab" * int(rng.integers(0, 9))) for _ in range(n))
+    t = pa.table({"l": pa.array(words, type=pa.string(), mask=rng.random(n) < 0.1),
+                  "d": pa.array(words, type=pa.string(), mask=rng.random(n) < 0.05)})
+    record("delta_strings", t, [("l", "flat"), ("d", "flat")], compression="snappy", data_page_version="1.0",
+           use_dictionary=False, column_encoding={"l": "DELTA_LENGTH_BYTE_ARRAY", "d": "DELTA_BYTE_ARRAY"},
+           row_group_size=20000)
+
     # ---- reference-rejected files (defects D3 / D4 in SURVEY.md Appendix) ----
     # D3: DELTA page whose value count is 1 + 256k -> lookahead reads a missing block header
     t = pa.table({"ts": pa.array(np.arange(257, dtype=np.int64) * 3)},
@@ -269,6 +280,14 @@ def fixtures():
     record("err_v2_uncompressed_flag", t, [("x", "flat")],
            errors={0: (7, "D4: page_v2.go:123 ignores is_compressed; snappy rejects the raw bytes")},
            compression="snappy", data_page_version="2.0", use_dictionary=False)
+
+    # D3 on a length stream: 129 strings -> the lookahead of the 129th length
+    # reads a block header out of the string bytes (widths > 32 here)
+    t = pa.table({"s": pa.array(["w%03d" % i for i in range(129)], type=pa.string())},
+                 schema=pa.schema([pa.field("s", pa.string(), nullable=False)]))
+    record("err_delta_strings_129", t, [("s", "flat")],
+           errors={0: (15, "D3: deltabp_decoder.go:115-127 lookahead reads a block header from the string bytes")},
+           compression="none", use_dictionary=False, column_encoding={"s": "DELTA_LENGTH_BYTE_ARRAY"})
 
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)

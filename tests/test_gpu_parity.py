@@ -342,3 +342,47 @@ def test_boolean_corrupted_pages_match_oracle():
                 p = int(rng.integers(lo + 8, hi))
                 data[p] ^= int(rng.integers(1, 256))
             check_file(bytes(data), "bool corrupt %s %d" % (enc, trial))
+
+
+@pytest.mark.parametrize("enc", ["DELTA_LENGTH_BYTE_ARRAY", "DELTA_BYTE_ARRAY"])
+def test_delta_strings_generated(enc):
+    """DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY (type_bytearray.go:98-240):
+    page sizes around the length streams' block and miniblock edges (the
+    reference's lookahead, D3, included), nulls, long values, V1 and V2, lists."""
+    pa = pytest.importorskip("pyarrow")
+    rng = np.random.default_rng(41)
+    for n in (1, 2, 63, 64, 65, 129, 130, 700, 25000):
+        words = sorted("p%04d:%s" % (rng.integers(0, 500), "xyz" * int(rng.integers(0, 30))) for _ in range(n))
+        if n == 700:  # long values, shared prefixes
+            words = [w * int(rng.integers(1, 60)) for w in words]
+        for nulls in (0.0, 0.2):
+            t = pa.table({"s": pa.array(words, type=pa.string(), mask=rng.random(n) < nulls)})
+            for ver in ("1.0", "2.0"):
+                check_file(_pq_bytes(t, compression="none" if ver == "2.0" else "snappy", data_page_version=ver,
+                                     use_dictionary=False, column_encoding={"s": enc}), "%s n%d %.1f v%s" % (enc, n, nulls, ver))
+    lists = [None if rng.random() < 0.05 else ["q%d" % v for v in sorted(rng.integers(0, 300, rng.poisson(3)))]
+             for _ in range(20000)]
+    tl = pa.table({"l": pa.array(lists, pa.list_(pa.string()))})
+    check_file(_pq_bytes(tl, compression="snappy", use_dictionary=False, column_encoding={"l": enc}), enc + " list")
+
+
+@pytest.mark.parametrize("enc", ["DELTA_LENGTH_BYTE_ARRAY", "DELTA_BYTE_ARRAY"])
+def test_delta_strings_corrupted_match_oracle(enc):
+    """Seeded corruption of uncompressed DELTA string pages: the GPU reports the
+    oracle's first error (length-stream init errors, EOF, invalid prefix
+    lengths) or decodes the same bytes."""
+    pq = pytest.importorskip("pyarrow.parquet")
+    pa = pytest.importorskip("pyarrow")
+    rng = np.random.default_rng(42 if enc[6] == "L" else 43)
+    n = 3000
+    words = sorted("k%03d/%s" % (rng.integers(0, 300), "ab" * int(rng.integers(0, 6))) for _ in range(n))
+    t = pa.table({"s": pa.array(words, type=pa.string())}, schema=pa.schema([pa.field("s", pa.string(), nullable=False)]))
+    base = _pq_bytes(t, compression="none", use_dictionary=False, column_encoding={"s": enc}, data_page_size=4 << 10)
+    cc = pq.ParquetFile(io.BytesIO(base)).metadata.row_group(0).column(0)
+    lo, hi = cc.data_page_offset, cc.data_page_offset + cc.total_compressed_size
+    for trial in range(20):
+        data = bytearray(base)
+        for _ in range(int(rng.integers(1, 4))):
+            p = int(rng.integers(lo + 8, hi))
+            data[p] ^= int(rng.integers(1, 256))
+        check_file(bytes(data), "%s corrupt %d" % (enc, trial))
