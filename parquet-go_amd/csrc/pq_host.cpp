@@ -1830,7 +1830,8 @@ int pqg_batch_stats_get(const pqg_batch *B, pqg_batch_stats *o) {
   memset(o, 0, sizeof(*o));
   o->pages = (int64_t)B->pages.size();
   o->data_pages = (int64_t)B->data_list.size();
-  o->dict_pages = (int64_t)B->dict_list.size();
+  o->dict_pages = 0;
+  for (const PageDesc &pd : B->pages) o->dict_pages += pd.kind == PAGE_DICT;
   o->snappy_pages = (int64_t)B->snappy_list.size();
   o->host_inflated_pages = B->host_inflated;
   o->staged_bytes = B->staged_bytes;

@@ -770,6 +770,14 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
   while (v < n) {
     // ---- chain mode ----
     if (chain) {
+#ifdef PQ_STAMPS
+      if (a.dbg3 && (int)(pi - a.info) == 1 && lane == 0 && iters < 60) {
+        a.dbg3[iters * 4 + 0] = __builtin_amdgcn_s_memrealtime();
+        a.dbg3[iters * 4 + 1] = (uint64_t)hpos | (1ull << 40);
+        a.dbg3[iters * 4 + 2] = (uint64_t)v;
+        a.dbg3[iters * 4 + 3] = (uint64_t)(R.base + R.cnt);
+      }
+#endif
       if (!W.ab || ks + hpos < W.ab || (ks + hpos) - W.ab > 512) W.fill(ks + hpos);
       const int64_t wbo = W.ab - ks;  // stream offset of window byte 0
       if (W.ab != nx_ab) {
