@@ -186,6 +186,9 @@ def main():
         step()
     batch.sync()
     batch.kernel_times()  # drop warmup events
+    # the decode phase is bracketed by HIP events on a sample of the timed steps
+    # (each event pair costs a few us of launch gap); at least 5 samples
+    batch.set_timing(max(1, args.steps // 5))
     barrier()
     hip = ctypes.CDLL("libamdhip64.so")
     hip.hipDeviceSynchronize()

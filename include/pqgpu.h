@@ -185,6 +185,10 @@ int pqg_batch_stats_get(const pqg_batch *b, pqg_batch_stats *out);
  * PQG_SEGMENT_TIMES=1 every phase is bracketed (events add launch gaps).
  * names/ms have room for `cap` entries; returns the number of segments. */
 int pqg_batch_kernel_times(pqg_batch *b, const char **names, float *ms, int cap);
+/* Record the timing events on every `every`-th decode only (1: every decode,
+ * the default; 0: never).  Each event pair costs a few µs of launch gap, so a
+ * throughput loop samples the kernel times instead of timing every pass. */
+int pqg_batch_set_timing(pqg_batch *b, int every);
 void pqg_batch_destroy(pqg_batch *b);
 
 #ifdef __cplusplus

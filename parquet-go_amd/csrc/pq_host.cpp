@@ -562,6 +562,8 @@ struct pqg_batch {
   hipEvent_t ev[kRing][8] = {};
   int nev = 0;
   bool seg_times = false;  // PQG_SEGMENT_TIMES=1: events between every phase (adds launch gaps)
+  int time_every = 1;      // pqg_batch_set_timing: events on every n-th decode (0: none)
+  int64_t decodes = 0;
   int ring_head = 0, ring_count = 0;
   double kms_sum[8] = {};
   int kms_n = 0;
@@ -1667,7 +1669,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   const int32_t ns = (int32_t)B->snappy_list.size(), nd = (int32_t)B->dict_list.size(),
                 ndata = (int32_t)B->data_list.size(), ngen = (int32_t)B->general_list.size();
   int e = 0;
-  B->nev = 0;
+  if (timed) B->nev = 0;  // an untimed decode keeps the last timed segment count
   hipEvent_t *evs = B->ev[B->ring_head];
   // events cost a gap between dependent kernels: by default only the decode
   // phase is bracketed (the roofline kernel), PQG_SEGMENT_TIMES=1 brackets all
@@ -1722,9 +1724,18 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
 int pqg_batch_decode(pqg_batch *B) {
   if (!B) return PQG_ERR_ARG;
   HIPCHK(hipSetDevice(B->ctx->device));
-  int rc = launch_all(B, false, true);
+  const bool timed = B->time_every > 0 && B->decodes % B->time_every == 0;
+  B->decodes++;
+  int rc = launch_all(B, false, timed);
   B->decoded = rc == 0;
   return rc;
+}
+
+int pqg_batch_set_timing(pqg_batch *B, int every) {
+  if (!B || every < 0) return PQG_ERR_ARG;
+  B->time_every = every;
+  B->decodes = 0;
+  return PQG_OK;
 }
 
 int pqg_batch_sync(pqg_batch *B) {

@@ -53,7 +53,7 @@ EXPORTS = [
     "pqg_file_column_count", "pqg_file_column_info", "pqg_file_find_column", "pqg_file_select_columns",
     "pqg_file_last_error", "pqg_batch_create", "pqg_batch_decode", "pqg_batch_sync",
     "pqg_batch_error_location", "pqg_batch_column", "pqg_batch_copy", "pqg_batch_stats_get",
-    "pqg_batch_kernel_times", "pqg_batch_destroy",
+    "pqg_batch_kernel_times", "pqg_batch_set_timing", "pqg_batch_destroy",
 ]
 
 
@@ -127,6 +127,7 @@ def lib():
                 "pqg_batch_copy": (i32, [vp, i32, i32, vp, sz, P(sz)]),
                 "pqg_batch_stats_get": (i32, [vp, P(BatchStats)]),
                 "pqg_batch_kernel_times": (i32, [vp, P(ctypes.c_char_p), P(ctypes.c_float), i32]),
+                "pqg_batch_set_timing": (i32, [vp, i32]),
                 "pqg_batch_destroy": (None, [vp]),
             }
             for name, (res, args) in sig.items():
@@ -288,6 +289,10 @@ class Batch:
         s = BatchStats()
         _check(lib().pqg_batch_stats_get(self._h, ctypes.byref(s)))
         return {f: getattr(s, f) for f, _ in s._fields_}
+
+    def set_timing(self, every):
+        """Record the timing events on every `every`-th decode (0: never)."""
+        _check(lib().pqg_batch_set_timing(self._h, int(every)), "pqg_batch_set_timing")
 
     def kernel_times(self):
         names = (ctypes.c_char_p * 16)()
