@@ -731,6 +731,24 @@ struct RunBuf {
     base += cnt;
     cnt = 0;
   }
+  // lanes 0..m-1 hold m new runs: buffer them after the ones already held
+  __device__ __forceinline__ void append(int m, uint2 x, int32_t s, int32_t e, int32_t b, int32_t w) {
+    if (cnt + m > 64) flush();
+    const int l = lane_id(), src = (l - cnt) & 63;
+    const bool mine = l >= cnt && l < cnt + m;
+    const uint32_t xx = shfl32(x.x, src), xy = shfl32(x.y, src);
+    const int32_t ss = (int32_t)shfl32((uint32_t)s, src), ee2 = (int32_t)shfl32((uint32_t)e, src);
+    const int32_t bb = (int32_t)shfl32((uint32_t)b, src), ww = (int32_t)shfl32((uint32_t)w, src);
+    if (mine) {
+      ent = make_uint2(xx, xy);
+      es = ss;
+      ee = ee2;
+      tb = bb;
+      tbw = ww;
+    }
+    cnt += m;
+    if (cnt == 64) flush();
+  }
 };
 
 // Chain mode (streams of short runs, e.g. a bit width 1 key stream that
@@ -809,8 +827,7 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
         r = (int32_t)nx;
       }
       if (cnt >= 2) {
-        R.flush();
-        const int32_t nr0 = R.base;
+        const int32_t nr0 = R.base + R.cnt;  // index of the first chained run
         const bool in = lane < cnt;
         const uint32_t b = in ? lbytes[myr] : 0u;
         const bool bp = (b & 1) != 0;
@@ -835,11 +852,10 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
         const uint64_t okm = ballot(ok), badm = ballot(ok && bad);
         const int m = min((int)__popcll(okm), badm ? (int)__builtin_ctzll(badm) : 64);
         if (m > 0) {
-          if (lane < m) {
-            const int64_t e = min<int64_t>(st + len, (int64_t)n);
-            R.runs[nr0 + lane] = make_uint2((uint32_t)st | (bp ? 0u : RUN_RLE), bp ? (uint32_t)data : val);
-            tiles_of_run(R.tf, st, e, nr0 + lane, bp ? data : data + sz, bp ? bw : -1);
-          }
+          // buffered in lanes with the serial step's runs: no stores before the next window load
+          const int64_t e = min<int64_t>(st + len, (int64_t)n);
+          R.append(m, make_uint2((uint32_t)st | (bp ? 0u : RUN_RLE), bp ? (uint32_t)data : val), (int32_t)st,
+                   (int32_t)e, (int32_t)(bp ? data : data + sz), bp ? bw : -1);
           const int32_t last = m - 1;
           const uint32_t lr = __builtin_amdgcn_readlane(myr, last);
           const uint32_t lb = __builtin_amdgcn_readlane(b, last);
@@ -847,7 +863,6 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
           const int64_t hnext = wbo + lr + 1 + ((lb & 1) ? (int64_t)(lb >> 1) * bw : (int64_t)sz);
           chain = hnext - hpos < 48 * (int64_t)m;  // still short runs on average
           hpos = hnext;
-          R.base += m;
           iters++;
           continue;
         }
