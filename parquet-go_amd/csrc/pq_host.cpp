@@ -519,6 +519,7 @@ struct pqg_batch {
   std::vector<int32_t> snappy_list, dict_list, data_list;
   std::vector<int32_t> general_list;  // data pages for k_decode (wave per page)
   std::vector<int32_t> dba_list;      // DELTA_BYTE_ARRAY pages: value bytes by k_dba
+  bool data_may_defer = false;        // some data page's Snappy body may hold a deferred literal
   std::vector<TileJob> tiles;         // k_expand work list (XCD-affine order)
   int64_t run_entries = 0, tile_entries = 0;
   bool any_count = false;
@@ -1087,6 +1088,7 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
     memset(&d, 0, sizeof(d));
     d.job_base = -1;  // not a tiled page
     d.lens_base = -1;
+    d.sidx = -1;
     d.col = ci;
     d.rg = rg;
     d.ord = w.ord;
@@ -1202,7 +1204,12 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
         B->lens_entries += 2 * (int64_t)std::max(d.num_values, 0);
       }
     }
-    if (needs_device_codec) B->snappy_list.push_back(my_index);
+    if (needs_device_codec) {
+      B->pages.back().sidx = (int32_t)B->snappy_list.size();
+      B->snappy_list.push_back(my_index);
+      // a data page whose body may wait on k_copy (literals >= 16 KiB are deferred)
+      if (d.kind != PAGE_DICT && body >= 16 * 1024) B->data_may_defer = true;
+    }
   }
   cp.levels = level_base;
   return 0;
@@ -1680,15 +1687,26 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.list = B->d_lists;
   a.nlist = ns;
   e |= pq_launch(0, &a, s);
-  e |= pq_launch(6, &a, s);  // k_copy: long literals, timed together with k_snappy
-  mark(false);
-  a.list = B->d_lists + ns;
-  a.nlist = nd;
-  e |= pq_launch(1, &a, s);
-  mark(false);
-  a.list = B->d_lists + ns + nd;
-  a.nlist = ndata;
-  e |= pq_launch(2, &a, s);  // (+ the run walk of tiled RLE_DICTIONARY pages)
+  // without BYTE_ARRAY dictionaries nothing k_prepare reads waits on k_copy
+  // except data pages with deferred literals: k_prepare runs beside the copies
+  // in one launch and those pages after it
+  const bool fused = nd == 0 && B->max_jobs > 0 && !B->seg_times;
+  if (fused) {
+    a.list = B->d_lists + ns + nd;
+    a.nlist = ndata;
+    e |= pq_launch(12, &a, s);  // k_prepare_copy (+ the run walk of tiled RLE_DICTIONARY pages)
+    if (B->data_may_defer) e |= pq_launch(11, &a, s);  // pages that waited on k_copy
+  } else {
+    e |= pq_launch(6, &a, s);  // k_copy: long literals, timed together with k_snappy
+    mark(false);
+    a.list = B->d_lists + ns;
+    a.nlist = nd;
+    e |= pq_launch(1, &a, s);
+    mark(false);
+    a.list = B->d_lists + ns + nd;
+    a.nlist = ndata;
+    e |= pq_launch(2, &a, s);  // (+ the run walk of tiled RLE_DICTIONARY pages)
+  }
   mark(false);
   if (B->any_count) e |= pq_launch(4, &a, s);  // scans only feed lists / strings
   mark(true);

@@ -499,9 +499,9 @@ constexpr int COPY_ITEMS = 4;     // work items per job slot and pass (64 KiB: a
 // Work item i = (job slot i / COPY_ITEMS, chunk i % COPY_ITEMS), grid-strided;
 // a job longer than COPY_ITEMS chunks is covered in passes.  Every load of a
 // chunk is issued before its stores.
-__global__ __launch_bounds__(256) void k_copy(KArgs a) {
+__device__ __forceinline__ void copy_items(const KArgs &a, uint32_t blk, uint32_t nblk) {
   const uint32_t items = a.copy_cnt[a.epoch & 1] * COPY_ITEMS;  // registered by k_snappy
-  for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
+  for (uint32_t it = blk; it < items; it += nblk) {
     const uint32_t c = it % COPY_ITEMS;
     const CopyJob job = a.jobs[a.copy_idx[it / COPY_ITEMS]];
     const int t = threadIdx.x;
@@ -542,6 +542,8 @@ __global__ __launch_bounds__(256) void k_copy(KArgs a) {
     }
   }
 }
+
+__global__ __launch_bounds__(256) void k_copy(KArgs a) { copy_items(a, blockIdx.x, gridDim.x); }
 
 // ===========================================================================
 // K2: dictionary pages (page_dict.go:30-64)
@@ -1024,17 +1026,19 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
 // ===========================================================================
 // K3: data page prepare
 // ===========================================================================
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_prepare(KArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t wl_bytes[4][1024];  // run walk: window bytes
-  __shared__ __attribute__((aligned(16))) uint16_t wl_nx[4][1024];    // run walk: chain table
-  const int wv = (int)ufirst(threadIdx.x >> 6);
-  const int gi = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
+// Page gi of the list.  mode -1: every page; 0: pages whose body does not
+// wait on k_copy (run beside it, k_prepare_copy); 1: only the pages that do.
+__device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lbytes, uint16_t *lnx, int mode) {
   if (gi >= a.nlist) return;
   const int lane = lane_id();
   const int page = ufirst(a.list[gi]);
   PSTAMP(page, 0, __builtin_amdgcn_s_memrealtime());
   const PageDesc d = a.pages[page];
   PageInfo *pi = &a.info[page];
+  if (mode >= 0) {
+    const bool waits = d.sidx >= 0 && a.njobs[d.sidx] > 0;  // deferred literals of this body
+    if (waits != (mode == 1)) return;
+  }
   if (page_status(a.status, page) != STATUS_OK) return;
   if (d.dict >= 0 && page_status(a.status, d.dict) != STATUS_OK) return;  // reported first anyway
   const ColDesc c = a.cols[d.col];
@@ -1121,7 +1125,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     }
     PSTAMP(page, 1, __builtin_amdgcn_s_memrealtime());
     const PageDesc dp = a.pages[d.dict];
-    walk_runs(a, d, pi, ps.body + ps.val_off + 1, ps.val_len - 1, d.num_values, idx_bw, wl_bytes[wv], wl_nx[wv],
+    walk_runs(a, d, pi, ps.body + ps.val_off + 1, ps.val_len - 1, d.num_values, idx_bw, lbytes, lnx,
               body_ptr(a, dp, d.dict), (uint32_t)dp.num_values);
     PSTAMP(page, 2, __builtin_amdgcn_s_memrealtime());
     PSTAMP(page, 4, (uint64_t)idx_bw);
@@ -1294,6 +1298,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     pi->non_null = nn;
     pi->str_bytes = sbytes;
   }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_prepare(KArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t wl_bytes[4][1024];  // run walk: window bytes
+  __shared__ __attribute__((aligned(16))) uint16_t wl_nx[4][1024];    // run walk: chain table
+  const int wv = (int)ufirst(threadIdx.x >> 6);
+  prepare_page(a, (int)blockIdx.x * 4 + wv, wl_bytes[wv], wl_nx[wv], MODE);
+}
+
+// k_prepare beside k_copy in one launch (batches without BYTE_ARRAY
+// dictionaries): the first blocks prepare every page whose body does not wait
+// on a deferred literal, the rest copy the deferred literals (mostly large
+// dictionaries, which k_prepare only points at).  Neither waits on the other;
+// pages that do wait are prepared by k_prepare<1> after this launch.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_prepare_copy(KArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t wl_bytes[4][1024];
+  __shared__ __attribute__((aligned(16))) uint16_t wl_nx[4][1024];
+  const uint32_t pb = ((uint32_t)a.nlist + 3) / 4;
+  if (blockIdx.x < pb) {
+    const int wv = (int)ufirst(threadIdx.x >> 6);
+    prepare_page(a, (int)blockIdx.x * 4 + wv, wl_bytes[wv], wl_nx[wv], 0);
+    return;
+  }
+  copy_items(a, blockIdx.x - pb, gridDim.x - pb);
 }
 
 // ===========================================================================
@@ -2659,6 +2688,14 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     hipLaunchKernelGGL(pq::k_scan, dim3(k.ncols), dim3(256), 0, s, k);
     return hipGetLastError() == hipSuccess ? 0 : 17;
   }
+  if (which == 12) {  // k_prepare_copy: the prepare blocks, then the copy grid
+    const uint32_t items = k.max_jobs * pq::COPY_ITEMS;
+    const uint32_t cb = items < 1024 ? items : 1024;
+    const uint32_t pb = ((uint32_t)(k.nlist > 0 ? k.nlist : 0) + 3) / 4;
+    if (pb + cb == 0) return 0;
+    hipLaunchKernelGGL(pq::k_prepare_copy, dim3(pb + (cb ? cb : 1)), dim3(256), 0, s, k);
+    return hipGetLastError() == hipSuccess ? 0 : 17;
+  }
   if (which == 6) {  // deferred literal copies: fixed grid, the job count lives on the device
     if (k.max_jobs == 0) return 0;
     const uint32_t items = k.max_jobs * pq::COPY_ITEMS;
@@ -2711,7 +2748,8 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
   switch (which) {
     case 0: hipLaunchKernelGGL(pq::k_snappy, grid, block, 0, s, k); break;
     case 1: hipLaunchKernelGGL(pq::k_dict_prepare, grid, block, 0, s, k); break;
-    case 2: hipLaunchKernelGGL(pq::k_prepare, grid, block, 0, s, k); break;
+    case 2: hipLaunchKernelGGL(pq::k_prepare<-1>, grid, block, 0, s, k); break;
+    case 11: hipLaunchKernelGGL(pq::k_prepare<1>, grid, block, 0, s, k); break;
     case 3: hipLaunchKernelGGL(pq::k_decode, grid, block, 0, s, k); break;
     case 5: hipLaunchKernelGGL(pq::k_level_check, grid, block, 0, s, k); break;
     case 10: hipLaunchKernelGGL(pq::k_dba, grid, block, 0, s, k); break;
