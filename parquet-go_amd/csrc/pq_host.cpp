@@ -7,6 +7,7 @@
 // readChunk/readPages page-header walk (chunk_reader.go:206-378).  Every byte
 // of page payload goes to HBM in one hipMemcpyAsync per batch; decompression
 // (Snappy) and all decoding run in pq_kernels.hip.
+#include <chrono>
 #include <errno.h>
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
@@ -473,8 +474,63 @@ struct pqg_ctx {
   hipStream_t stream = nullptr;
   hipStream_t side[3] = {nullptr, nullptr, nullptr};  // concurrent size-class decode launches
   hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr};
+  // pinned upload ring (allocated on first use): chunk bytes are copied into
+  // one buffer while the DMA of the previous one runs
+  static constexpr int kRingBufs = 4;
+  static constexpr size_t kRingBytes = 16u << 20;
+  void *pin[kRingBufs] = {};
+  hipEvent_t pin_ev[kRingBufs] = {};
   std::string err;
 };
+
+// host -> device upload of the input layout straight from the file's pages
+// through the context's pinned ring (each buffer filled while the DMA of the
+// previous one runs); alignment gaps are zeroed
+template <class Layout>
+static int ring_upload(pqg_ctx *c, uint8_t *dst, const Layout &in, hipStream_t s) {
+  const size_t n = in.n;
+  if (!c->pin[0]) {
+    for (int i = 0; i < pqg_ctx::kRingBufs; i++) {
+      if (hipHostMalloc(&c->pin[i], pqg_ctx::kRingBytes, hipHostMallocDefault) != hipSuccess ||
+          hipEventCreateWithFlags(&c->pin_ev[i], hipEventDisableTiming) != hipSuccess) {
+        c->pin[i] = nullptr;
+        for (const auto &r : in.ranges)  // pageable fallback
+          if (r.len && hipMemcpy(dst + r.off, r.src, r.len, hipMemcpyHostToDevice) != hipSuccess) return 1;
+        return 0;
+      }
+    }
+  }
+  size_t off = 0, ri = 0;
+  int k = 0;
+  bool used[pqg_ctx::kRingBufs] = {};
+  while (off < n) {
+    const size_t m = std::min(pqg_ctx::kRingBytes, n - off);
+    if (used[k] && hipEventSynchronize(c->pin_ev[k]) != hipSuccess) return 1;
+    // gather [off, off + m) of the layout into the pinned buffer
+    uint8_t *pb = (uint8_t *)c->pin[k];
+    size_t at = off;
+    while (at < off + m) {
+      while (ri < in.ranges.size() && in.ranges[ri].off + in.ranges[ri].len <= at) ri++;
+      const size_t next = ri < in.ranges.size() ? in.ranges[ri].off : n;
+      if (at < next) {  // alignment gap
+        const size_t z = std::min(next, off + m) - at;
+        memset(pb + (at - off), 0, z);
+        at += z;
+        continue;
+      }
+      const auto &r = in.ranges[ri];
+      const size_t z = std::min(r.off + r.len, off + m) - at;
+      memcpy(pb + (at - off), r.src + (at - r.off), z);
+      at += z;
+    }
+    if (hipMemcpyAsync(dst + off, c->pin[k], m, hipMemcpyHostToDevice, s) != hipSuccess) return 1;
+    hipEventRecord(c->pin_ev[k], s);
+    used[k] = true;
+    off += m;
+    k = (k + 1) % pqg_ctx::kRingBufs;
+  }
+  return hipStreamSynchronize(s) == hipSuccess ? 0 : 1;
+}
 
 struct pqg_file {
   const uint8_t *data = nullptr;
@@ -642,6 +698,10 @@ void pqg_ctx_destroy(pqg_ctx *ctx) {
     if (ctx->join[i]) hipEventDestroy(ctx->join[i]);
   }
   if (ctx->fork) hipEventDestroy(ctx->fork);
+  for (int i = 0; i < pqg_ctx::kRingBufs; i++) {
+    if (ctx->pin[i]) hipHostFree(ctx->pin[i]);
+    if (ctx->pin_ev[i]) hipEventDestroy(ctx->pin_ev[i]);
+  }
   delete ctx;
 }
 
@@ -983,12 +1043,17 @@ static int supported_encoding(int ptype, int enc) {
 }
 
 namespace {
-struct HostBuf {  // growable host staging for the input upload / host-inflated bodies
-  std::vector<uint8_t> v;
-  size_t append(const uint8_t *p, size_t n, size_t align = 16) {
-    size_t off = (v.size() + align - 1) & ~(align - 1);
-    v.resize(off + n);
-    if (n) memcpy(v.data() + off, p, n);
+struct HostBuf {  // the device input buffer's layout: byte ranges of the (mapped) file, 16-byte aligned
+  struct Range {
+    const uint8_t *src;
+    size_t off, len;
+  };
+  std::vector<Range> ranges;
+  size_t n = 0;
+  size_t append(const uint8_t *src, size_t k, size_t align = 16) {
+    const size_t off = (n + align - 1) & ~(align - 1);
+    ranges.push_back({src, off, k});
+    n = off + k;
     return off;
   }
 };
@@ -1265,6 +1330,15 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
     cp.levels = 0;
     B->cols.push_back(cp);
   }
+  // PQG_TRACE_CREATE=1: host time of each batch-creation phase on stderr
+  const bool trace = getenv("PQG_TRACE_CREATE") != nullptr;
+  auto t_last = std::chrono::steady_clock::now();
+  auto phase = [&](const char *what) {
+    if (!trace) return;
+    auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "pqg_batch_create %-14s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
+    t_last = t;
+  };
   HostBuf in;
   std::vector<std::pair<uint64_t, std::vector<uint8_t>>> host_bodies;
   int64_t stage_off = 0;
@@ -1431,9 +1505,10 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   B->tiles.insert(B->tiles.end(), ld_tiles.begin(), ld_tiles.end());
   B->ntiles_g = 0;  // every job runs in k_expand_mix
 
+  phase("plan");
   // device buffers
   int rc = 0;
-  size_t in_bytes = in.v.size();
+  size_t in_bytes = in.n;
   rc |= alloc_dev((void **)&B->d_in, in_bytes);
   rc |= alloc_dev((void **)&B->d_stage, (size_t)stage_off);
   rc |= alloc_dev((void **)&B->d_pages, sizeof(PageDesc) * npages);
@@ -1495,17 +1570,13 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
     set_err("hipHostMalloc failed");
     return PQG_ERR_DEVICE;
   }
+  phase("alloc");
   hipStream_t s = ctx->stream;
-  // one upload of all chunk bytes (pinned bounce for large inputs)
+  // one upload of all chunk bytes through the context's pinned ring
   {
-    void *pin = nullptr;
-    if (in_bytes && hipHostMalloc(&pin, in_bytes, hipHostMallocDefault) == hipSuccess) {
-      memcpy(pin, in.v.data(), in_bytes);
-      hipMemcpyAsync(B->d_in, pin, in_bytes, hipMemcpyHostToDevice, s);
-      hipStreamSynchronize(s);
-      hipHostFree(pin);
-    } else if (in_bytes) {
-      hipMemcpy(B->d_in, in.v.data(), in_bytes, hipMemcpyHostToDevice);
+    if (in_bytes && ring_upload(ctx, B->d_in, in, s)) {
+      set_err("input upload failed");
+      return PQG_ERR_DEVICE;
     }
     hipMemsetAsync(B->d_in + in_bytes, 0, kPad, s);
     B->h2d_bytes += (int64_t)in_bytes;
@@ -1527,6 +1598,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
     if (!lists.empty()) HIPCHK(hipMemcpy(B->d_lists, lists.data(), sizeof(int32_t) * lists.size(), hipMemcpyHostToDevice));
   }
   memcpy(B->h_status, B->status0.data(), sizeof(uint32_t) * npages);
+  phase("upload");
 
   // column descriptors (outputs allocated after the counting pass)
   B->hcols.resize(B->cols.size());
@@ -1623,6 +1695,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   for (int k = 0; k < pqg_batch::kRing; k++)
     for (int i = 0; i < 8; i++) hipEventCreate(&B->ev[k][i]);
   *out = B;
+  phase("outputs+tables");
   return PQG_OK;
 }
 
