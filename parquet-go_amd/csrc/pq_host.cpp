@@ -58,16 +58,13 @@ struct pq_launch_args {
   void *runs;
   void *tile_info;
   const void *tiles;
-  int32_t ntiles, ntiles4;
   int32_t ex_lds;
   void *recs;
   const int32_t *page_jobs;
   uint32_t epoch;
-  int32_t knob;
   const void *lgroups;
   int32_t ldn[6];   // k_expand_ld groups per (width 4, 8) x LDS class, in that order
   int32_t ldl[6];   // dynamic LDS bytes of each
-  int32_t ld_sel;   // the class pq_launch(9) launches (both widths)
 };
 int pq_launch(int which, const pq_launch_args *p, hipStream_t s);
 }
@@ -602,13 +599,11 @@ struct pqg_batch {
   void *d_runs = nullptr;        // run tables (k_prepare's run walk -> k_expand)
   void *d_tile_info = nullptr;     // per RUN_TILE values of a tiled page: {first run, first key byte}
   int32_t ex_lds = 0;              // k_expand staged key bytes per wave
-  int32_t ntiles4 = 0;             // k_expand jobs of 4-byte columns (they come first)
   void *d_recs = nullptr;          // k_expand job records (k_prepare writes them every decode)
   int32_t *d_page_jobs = nullptr;  // per tiled page: positions of its jobs in the launch order
   int64_t page_job_entries = 0;
   uint32_t epoch = 0;
   TileJob *d_tiles = nullptr;
-  int32_t ntiles_g = 0;              // k_expand jobs (the LDS-dictionary groups' jobs follow them)
   std::vector<LdsGroup> lgroups;     // k_expand_ld groups, 4-byte columns first
   LdsGroup *d_lgroups = nullptr;
   int32_t ldn[6] = {}, ldl[6] = {};  // groups and LDS bytes per (width 4, 8) x LDS class
@@ -1411,7 +1406,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   // Blocks are emitted in rounds of 8 (one per residue), global and LDS rounds
   // interleaved by job count so that L2-bound gathers and LDS-bound ones share
   // the machine for the whole launch.
-  B->ex_lds = (B->ex_lds + 1023) & ~1023;  // whole 1 KiB LDS-DMA chunks
+  B->ex_lds = (B->ex_lds + 255) & ~255;  // LDS-DMA pieces of 16 bytes per lane, the last one partial
   const bool ld_off = getenv("PQG_NO_LDS_DICT") != nullptr;
   std::vector<TileJob> slot_tiles, ld_tiles;
   const int64_t ld_max = getenv("PQG_LD_MAX_KB") ? 1024 * (int64_t)atoi(getenv("PQG_LD_MAX_KB")) : LD_MIX_MAX;
@@ -1431,7 +1426,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
         const int64_t dbytes = ((int64_t)std::max(B->pages[(size_t)ct[0].dict].num_values, 0) * W + 15) & ~15;
         int32_t ks = 0;
         for (const TileJob &tj : ct) ks = std::max(ks, page_need[(size_t)tj.page]);
-        ks = (ks + 1023) & ~1023;
+        ks = (ks + 255) & ~255;
         const int64_t J = (int64_t)ct.size();
         if (dbytes > 0 && ks > 0 && dbytes + (int64_t)LD_WAVES_H * ks <= ld_max &&
             dbytes * 4 <= J * EX_WAVE_VALUES * W) {
@@ -1503,7 +1498,6 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   }
   B->tiles = std::move(slot_tiles);
   B->tiles.insert(B->tiles.end(), ld_tiles.begin(), ld_tiles.end());
-  B->ntiles_g = 0;  // every job runs in k_expand_mix
 
   phase("plan");
   // device buffers
@@ -1737,10 +1731,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.recs = B->d_recs;
   a.page_jobs = B->d_page_jobs;
   a.epoch = ++B->epoch;
-  a.knob = getenv("PQG_KNOB") ? atoi(getenv("PQG_KNOB")) : 0;
   a.tiles = B->d_tiles;
-  a.ntiles = B->ntiles_g;
-  a.ntiles4 = B->ntiles4;
   a.lgroups = B->d_lgroups;
   for (int i = 0; i < 6; i++) {
     a.ldn[i] = B->ldn[i];
@@ -1793,7 +1784,6 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
       e |= pq_launch(10, &a, s);
     }
     a.nlist = (int32_t)B->tiles.size();
-    a.ld_sel = getenv("PQG_OLD_EXPAND") && getenv("PQG_NO_LDS_DICT") ? 1 : 0;
     e |= pq_launch(9, &a, s);  // k_expand_mix (tiled pages)
     mark(true);
     a.list = B->d_lists + ns + nd;

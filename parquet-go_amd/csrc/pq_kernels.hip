@@ -72,7 +72,6 @@ struct KArgs {
   ExRec *recs;            // k_prepare -> k_expand: one record per job (launch order)
   const int32_t *page_jobs;  // per tiled page (PageDesc.job_base): positions of its jobs
   uint32_t epoch;         // this decode's record epoch
-  int32_t knob;           // analysis only (PQG_KNOB): 1 no gathers, 2 no stores, 3 neither
   uint32_t *copy_cnt;     // deferred literals registered this decode: [epoch & 1] (the other is reset)
   int32_t *copy_idx;      // their job slots, compact (k_snappy -> k_copy)
   int32_t *lens;          // DELTA string pages: suffix lengths [0, nv), prefix lengths [nv, 2 nv)
@@ -2145,13 +2144,15 @@ __device__ __forceinline__ void expand_job(const KArgs &a, const TileJob &tj, co
   const int64_t nb = (int64_t)((uintptr_t)ks + (uintptr_t)byte_hi - A);
   const bool staged = nb <= ex_lds;
   if (staged) {
-    // LDS-DMA: lane l's 16 bytes of chunk i land at kspan + 1024 i + 16 l.  Bytes
-    // past the stream end are never used as key bits (fast rows stay inside it,
-    // the general path masks them), so they are staged as they are.
+    // LDS-DMA: lane l's 16 bytes of chunk i land at kspan + 1024 i + 16 l (the
+    // last chunk only as far as the span: kspan is sized in 256-byte steps).
+    // Bytes past the stream end are never used as key bits (fast rows stay
+    // inside it, the general path masks them), so they are staged as they are.
     const uintptr_t src = A + 16 * (uintptr_t)lane;
     for (int32_t off = 0; off < nb; off += 1024)
-      __builtin_amdgcn_global_load_lds((const void *)(src + off),
-                                       (__attribute__((address_space(3))) void *)(kspan + off / 4), 16, 0, 0);
+      if (off + 16 * lane < nb)
+        __builtin_amdgcn_global_load_lds((const void *)(src + off),
+                                         (__attribute__((address_space(3))) void *)(kspan + off / 4), 16, 0, 0);
   }
   // every run meeting [v0, lim) must sit in lanes 0..62 (its end is the next lane's start),
   // and no row of EX_ROW values may hold two run starts (rows meet at most two runs)
@@ -2167,10 +2168,6 @@ __device__ __forceinline__ void expand_job(const KArgs &a, const TileJob &tj, co
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the staged bytes (LDS-DMA) and the window
   STAMP(3);
-  if (a.knob == 4) {  // analysis: record + window + staging only
-    if (W.start == 0x7fffffe || kspan[lane] == 0x12345u) a.status[0] = 0;
-    return;
-  }
   const int64_t lbase = (int64_t)(A - (uintptr_t)ks) * 8;  // stream bit of kspan bit 0
   const int64_t end_bit = slen * 8;
   const uint32_t mask = bw >= 32 ? 0xffffffffu : ((1u << bw) - 1);
@@ -2335,11 +2332,6 @@ __device__ __forceinline__ void expand_job(const KArgs &a, const TileJob &tj, co
           if (WIDTH == 4) val[h][r][q] = sdict[key[r][q]];
           else val[h][r][q] = ((const uint64_t *)sdict)[key[r][q]];
         }
-    } else if (a.knob & 1) {
-#pragma unroll
-      for (int r = 0; r < HR; r++)
-#pragma unroll
-        for (int q = 0; q < 4; q++) val[h][r][q] = key[r][q];
     } else if (dsh == 0) {
 #pragma unroll
       for (int r = 0; r < HR; r++)
@@ -2371,17 +2363,6 @@ __device__ __forceinline__ void expand_job(const KArgs &a, const TileJob &tj, co
     }
   }
   STAMP(4);
-  if (a.knob & 2) {  // analysis: keep the values live, store one word
-    uint32_t acc = 0;
-#pragma unroll
-    for (int h = 0; h < 2; h++)
-#pragma unroll
-      for (int r = 0; r < HR; r++)
-#pragma unroll
-        for (int q = 0; q < 4; q++) acc ^= (uint32_t)val[h][r][q];
-    if (acc == 0x12345678u) __builtin_amdgcn_raw_buffer_store_b32(acc, ors, 0, 0, 0);
-    return;
-  }
   // 4. stores: 16 / 32 contiguous bytes per lane per row
   const bool out_al = ((uintptr_t)tj.out & 15) == 0;
 #pragma unroll
@@ -2419,22 +2400,6 @@ __device__ __forceinline__ void expand_job(const KArgs &a, const TileJob &tj, co
   STAMP(5);
 }
 
-template <int WIDTH>
-__global__ __launch_bounds__(256) void k_expand(KArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t kspan_dyn[];
-  STAMP(0);
-  const int wv = (int)ufirst(threadIdx.x >> 6);
-  const int job = (int)blockIdx.x * 4 + wv;
-  if (job >= a.nlist) return;
-  const TileJob tj = sload(a.tiles + job);
-  const ExRec rc = sload(a.recs + job);  // written by this decode's k_prepare, or stale (epoch)
-  if (rc.epoch != a.epoch) return;  // the page failed before k_prepare finished it
-  if (a.knob == 5) {  // analysis: record only
-    if (rc.v0 == 0x7fffffff) a.status[0] = 0;
-    return;
-  }
-  expand_job<WIDTH, false>(a, tj, rc, kspan_dyn + wv * (a.ex_lds / 4), a.ex_lds, nullptr);
-}
 
 
 // ===========================================================================
@@ -2634,16 +2599,13 @@ struct pq_launch_args {
   void *runs;
   void *tile_info;
   const void *tiles;
-  int32_t ntiles, ntiles4;  // k_expand jobs; the first ntiles4 are of 4-byte columns
   int32_t ex_lds;
   void *recs;
   const int32_t *page_jobs;
   uint32_t epoch;
-  int32_t knob;
   const void *lgroups;
   int32_t ldn[6];   // k_expand_mix blocks of 4-byte, 8-byte columns ([0], [1])
   int32_t ldl[6];   // their dynamic LDS bytes
-  int32_t ld_sel;
 };
 
 static pq::KArgs to_k(const pq_launch_args *p) {
@@ -2675,7 +2637,6 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   k.recs = (pq::ExRec *)p->recs;
   k.page_jobs = p->page_jobs;
   k.epoch = p->epoch;
-  k.knob = p->knob;
   k.tiles = (const pq::TileJob *)p->tiles;
   k.lgroups = (const pq::LdsGroup *)p->lgroups;
   return k;
@@ -2702,21 +2663,6 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     hipLaunchKernelGGL(pq::k_copy, dim3(items < 4096 ? items : 4096), dim3(256), 0, s, k);
     return hipGetLastError() == hipSuccess ? 0 : 17;
   }
-  if (which == 8) {  // k_expand: one workgroup per tile job
-    if (p->ntiles <= 0) return 0;
-    // jobs of 4-byte columns first, then 8-byte ones (p->ntiles4 of them first)
-    if (p->ntiles4 > 0) {
-      k.nlist = p->ntiles4;
-      hipLaunchKernelGGL(pq::k_expand<4>, dim3((p->ntiles4 + 3) / 4), dim3(256), (size_t)4 * p->ex_lds, s, k);
-    }
-    if (p->ntiles > p->ntiles4) {
-      k.tiles = (const pq::TileJob *)p->tiles + p->ntiles4;
-      k.recs = (pq::ExRec *)p->recs + p->ntiles4;
-      k.nlist = p->ntiles - p->ntiles4;
-      hipLaunchKernelGGL(pq::k_expand<8>, dim3((k.nlist + 3) / 4), dim3(256), (size_t)4 * p->ex_lds, s, k);
-    }
-    return hipGetLastError() == hipSuccess ? 0 : 17;
-  }
   if (which == 9) {  // k_expand_mix: one 512-thread workgroup per LdsGroup (absolute job indices)
     static bool attr = false;
     if (!attr) {
@@ -2725,15 +2671,6 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
       attr = true;
     }
     const dim3 blk(pq::LD_WAVES_H * 64);
-    if (p->ld_sel == 1) {  // analysis (PQG_OLD_EXPAND, no LDS groups): the one-job-per-wave kernel on the same slots
-      k.nlist = p->ldn[0] * pq::LD_WAVES_H;
-      if (p->ldn[0] > 0) hipLaunchKernelGGL(pq::k_expand<4>, dim3(p->ldn[0]), blk, (size_t)p->ldl[0], s, k);
-      k.tiles = (const pq::TileJob *)p->tiles + (size_t)p->ldn[0] * pq::LD_WAVES_H;
-      k.recs = (pq::ExRec *)p->recs + (size_t)p->ldn[0] * pq::LD_WAVES_H;
-      k.nlist = p->ldn[1] * pq::LD_WAVES_H;
-      if (p->ldn[1] > 0) hipLaunchKernelGGL(pq::k_expand<8>, dim3(p->ldn[1]), blk, (size_t)p->ldl[1], s, k);
-      return hipGetLastError() == hipSuccess ? 0 : 17;
-    }
     if (p->ldn[0] > 0) hipLaunchKernelGGL(pq::k_expand_mix<4>, dim3(p->ldn[0]), blk, (size_t)p->ldl[0], s, k);
     if (p->ldn[1] > 0) {
       k.lgroups = (const pq::LdsGroup *)p->lgroups + p->ldn[0];
