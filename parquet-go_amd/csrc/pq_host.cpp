@@ -1395,7 +1395,9 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   // 4-byte columns' jobs first (k_expand<4>), then 8-byte ones (k_expand<8>).
   // k_expand_mix blocks (512 threads, eight waves), per value width:
   //  * LDS groups: chunks whose dictionary fits in LDS beside four waves'
-  //    staged keys (within LD_MIX_MAX) and whose jobs amortise copying it
+  //    staged keys (within LD_MIX_MAX) and whose jobs amortise copying it;
+  //    groups are small (one job per wave unless the dictionary is large:
+  //    output >= 2 x dictionary), measured faster than longer-lived groups
   //    (the copy at most a quarter of the output) -> groups of consecutive jobs;
   //  * global blocks: every other job, one per wave, gathering through L1/L2.
   //    (Workgroups of four waves: a workgroup holds its slot until its last
@@ -1430,8 +1432,10 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
         const int64_t J = (int64_t)ct.size();
         if (dbytes > 0 && ks > 0 && dbytes + (int64_t)LD_WAVES_H * ks <= ld_max &&
             dbytes * 4 <= J * EX_WAVE_VALUES * W) {
-          int64_t G = (dbytes * 4 + (int64_t)EX_WAVE_VALUES * W - 1) / ((int64_t)EX_WAVE_VALUES * W);
-          G = std::min<int64_t>(std::max<int64_t>((G + LD_WAVES_H - 1) / LD_WAVES_H * LD_WAVES_H, 2 * LD_WAVES_H), 128);
+          const int64_t amort = getenv("PQG_LD_AMORT") ? atoi(getenv("PQG_LD_AMORT")) : 2;
+          int64_t G = (dbytes * amort + (int64_t)EX_WAVE_VALUES * W - 1) / ((int64_t)EX_WAVE_VALUES * W);
+          const int64_t gmin = getenv("PQG_LD_GMIN") ? atoi(getenv("PQG_LD_GMIN")) : LD_WAVES_H;
+          G = std::min<int64_t>(std::max<int64_t>((G + LD_WAVES_H - 1) / LD_WAVES_H * LD_WAVES_H, gmin), 128);
           const int64_t ng = (J + G - 1) / G;
           for (int64_t q = 0; q < ng; q++) ldg.push_back({&ct, q * J / ng, (q + 1) * J / ng, (int32_t)dbytes, ks});
           ld = true;

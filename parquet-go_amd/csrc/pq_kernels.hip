@@ -2431,26 +2431,60 @@ __device__ __forceinline__ void mix_global(const KArgs &a, const LdsGroup &g, ui
 template <int WIDTH>
 __device__ __forceinline__ void mix_lds(const KArgs &a, const LdsGroup &g, uint32_t *lds_dyn) {
   const int wv = (int)ufirst(threadIdx.x >> 6);
-  if (page_status(a.status, g.dpage) != STATUS_OK) return;  // no record of the chunk was written
-  const PageDesc dp = a.pages[g.dpage];
-  const uint8_t *dict = body_ptr(a, dp, g.dpage);
-  const uint32_t nbytes = min((uint32_t)max(dp.num_values, 0) * (uint32_t)WIDTH, (uint32_t)g.dict_bytes);
+  const int jend = g.job0 + g.njobs;
+  // the group's first record (its dictionary: pointer and size, written by this
+  // decode's k_prepare) and this wave's first job, loaded together
+  const ExRec r0 = sload(a.recs + g.job0);
+  int j = g.job0 + wv;
+  TileJob tj = {};
+  ExRec rc = {};
+  if (j < jend) {
+    tj = sload(a.tiles + j);
+    rc = sload(a.recs + j);
+  }
+  const uint8_t *dict;
+  uint32_t dn;
+  if (r0.epoch == a.epoch && r0.dict) {
+    dict = r0.dict;
+    dn = r0.dict_n;
+  } else {  // a failed or PLAIN first page: the dictionary page itself
+    if (page_status(a.status, g.dpage) != STATUS_OK) return;  // no record of the chunk was written
+    const PageDesc dp = a.pages[g.dpage];
+    dict = body_ptr(a, dp, g.dpage);
+    dn = (uint32_t)max(dp.num_values, 0);
+  }
+  const uint32_t nbytes = min(dn * (uint32_t)WIDTH, (uint32_t)g.dict_bytes);
   const uint32_t dsh = (uint32_t)((uintptr_t)dict & 3);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       (void *)((uintptr_t)dict & ~(uintptr_t)3), (short)0, (int)((nbytes + dsh + 3) & ~3u), 0x00020000);
   const uint32_t n16 = (nbytes + 15) / 16;
-  for (uint32_t i = threadIdx.x; i < n16; i += LD_WAVES * 64) {
-    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * i, 0, 0);
-    const uint32_t y = dsh ? __builtin_amdgcn_raw_buffer_load_b32(rs, 16 * i + 16, 0, 0) : 0u;
-    *(u32x4 *)(lds_dyn + 4 * i) =
-        u32x4{__builtin_amdgcn_alignbyte(x.y, x.x, dsh), __builtin_amdgcn_alignbyte(x.z, x.y, dsh),
-              __builtin_amdgcn_alignbyte(x.w, x.z, dsh), __builtin_amdgcn_alignbyte(y, x.w, dsh)};
+  // the copy: four 16-byte pieces per thread in flight at a time
+  constexpr uint32_t T = LD_WAVES * 64;
+  for (uint32_t i0 = threadIdx.x; i0 < n16; i0 += 4 * T) {
+    u32x4 x[4];
+    uint32_t y[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t i = i0 + q * T;
+      x[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * i, 0, 0);  // out of range: zeros
+      y[q] = dsh ? __builtin_amdgcn_raw_buffer_load_b32(rs, 16 * i + 16, 0, 0) : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t i = i0 + q * T;
+      if (i < n16)
+        *(u32x4 *)(lds_dyn + 4 * i) =
+            u32x4{__builtin_amdgcn_alignbyte(x[q].y, x[q].x, dsh), __builtin_amdgcn_alignbyte(x[q].z, x[q].y, dsh),
+                  __builtin_amdgcn_alignbyte(x[q].w, x[q].z, dsh), __builtin_amdgcn_alignbyte(y[q], x[q].w, dsh)};
+    }
   }
   __syncthreads();
   uint32_t *kspan = lds_dyn + g.dict_bytes / 4 + wv * (g.kspan / 4);
-  for (int j = g.job0 + wv; j < g.job0 + g.njobs; j += LD_WAVES) {
-    const TileJob tj = sload(a.tiles + j);
-    const ExRec rc = sload(a.recs + j);
+  for (; j < jend; j += LD_WAVES) {
+    if (j != g.job0 + wv) {
+      tj = sload(a.tiles + j);
+      rc = sload(a.recs + j);
+    }
     if (rc.epoch != a.epoch) continue;  // the page failed before k_prepare finished it
     expand_job<WIDTH, true>(a, tj, rc, kspan, g.kspan, lds_dyn);
   }
@@ -2459,9 +2493,16 @@ __device__ __forceinline__ void mix_lds(const KArgs &a, const LdsGroup &g, uint3
 template <int WIDTH>
 __global__ __launch_bounds__(LD_WAVES_H * 64) void k_expand_mix(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
+  STAMP(0);
   const LdsGroup g = sload(a.lgroups + blockIdx.x);
   if (g.dpage < 0) mix_global<WIDTH>(a, g, lds_dyn);
   else mix_lds<WIDTH>(a, g, lds_dyn);
+#ifdef PQ_STAMPS
+  if (a.dbg && lane_id() == 0) {  // block kind and the wave's end
+    a.dbg[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + 6] = g.dpage >= 0 ? 1 : 2;
+    a.dbg[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }
 
 // ===========================================================================
