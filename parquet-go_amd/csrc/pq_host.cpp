@@ -1458,8 +1458,12 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
     const TileJob none = {nullptr, -1, -1, 0, 0, 0, 0};
     while (gr < ngr || lr < nlr) {
       // the round kind that is behind in its share of the jobs goes next
-      const bool take_g = lr >= nlr || (gr < ngr && (double)gdone * (double)std::max<size_t>(ljobs, 1) <=
-                                                        (double)ldone * (double)std::max<size_t>(gjobs, 1));
+      // (PQG_MIX_ORDER, analysis: 1 L1/L2 rounds first, 2 LDS rounds first)
+      static const int mix_order = getenv("PQG_MIX_ORDER") ? atoi(getenv("PQG_MIX_ORDER")) : 0;
+      bool take_g = lr >= nlr || (gr < ngr && (double)gdone * (double)std::max<size_t>(ljobs, 1) <=
+                                                  (double)ldone * (double)std::max<size_t>(gjobs, 1));
+      if (mix_order == 1) take_g = gr < ngr;
+      if (mix_order == 2) take_g = lr >= nlr;
       for (size_t q = 0; q < 8; q++) {
         // every block owns LD_WAVES_H job slots (wave w: slot 4 b + w), so a
         // global block's waves load their jobs without waiting for the block's
