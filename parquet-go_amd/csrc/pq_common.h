@@ -77,6 +77,12 @@ struct PageDesc {
 // workgroup takes 4 waves x EX_WAVE_VALUES consecutive values of one page.
 constexpr int RUN_TILE = 512;
 constexpr int EX_WAVE_VALUES = 2048;
+// k_reset: a device buffer zeroed at the start of every decode
+struct ZeroRange {
+  uint32_t *ptr;
+  uint64_t words;
+};
+
 // k_expand_ld: one workgroup per group of consecutive jobs of one column
 // chunk, whose dictionary it holds in LDS (host-built)
 constexpr int LD_WAVES_H = 4;             // waves of a k_expand_mix workgroup

@@ -65,6 +65,9 @@ struct pq_launch_args {
   const void *lgroups;
   int32_t ldn[6];   // k_expand_ld groups per (width 4, 8) x LDS class, in that order
   int32_t ldl[6];   // dynamic LDS bytes of each
+  const uint32_t *status0;
+  const void *zr;
+  int32_t nzr, npages;
 };
 int pq_launch(int which, const pq_launch_args *p, hipStream_t s);
 }
@@ -583,6 +586,9 @@ struct pqg_batch {
   PageDesc *d_pages = nullptr;
   PageInfo *d_info = nullptr;
   uint32_t *d_status = nullptr;
+  uint32_t *d_status0 = nullptr;  // initial statuses (k_reset copies them in every decode)
+  void *d_zr = nullptr;           // ZeroRange table of the validity bitmaps
+  int32_t nzr = 0;
   ColDesc *d_cols = nullptr;
   uint64_t *d_dict = nullptr;
   int32_t *d_lists = nullptr;
@@ -1516,6 +1522,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   rc |= alloc_dev((void **)&B->d_pages, sizeof(PageDesc) * npages);
   rc |= alloc_dev((void **)&B->d_info, sizeof(PageInfo) * npages);
   rc |= alloc_dev((void **)&B->d_status, sizeof(uint32_t) * npages);
+  rc |= alloc_dev((void **)&B->d_status0, sizeof(uint32_t) * npages);
   rc |= alloc_dev((void **)&B->d_cols, sizeof(ColDesc) * B->cols.size());
   rc |= alloc_dev((void **)&B->d_dict, sizeof(uint64_t) * (size_t)B->dict_entries);
   size_t nl = B->snappy_list.size() + B->dict_list.size() + 3 * B->data_list.size() + 16;
@@ -1600,6 +1607,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
     if (!lists.empty()) HIPCHK(hipMemcpy(B->d_lists, lists.data(), sizeof(int32_t) * lists.size(), hipMemcpyHostToDevice));
   }
   memcpy(B->h_status, B->status0.data(), sizeof(uint32_t) * npages);
+  if (npages) HIPCHK(hipMemcpy(B->d_status0, B->status0.data(), sizeof(uint32_t) * npages, hipMemcpyHostToDevice));
   phase("upload");
 
   // column descriptors (outputs allocated after the counting pass)
@@ -1697,6 +1705,21 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   for (int k = 0; k < pqg_batch::kRing; k++)
     for (int i = 0; i < 8; i++) hipEventCreate(&B->ev[k][i]);
   *out = B;
+  {  // the validity bitmaps k_reset zeroes in every decode
+    std::vector<ZeroRange> zr;
+    for (auto &cp : B->cols) {
+      if (cp.validity) zr.push_back({(uint32_t *)cp.validity, cp.validity_bytes / 4});
+      if (cp.list_validity) zr.push_back({(uint32_t *)cp.list_validity, cp.list_val_bytes / 4});
+    }
+    B->nzr = (int32_t)zr.size();
+    if (!zr.empty()) {
+      if (alloc_dev(&B->d_zr, sizeof(ZeroRange) * zr.size())) {
+        set_err("device allocation failed");
+        return PQG_ERR_DEVICE;
+      }
+      HIPCHK(hipMemcpy(B->d_zr, zr.data(), sizeof(ZeroRange) * zr.size(), hipMemcpyHostToDevice));
+    }
+  }
   phase("outputs+tables");
   return PQG_OK;
 }
@@ -1704,15 +1727,6 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
 static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   hipStream_t s = B->ctx->stream;
   const size_t npages = B->pages.size();
-  if (npages) {
-    HIPCHK(hipMemcpyAsync(B->d_status, B->h_status, sizeof(uint32_t) * npages, hipMemcpyHostToDevice, s));
-  }
-  if (!upto_scan) {
-    for (auto &cp : B->cols) {
-      if (cp.validity) HIPCHK(hipMemsetAsync(cp.validity, 0, cp.validity_bytes, s));
-      if (cp.list_validity) HIPCHK(hipMemsetAsync(cp.list_validity, 0, cp.list_val_bytes, s));
-    }
-  }
   pq_launch_args a = {};
   a.in = B->d_in;
   a.stage = B->d_stage;
@@ -1730,6 +1744,10 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.copy_cnt = B->d_copy_cnt;
   a.copy_idx = B->d_copy_idx;
   a.lens = B->d_lens;
+  a.status0 = B->d_status0;
+  a.zr = B->d_zr;
+  a.nzr = upto_scan ? 0 : B->nzr;  // the bitmaps are written by the decode kernels only
+  a.npages = (int32_t)npages;
   a.dbg = B->d_dbg;
   a.dbg2 = B->d_dbg2;
   a.npages_dbg = (int32_t)B->pages.size() + 1;
@@ -1748,6 +1766,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   const int32_t ns = (int32_t)B->snappy_list.size(), nd = (int32_t)B->dict_list.size(),
                 ndata = (int32_t)B->data_list.size(), ngen = (int32_t)B->general_list.size();
   int e = 0;
+  if (npages || a.nzr) e |= pq_launch(13, &a, s);  // k_reset: statuses and validity bitmaps
   if (timed) B->nev = 0;  // an untimed decode keeps the last timed segment count
   hipEvent_t *evs = B->ev[B->ring_head];
   // events cost a gap between dependent kernels: by default only the decode
@@ -2008,6 +2027,8 @@ void pqg_batch_destroy(pqg_batch *B) {
   hipFree(B->d_job_base);
   hipFree(B->d_job_owner);
   hipFree(B->d_copy_cnt);
+  hipFree(B->d_status0);
+  hipFree(B->d_zr);
   hipFree(B->d_copy_idx);
   hipFree(B->d_lens);
   hipFree(B->d_dbg);

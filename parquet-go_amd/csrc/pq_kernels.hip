@@ -75,6 +75,9 @@ struct KArgs {
   uint32_t *copy_cnt;     // deferred literals registered this decode: [epoch & 1] (the other is reset)
   int32_t *copy_idx;      // their job slots, compact (k_snappy -> k_copy)
   int32_t *lens;          // DELTA string pages: suffix lengths [0, nv), prefix lengths [nv, 2 nv)
+  const uint32_t *status0;  // k_reset: every page's initial status (host planning errors)
+  const ZeroRange *zr;      // k_reset: buffers zeroed per decode (validity bitmaps)
+  int32_t nzr, npages;
   const TileJob *tiles;   // k_expand: one workgroup per entry
   const LdsGroup *lgroups;  // k_expand_ld: one workgroup per entry
 };
@@ -543,6 +546,21 @@ __device__ __forceinline__ void copy_items(const KArgs &a, uint32_t blk, uint32_
 }
 
 __global__ __launch_bounds__(256) void k_copy(KArgs a) { copy_items(a, blockIdx.x, gridDim.x); }
+
+// ===========================================================================
+// K0: start of a decode — every page's status back to its host-planned value
+// (blockIdx.y == 0) and the validity bitmaps zeroed (blockIdx.y == 1 + range),
+// one launch instead of a status upload and a memset per bitmap
+// ===========================================================================
+__global__ __launch_bounds__(256) void k_reset(KArgs a) {
+  const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x, stride = (uint64_t)gridDim.x * 256;
+  if (blockIdx.y == 0) {
+    for (uint64_t i = t; i < (uint64_t)a.npages; i += stride) a.status[i] = a.status0[i];
+    return;
+  }
+  const ZeroRange z = a.zr[blockIdx.y - 1];
+  for (uint64_t i = t; i < z.words; i += stride) z.ptr[i] = 0u;
+}
 
 // ===========================================================================
 // K2: dictionary pages (page_dict.go:30-64)
@@ -2647,6 +2665,9 @@ struct pq_launch_args {
   const void *lgroups;
   int32_t ldn[6];   // k_expand_mix blocks of 4-byte, 8-byte columns ([0], [1])
   int32_t ldl[6];   // their dynamic LDS bytes
+  const uint32_t *status0;
+  const void *zr;
+  int32_t nzr, npages;
 };
 
 static pq::KArgs to_k(const pq_launch_args *p) {
@@ -2669,6 +2690,10 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   k.copy_cnt = p->copy_cnt;
   k.copy_idx = p->copy_idx;
   k.lens = p->lens;
+  k.status0 = p->status0;
+  k.zr = (const pq::ZeroRange *)p->zr;
+  k.nzr = p->nzr;
+  k.npages = p->npages;
   k.dbg = p->dbg;
   k.dbg2 = p->dbg2;
   k.dbg3 = p->dbg2 ? p->dbg2 + 8 * (size_t)p->npages_dbg : nullptr;
@@ -2688,6 +2713,10 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
   if (which == 4) {
     if (k.ncols <= 0) return 0;
     hipLaunchKernelGGL(pq::k_scan, dim3(k.ncols), dim3(256), 0, s, k);
+    return hipGetLastError() == hipSuccess ? 0 : 17;
+  }
+  if (which == 13) {  // k_reset
+    hipLaunchKernelGGL(pq::k_reset, dim3(64, 1 + (k.nzr > 0 ? k.nzr : 0)), dim3(256), 0, s, k);
     return hipGetLastError() == hipSuccess ? 0 : 17;
   }
   if (which == 12) {  // k_prepare_copy: the prepare blocks, then the copy grid
