@@ -8,6 +8,9 @@ data (seeded), written with pyarrow on the box, then planned on the host and
 uploaded to HBM once; the timed region is the whole GPU decode pipeline
 (snappy -> prepare -> scan -> decode) with every page already resident.
 
+`--config c1|c3|c4|c5` runs the other BASELINE.json configs through the same
+pipeline (analysis lines; tools/synth.py describes their files).
+
 A "step" decodes every page of the rank's shard once.  For N > 1 the file holds
 N x 100M rows and each rank decodes a contiguous, byte-balanced slice of its
 row groups (pqgpu.plan_row_group_shards) on its own GPU: weak scaling, no
@@ -27,32 +30,14 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "parquet-go_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import synth  # noqa: E402  (tools/synth.py: the configs' synthetic files)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def make_file(path, rows, rg_rows, seed=2, fixed_bw=0):
-    import pyarrow as pa
-    import pyarrow.parquet as pq
-    rng = np.random.default_rng(seed)
-    schema = pa.schema([pa.field("v", pa.int32(), nullable=False)])
-    tmp = path + ".tmp%d" % os.getpid()
-    with pq.ParquetWriter(tmp, schema, compression="snappy", use_dictionary=True, data_page_version="1.0",
-                          dictionary_pagesize_limit=1 << 30) as w:
-        done, i = 0, 0
-        while done < rows:
-            n = min(rg_rows, rows - done)
-            bw = fixed_bw if fixed_bw else 1 + (i % 20)
-            K = 1 << bw
-            dvals = (rng.permutation(K).astype(np.int64) * 2654435761 % (1 << 32) - (1 << 31)).astype(np.int32)
-            idx = rng.integers(0, K, n)
-            w.write_table(pa.table({"v": pa.array(dvals[idx])}, schema=schema), row_group_size=n)
-            done += n
-            i += 1
-    os.replace(tmp, path)
-
-
-def cpu_baseline(path, budget_s=10.0, threads=None):
+def cpu_baseline(path, budget_s=10.0, threads=None, min_s=1.0):
     """The CPU oracle (a C port of the reference read path) on a bounded sample
     of the same file: whole row groups, one per worker thread at a time (the
     oracle releases the GIL inside its C calls), until ~budget_s of wall time.
@@ -65,33 +50,45 @@ def cpu_baseline(path, budget_s=10.0, threads=None):
     L = oracle.lib()
     threads = threads or min(16, os.cpu_count() or 1)
 
+    leaves = range(len(f.leaves()))
+
     def one(rg):
-        r = ctypes.c_void_p()
-        st = L.pqref_decode(f._h, 0, rg, rg + 1, ctypes.byref(r))
-        if st != 0:
-            raise RuntimeError("oracle failed on the bench file: %d" % st)
-        n = L.pqref_result_count(r, oracle.CNT_SLOTS)
-        L.pqref_result_free(r)
-        return n
+        # every selected leaf of the row group; output bytes as the GPU counts
+        # them (values + validity + list offsets/validity + string offsets)
+        nbytes, rows = 0, f.rg_num_rows(rg)
+        for leaf in leaves:
+            r = ctypes.c_void_p()
+            st = L.pqref_decode(f._h, leaf, rg, rg + 1, ctypes.byref(r))
+            if st != 0:
+                raise RuntimeError("oracle failed on the bench file: %d" % st)
+            for bid in (oracle.BUF_VALUES, oracle.BUF_VALIDITY, oracle.BUF_LIST_OFFSETS,
+                        oracle.BUF_LIST_VALIDITY, oracle.BUF_STR_OFFSETS):
+                n = ctypes.c_size_t()
+                L.pqref_result_buffer(r, bid, ctypes.byref(n))
+                nbytes += n.value
+            L.pqref_result_free(r)
+        return nbytes, rows
 
     out_bytes, rows, rgs = 0, 0, 0
     t0 = time.perf_counter()
     with cf.ThreadPoolExecutor(threads) as ex:
         rg = 0
-        while rg < f.num_row_groups and time.perf_counter() - t0 < budget_s:
-            wave = list(range(rg, min(rg + threads, f.num_row_groups)))
-            for n in ex.map(one, wave):
-                out_bytes += n * 4
-                rows += n
+        # whole passes over the file until ~min_s of wall (>= min_s x threads
+        # CPU-seconds), stopping early at budget_s
+        while time.perf_counter() - t0 < budget_s and (rg < f.num_row_groups or time.perf_counter() - t0 < min_s):
+            wave = [(rg + k) % f.num_row_groups for k in range(min(threads, f.num_row_groups))]
+            for nb, nr in ex.map(one, wave):
+                out_bytes += nb
+                rows += nr
             rgs += len(wave)
             rg += len(wave)
     t_total = time.perf_counter() - t0
     return {"value": out_bytes / t_total / 1e9, "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": "oracle/pqref.c on %d threads, %d of %d row groups (%d rows) of the bench file, %.1f s wall"
+            "sample": "oracle/pqref.c on %d threads, %d row-group decodes over the file's %d row groups (%d rows), %.1f s wall"
                       % (threads, rgs, f.num_row_groups, rows, t_total)}
 
 
-def pmc_traffic(args, kernels=("k_expand", "k_decode")):
+def pmc_traffic(args, kernels=("k_expand", "k_decode", "k_dba")):
     """HBM bytes per launch of the decode phase from rocprofv3 PMC counters,
     collected in separate passes (FETCH_SIZE, then WRITE_SIZE) over a short
     child run of this same bench; MI355X_MICROARCH.md: on gfx950 FETCH_SIZE
@@ -105,7 +102,7 @@ def pmc_traffic(args, kernels=("k_expand", "k_decode")):
     if not shutil.which("rocprofv3"):
         return None
     base = [sys.executable, os.path.abspath(__file__), "--no-cpu", "--no-pmc", "--steps", "3", "--warmup", "1",
-            "--rows", str(args.rows), "--rg-rows", str(args.rg_rows), "--bw", str(args.bw)]
+            "--config", args.config, "--rows", str(args.rows), "--rg-rows", str(args.rg_rows), "--bw", str(args.bw)]
     if args.file:
         base += ["--file", args.file]
     per = {}
@@ -139,14 +136,17 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=int, default=100_000_000)
-    ap.add_argument("--rg-rows", type=int, default=1 << 20)
+    ap.add_argument("--config", default="c2", choices=sorted(synth.DEFAULTS))
+    ap.add_argument("--rows", type=int, default=0, help="rows per GPU (default: the config's)")
+    ap.add_argument("--rg-rows", type=int, default=0, help="rows per row group (default: the config's)")
     ap.add_argument("--file", default=None)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes behind roofline.traffic")
     ap.add_argument("--bw", type=int, default=0, help="analysis: one dictionary bit width for every row group")
     args = ap.parse_args()
+    args.rows = args.rows or synth.DEFAULTS[args.config][0]
+    args.rg_rows = args.rg_rows or synth.DEFAULTS[args.config][1]
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -165,9 +165,9 @@ def main():
     import pqgpu
     total_rows = args.rows * world
     path = args.file or os.path.join(os.environ.get("TMPDIR", "/tmp"),
-                                     "pqgpu_bench_c2_%d_%d_%d.parquet" % (total_rows, args.rg_rows, args.bw))
+                                     "pqgpu_bench_%s_%d_%d_%d.parquet" % (args.config, total_rows, args.rg_rows, args.bw))
     if local == 0 and not os.path.exists(path):
-        make_file(path, total_rows, args.rg_rows, fixed_bw=args.bw)
+        synth.make(args.config, path, total_rows, args.rg_rows, fixed_bw=args.bw)
     barrier()
 
     ctx = pqgpu.Context(local if world > 1 else 0)
@@ -234,10 +234,9 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "int32",
-        "data": "synthetic (seeded pyarrow writer: dictionary INT32, bit widths 1-20 across row groups, snappy, V1)",
-        "config": {"workload": "C2: INT32 RLE_DICTIONARY bw 1-20, Snappy, V1, %d rows, %d-row row groups"
-                               % (args.rows, args.rg_rows),
+        "dtype": synth.DTYPE[args.config],
+        "data": "synthetic (seeded pyarrow writer on the box, tools/synth.py %s)" % args.config,
+        "config": {"workload": synth.DESCR[args.config] % (args.rows, args.rg_rows),
                    "rows_per_gpu": args.rows, "row_groups": [rg0, rg1],
                    "pages": stats["data_pages"], "dict_pages": stats["dict_pages"],
                    "B_in": in_b, "B_out": out_b, "staged": stats["staged_bytes"],
