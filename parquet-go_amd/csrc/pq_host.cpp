@@ -68,6 +68,7 @@ struct pq_launch_args {
   const uint32_t *status0;
   const void *zr;
   int32_t nzr, npages;
+  const uint8_t *in_end, *stage_end;  // allocation ends (incl. pad): bounds of the guarded debug build
 };
 int pq_launch(int which, const pq_launch_args *p, hipStream_t s);
 }
@@ -583,6 +584,7 @@ struct pqg_batch {
   int64_t input_bytes = 0, staged_bytes = 0, h2d_bytes = 0, host_inflated = 0, dict_entries = 0;
   // device
   uint8_t *d_in = nullptr, *d_stage = nullptr;
+  size_t in_alloc = 0, stage_alloc = 0;  // bytes incl. pad
   PageDesc *d_pages = nullptr;
   PageInfo *d_info = nullptr;
   uint32_t *d_status = nullptr;
@@ -1519,6 +1521,8 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   size_t in_bytes = in.n;
   rc |= alloc_dev((void **)&B->d_in, in_bytes);
   rc |= alloc_dev((void **)&B->d_stage, (size_t)stage_off);
+  B->in_alloc = in_bytes + kPad;
+  B->stage_alloc = (size_t)stage_off + kPad;
   rc |= alloc_dev((void **)&B->d_pages, sizeof(PageDesc) * npages);
   rc |= alloc_dev((void **)&B->d_info, sizeof(PageInfo) * npages);
   rc |= alloc_dev((void **)&B->d_status, sizeof(uint32_t) * npages);
@@ -1629,6 +1633,9 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   const bool any_count = B->any_count;
   if (!B->cols.empty())
     HIPCHK(hipMemcpy(B->d_cols, B->hcols.data(), sizeof(ColDesc) * B->cols.size(), hipMemcpyHostToDevice));
+  // the set-up copies and memsets above ran on the null stream, which the
+  // non-blocking context stream does not wait for
+  HIPCHK(hipDeviceSynchronize());
   if (any_count) {
     // counting pass: snappy + prepare + scan once to size list/string outputs
     rc = launch_all(B, true, false);
@@ -1720,6 +1727,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
       HIPCHK(hipMemcpy(B->d_zr, zr.data(), sizeof(ZeroRange) * zr.size(), hipMemcpyHostToDevice));
     }
   }
+  HIPCHK(hipDeviceSynchronize());  // null-stream set-up done before the first decode on the context stream
   phase("outputs+tables");
   return PQG_OK;
 }
@@ -1730,6 +1738,8 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   pq_launch_args a = {};
   a.in = B->d_in;
   a.stage = B->d_stage;
+  a.in_end = B->d_in + B->in_alloc;
+  a.stage_end = B->d_stage + B->stage_alloc;
   a.pages = B->d_pages;
   a.info = B->d_info;
   a.status = B->d_status;
@@ -2074,12 +2084,13 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
   int32_t *d_ci = nullptr;
   rc |= alloc_dev((void **)&d_cc, 16);
   rc |= alloc_dev((void **)&d_ci, 4 * (size_t)(max_jobs + 1));
-  if (!rc) hipMemset(d_cc, 0, 16);
+  if (!rc) hipMemsetAsync(d_cc, 0, 16, s);
   if (!rc) {
     int32_t zero4[4] = {0, 0, 0, 0};
-    hipMemcpy(d_jb, zero4, 16, hipMemcpyHostToDevice);
+    hipMemcpyAsync(d_jb, zero4, 16, hipMemcpyHostToDevice, s);
     std::vector<int32_t> owners(max_jobs + 1, 0);
-    hipMemcpy(d_jo, owners.data(), 4 * owners.size(), hipMemcpyHostToDevice);
+    hipMemcpyAsync(d_jo, owners.data(), 4 * owners.size(), hipMemcpyHostToDevice, s);
+    hipStreamSynchronize(s);  // host sources go out of scope
   }
   if (!rc) {
     PageDesc d;
@@ -2090,14 +2101,16 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
     d.body_src = BODY_SNAPPY;
     uint32_t st = STATUS_OK;
     int32_t zero = 0;
-    hipMemcpy(d_in, src, n, hipMemcpyHostToDevice);
-    hipMemcpy(d_page, &d, sizeof(d), hipMemcpyHostToDevice);
-    hipMemcpy(d_st, &st, 4, hipMemcpyHostToDevice);
-    hipMemcpy(d_list, &zero, 4, hipMemcpyHostToDevice);
+    hipMemcpyAsync(d_in, src, n, hipMemcpyHostToDevice, s);
+    hipMemcpyAsync(d_page, &d, sizeof(d), hipMemcpyHostToDevice, s);
+    hipMemcpyAsync(d_st, &st, 4, hipMemcpyHostToDevice, s);
+    hipMemcpyAsync(d_list, &zero, 4, hipMemcpyHostToDevice, s);
     pq_launch_args a = {};
     memset(&a, 0, sizeof(a));
     a.in = d_in;
     a.stage = d_out;
+    a.in_end = d_in + n + kPad;
+    a.stage_end = d_out + expect + kPad;
     a.pages = d_page;
     a.status = d_st;
     a.list = d_list;
@@ -2112,19 +2125,29 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
     a.dbg = nullptr;
     PageInfo *d_info = nullptr;
     rc |= alloc_dev((void **)&d_info, sizeof(PageInfo));
-    hipMemset(d_info, 0, sizeof(PageInfo));
+    hipMemsetAsync(d_info, 0, sizeof(PageInfo), s);
     a.info = d_info;
+    hipDeviceSynchronize();  // null-stream set-up before the launches on the non-blocking stream
     rc |= pq_launch(0, &a, s);
     rc |= pq_launch(6, &a, s);
-    hipStreamSynchronize(s);
+    const hipError_t e1 = hipStreamSynchronize(s);
+    if (e1 != hipSuccess) {
+      set_err("HIP error %s in the snappy kernels", hipGetErrorString(e1));
+      rc |= PQG_ERR_DEVICE;
+    }
     PageInfo hi;
-    hipMemcpy(&hi, d_info, sizeof(hi), hipMemcpyDeviceToHost);
-    if (hi.alias1 && expect) hipMemcpy(d_out, d_in + (hi.alias1 - 1), expect, hipMemcpyDeviceToDevice);
+    hipMemcpyAsync(&hi, d_info, sizeof(hi), hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    if (hi.alias1 && expect) hipMemcpyAsync(d_out, d_in + (hi.alias1 - 1), expect, hipMemcpyDeviceToDevice, s);
     hipFree(d_info);
     hipStreamSynchronize(s);
-    hipMemcpy(&st, d_st, 4, hipMemcpyDeviceToHost);
+    hipMemcpyAsync(&st, d_st, 4, hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
     *code = st == STATUS_OK ? 0 : (int)(st & 0xffff);
-    if (!*code && expect) hipMemcpy(dst, d_out, expect, hipMemcpyDeviceToHost);
+    if (!*code && expect) {
+      hipMemcpyAsync(dst, d_out, expect, hipMemcpyDeviceToHost, s);
+      hipStreamSynchronize(s);
+    }
   }
   hipFree(d_in);
   hipFree(d_out);
@@ -2138,7 +2161,7 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
   hipFree(d_jb);
   hipFree(d_jo);
   if (rc) {
-    set_err("device snappy failed");
+    if (g_err.empty()) set_err("device snappy failed");
     return PQG_ERR_DEVICE;
   }
   return PQG_OK;

@@ -80,6 +80,7 @@ struct KArgs {
   int32_t nzr, npages;
   const TileJob *tiles;   // k_expand: one workgroup per entry
   const LdsGroup *lgroups;  // k_expand_ld: one workgroup per entry
+  const uint8_t *in_end, *stage_end;  // allocation ends (PQ_SNAP_GUARD build)
 };
 
 #ifdef PQ_STAMPS
@@ -241,8 +242,278 @@ __device__ __forceinline__ void ring_fill(const uint8_t *s, int64_t dpos, int64_
 constexpr int64_t BIG_LITERAL = 16 * 1024;  // longer literals are copied by k_copy (many workgroups)
 constexpr int MAX_DEFER = 64;  // one entry per lane
 
+// ---- batched short tokens --------------------------------------------------
+// A run of copies and short literals (the body of a compressible block) is
+// decoded SB_TOK tokens at a time instead of one token per wave iteration:
+//  1. 512 compressed bytes are staged in LDS; each lane classifies the 4 tag
+//     positions it holds (token size + output length, 16 bits each);
+//  2. the token chain is walked on the scalar unit (two v_readlane per hop),
+//     token k's position written to lane k;
+//  3. lane k decodes token k, checks it (decode_other.go:14-101 order: header
+//     inside src, literal/copy length <= remaining dst, 0 < offset <= d) and an
+//     exclusive scan gives every token's output position;
+//  4. every output byte of the batch is resolved by its own lane: the byte's
+//     token comes from a token-start bitmap (+ per-word prefix counts); a copy
+//     byte maps to dst[start - offset + (r mod offset)] and is chased back
+//     until it lands in a literal or before the batch (LDS history, or the
+//     staged output / a deferred literal's payload when older than RING);
+//  5. the bytes enter the history; whole 16-byte chunks go to HBM.
+constexpr int SB_TOK = 64;    // tokens per batch (one per lane)
+constexpr int SB_OUT = 1024;  // output bytes per batch (token-start bitmap: 32 words)
+constexpr int SB_WIN = 512;   // compressed bytes staged per batch (walk covers the first 256)
+
+struct SnapLds {  // per wave
+  uint32_t win[SB_WIN / 4 + 4];
+  uint4 tok[SB_TOK];        // {out_rel, len | literal << 31, literal: window byte / copy: offset, 0}
+  uint2 bmc[SB_OUT / 32];   // token-start bits, tokens starting in earlier words
+};
+
+#ifdef PQ_SNAP_GUARD
+#define PQ_CHK(c, id, u, v, onfail)                                                                   \
+  do {                                                                                                \
+    if (c) {                                                                                          \
+      printf("PQ_CHK %d: %llx %llx\n", id, (unsigned long long)(u), (unsigned long long)(v));        \
+      onfail;                                                                                         \
+    }                                                                                                 \
+  } while (0)
+#define SNAP_GUARD(c, id, u, v)                                                                      \
+  do {                                                                                               \
+    if (c) printf("SNAP_GUARD %d: %lld %lld (dpos %lld dl %lld s %lld)\n", id, (long long)(u),        \
+                  (long long)(v), (long long)dpos, (long long)dl, (long long)s);                     \
+  } while (0)
+#else
+#define PQ_CHK(c, id, u, v, onfail) \
+  do {                              \
+  } while (0)
+#define SNAP_GUARD(c, id, u, v) \
+  do {                          \
+  } while (0)
+#endif
+
+__device__ __forceinline__ uint32_t snappy_tok_class(uint32_t tag) {
+  // token size in the stream (low byte) | output length << 8; 0: long literal
+  const uint32_t t = tag & 3, x = tag >> 2;
+  if (t == 0) return x >= 60 ? 0u : (x + 2) | ((x + 1) << 8);
+  if (t == 1) return 2u | ((4 + (x & 7)) << 8);
+  return (t == 2 ? 3u : 5u) | ((1 + x) << 8);
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One batch starting at the short token at s.  Returns false on a corrupt
+// token (err set); advances s / dpos / F otherwise.
+__device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const uint8_t *src, int64_t slen, uint8_t *dst,
+                                             int64_t dl, bool write, int64_t &s, int64_t &dpos, int64_t &F,
+                                             uint32_t &err, const uint8_t *pend_src, int64_t pend_dpos,
+                                             int64_t &pend_len, int ndefer, int64_t def_dst, int64_t def_len,
+                                             uint64_t def_src, int lane, const uint8_t *in_end) {
+  // 1. stage the window (aligned base; `sh` = position of byte s)
+  const uintptr_t abase = (uintptr_t)(src + s) & ~(uintptr_t)3;
+  const int sh = (int)((uintptr_t)(src + s) & 3);
+  const uint32_t *ga = (const uint32_t *)abase;
+  PQ_CHK(in_end && abase + 528 > (uintptr_t)in_end, 10, abase, in_end, err = E_SNAPPY; return false);
+  const uint32_t g0 = ga[lane], g1 = ga[lane + 64];
+  const uint32_t g2 = lane < 4 ? ga[lane + 128] : 0u;
+  L.win[lane] = g0;
+  L.win[lane + 64] = g1;
+  if (lane < 4) L.win[lane + 128] = g2;
+  const uint32_t pk01 = snappy_tok_class(g0 & 0xff) | (snappy_tok_class((g0 >> 8) & 0xff) << 16);
+  const uint32_t pk23 = snappy_tok_class((g0 >> 16) & 0xff) | (snappy_tok_class(g0 >> 24) << 16);
+  // 2. walk the chain over the first 256 window bytes
+  const int64_t lim64 = (int64_t)sh + (slen - s) - 1;  // last position inside the block
+  const int lim = lim64 < 255 ? (int)lim64 : 255;
+  int cur = sh, ntok = 0, T = 0;
+  uint32_t tokpos = 0;
+  while (ntok < SB_TOK && cur <= lim) {
+    const uint32_t w = (cur & 2) ? __builtin_amdgcn_readlane(pk23, cur >> 2) : __builtin_amdgcn_readlane(pk01, cur >> 2);
+    const uint32_t p = (cur & 1) ? (w >> 16) : (w & 0xffff);
+    if (p == 0 || T + (int)(p >> 8) > SB_OUT) break;
+    if (lane == ntok) tokpos = (uint32_t)cur;
+    ntok++;
+    T += (int)(p >> 8);
+    cur += (int)(p & 0xff);
+  }
+  wave_lds_sync();
+  // 3. decode + check token `lane`
+  const bool act = lane < ntok;
+  uint32_t len = 0, x = 0;
+  bool lit = false, bad = false;
+  if (act) {
+    const int pos = (int)tokpos;
+    uint64_t hv = (uint64_t)L.win[pos >> 2] | ((uint64_t)L.win[(pos >> 2) + 1] << 32);
+    hv >>= (pos & 3) * 8;
+    const uint32_t tag = (uint32_t)hv & 0xff;
+    const int64_t sabs = s + (pos - sh);  // stream position of the tag
+    if ((tag & 3) == 0) {
+      lit = true;
+      len = (tag >> 2) + 1;
+      x = (uint32_t)pos + 1;
+      bad = sabs + 1 + (int64_t)len > slen;
+    } else {
+      int hs;
+      if ((tag & 3) == 1) {
+        hs = 2;
+        len = 4 + ((tag >> 2) & 7);
+        x = ((tag & 0xe0) << 3) | (uint32_t)((hv >> 8) & 0xff);
+      } else if ((tag & 3) == 2) {
+        hs = 3;
+        len = 1 + (tag >> 2);
+        x = (uint32_t)((hv >> 8) & 0xffff);
+      } else {
+        hs = 5;
+        len = 1 + (tag >> 2);
+        x = (uint32_t)(hv >> 8);
+      }
+      bad = sabs + hs > slen;
+    }
+  }
+  int32_t total = 0;
+  const int32_t out_rel = wave_excl_scan32((int32_t)len, &total);
+  if (act) {
+    const int64_t d = dpos + out_rel;
+    bad |= (int64_t)len > dl - d;
+    if (!lit) bad |= x == 0 || (int64_t)x > d;
+  }
+  if (ballot(act && bad)) {
+    err = E_SNAPPY;
+    return false;
+  }
+  if (write) {
+    if (pend_len) {  // the history must hold the last deferred literal's tail
+      ring_fill(pend_src, pend_dpos, pend_len, ring, lane);
+      pend_len = 0;
+    }
+    // 4. token table + start bitmap
+    if (act) L.tok[lane] = make_uint4((uint32_t)out_rel, len | (lit ? 0x80000000u : 0u), x, 0u);
+    if (lane < SB_OUT / 32) L.bmc[lane] = make_uint2(0u, 0u);
+    wave_lds_sync();
+    if (act) __hip_atomic_fetch_or(&L.bmc[out_rel >> 5].x, 1u << (out_rel & 31), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WAVEFRONT);
+    wave_lds_sync();
+    const uint32_t bits = lane < SB_OUT / 32 ? L.bmc[lane].x : 0u;
+    int32_t tot2;
+    const int32_t before = wave_excl_scan32((int32_t)__builtin_popcount(bits), &tot2);
+    if (lane < SB_OUT / 32) L.bmc[lane].y = (uint32_t)before;
+    wave_lds_sync();
+    const int64_t near_lo = dpos + T - RING;  // older bytes may be overwritten by this batch
+    const uint8_t *winb = (const uint8_t *)L.win;
+    uint32_t farm = 0;  // iterations whose byte is older than the history
+    for (int it = 0, j = lane; j < T; it++, j += 64) {
+      int q = j;
+      uint8_t b = 0;
+      for (;;) {
+        const uint2 e = L.bmc[q >> 5];
+        const int k = (int)e.y + __builtin_popcount(e.x & (0xffffffffu >> (31 - (q & 31)))) - 1;
+        SNAP_GUARD(k < 0 || k >= ntok, 3, k, q);
+        const uint4 t = L.tok[k];
+        const int r = q - (int)t.x;
+        if (t.y >> 31) {
+          SNAP_GUARD(t.z + r >= 528u, 4, t.z, r);
+          b = winb[t.z + r];
+          break;
+        }
+        const uint32_t tl = t.y & 0x7fffffffu, off = t.z;
+        const int q2 = (int)t.x - (int)off + (int)(off >= tl ? (uint32_t)r : (uint32_t)r % off);
+        if (q2 >= 0) {
+          q = q2;
+          continue;
+        }
+        const int64_t p = dpos + q2;
+        if (p >= near_lo) b = ring[p & RING_MASK];
+        else farm |= 1u << it;
+        break;
+      }
+      if (!(farm >> it & 1)) ring[(dpos + j) & RING_MASK] = b;
+    }
+    if (ballot(farm != 0)) {
+      // rare: bytes older than the history come from HBM (this wave's earlier
+      // staging stores, made visible first) or from a deferred literal's
+      // payload; the deferred-literal table is read with readlane while every
+      // lane is active
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      for (int it = 0; it * 64 < T; it++) {
+        const int j = lane + 64 * it;
+        int64_t p = -1;
+        if (j < T && (farm >> it & 1)) {
+          int q = j;
+          for (;;) {
+            const uint2 e = L.bmc[q >> 5];
+            const int k = (int)e.y + __builtin_popcount(e.x & (0xffffffffu >> (31 - (q & 31)))) - 1;
+            const uint4 t = L.tok[k];
+            const int r = q - (int)t.x;
+            const uint32_t tl = t.y & 0x7fffffffu, off = t.z;
+            const int q2 = (int)t.x - (int)off + (int)(off >= tl ? (uint32_t)r : (uint32_t)r % off);
+            if (q2 >= 0) {
+              q = q2;
+              continue;
+            }
+            p = dpos + q2;
+            break;
+          }
+        }
+        uintptr_t from = (p >= 0 && p < F) ? (uintptr_t)(dst + p) : 0;  // staged output (p < F by construction)
+        bool payload = false;
+        for (int k = 0; k < ndefer; k++) {
+          // (readlane returns int: widen through uint32_t, no sign extension)
+          const int64_t kd =
+              (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)def_dst >> 32), k) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)def_dst, k));
+          const int64_t kl = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)def_len, k);
+          const uint64_t ks = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(def_src >> 32), k) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)def_src, k);
+          if (p >= kd && p < kd + kl) {
+            from = (uintptr_t)ks + (uintptr_t)(p - kd);
+            payload = true;
+          }
+        }
+        PQ_CHK(p >= 0 && from && payload && (from < (uintptr_t)src || from >= (uintptr_t)(src + slen)), 11, from, p,
+               from = 0);
+        PQ_CHK(p >= 0 && from && !payload && (from < (uintptr_t)dst || from >= (uintptr_t)(dst + dl)), 12, from, p,
+               from = 0);
+        if (p >= 0 && from) {
+          uint8_t b;
+          if (payload) {
+            b = *(const uint8_t *)from;
+          } else {
+            const uint32_t word = __hip_atomic_load((const uint32_t *)(from & ~(uintptr_t)3), __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+            b = (uint8_t)(word >> ((from & 3) * 8));
+          }
+          ring[(dpos + j) & RING_MASK] = b;
+        }
+      }
+    }
+    wave_lds_sync();
+    // 5. to HBM: bytes up to the next 16-byte boundary (F is unaligned after
+    // a long literal), then whole 16-byte chunks up to floor16(dpos + T)
+    // (dst is 16-byte aligned)
+    const int64_t end = dpos + T;
+    int64_t a16 = (F + 15) & ~(int64_t)15;
+    if (a16 > end) a16 = end;
+    SNAP_GUARD(a16 - F > 64 || a16 > dl, 1, a16, F);
+    if (lane < a16 - F) dst[F + lane] = ring[(F + lane) & RING_MASK];
+    F = a16;
+    const int64_t e16 = end & ~(int64_t)15;
+    if ((F & 15) == 0)
+      for (int64_t c = F + 16 * (int64_t)lane; c < e16; c += 1024) {
+      const uint4 v = *(const uint4 *)(ring + (c & RING_MASK));
+      *(uint4 *)(dst + c) = v;
+    }
+    SNAP_GUARD(e16 > dl, 5, e16, dl);
+    if (e16 > F) F = e16;
+  }
+  dpos += total;
+  s += cur - sh;
+  return true;
+}
+
 __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t ring_all[SNAPPY_WAVES][RING];
+  __shared__ SnapLds sl_all[SNAPPY_WAVES];
   const int lane = lane_id();
   const int wv = (int)ufirst(threadIdx.x >> 6);  // wave-uniform (keeps per-wave state in SGPRs)
   const int gi = blockIdx.x * SNAPPY_WAVES + wv;
@@ -253,12 +524,15 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
   if (a.max_jobs > 0 && lane == 0) a.njobs[gi] = 0u;  // no deferred jobs unless written below
   if (page_status(a.status, page) < make_status(ST_DECOMPRESS, 0)) return;
   uint8_t *ring = ring_all[wv];
+  SnapLds &L = sl_all[wv];
 
   const int64_t lsize = d.kind == PAGE_V2 ? (int64_t)d.v2_rep_len + d.v2_def_len : 0;
   const uint8_t *src = a.in + d.src + lsize;
   const int64_t slen = d.comp_len;
   uint8_t *dst = a.stage + d.body;
   const int64_t expect = d.body_len;
+  PQ_CHK(a.in_end && (src < a.in || src + slen > a.in_end), 13, (uintptr_t)src, slen, return);
+  PQ_CHK(a.stage_end && (dst < a.stage || dst + expect > a.stage_end), 14, (uintptr_t)dst, expect, return);
 
   Win W;
   W.reset();
@@ -316,6 +590,7 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
     }
   }
   int64_t dpos = 0;
+  int64_t F = 0;  // staged output below F is in HBM; [F, dpos) only in the history
   uint32_t err = E_OK;
   int ndefer = 0;                      // deferred literals: lane k holds entry k
   const uint8_t *pend_src = nullptr;   // last deferred literal whose tail is not yet in the history
@@ -324,8 +599,22 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
   uint64_t def_src = 0;
   while (s < slen) {
     uint32_t tag = W.byte_at(src + s);
-    int64_t length, offset;
-    if ((tag & 3) == 0) {  // literal
+    if ((tag & 3) != 0 || (tag >> 2) < 60) {
+      // ---- short tokens (copies, literals <= 60 bytes): one batch of up to
+      // SB_TOK tokens / SB_OUT output bytes per pass (snappy_batch)
+      if (!snappy_batch(L, ring, src, slen, dst, dl, write, s, dpos, F, err, pend_src, pend_dpos, pend_len, ndefer,
+                        def_dst, def_len, def_src, lane, a.in_end))
+        break;
+      continue;
+    }
+    // ---- long literal (tag >= 60 << 2): whole-wave copy or deferred to k_copy
+    if (write && F < dpos) {  // bytes of the last batch still only in the history
+      SNAP_GUARD(dpos - F > 64, 6, dpos, F);
+      if (lane < dpos - F) dst[F + lane] = ring[(F + lane) & RING_MASK];
+      F = dpos;
+    }
+    int64_t length;
+    {
       uint32_t x = tag >> 2;
       if (x < 60) {
         s += 1;
@@ -370,6 +659,7 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
             ring_fill(pend_src, pend_dpos, pend_len, ring, lane);
             pend_len = 0;
           }
+          PQ_CHK(dpos + length > dl || s + length > slen, 15, dpos + length, s + length, return);
           copy_literal(src + s, dst, dpos, length, ring, lane);
         }
       }
@@ -410,76 +700,13 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
           s += (int64_t)m * stride;
         }
       }
+      if (write) F = dpos;
       continue;
     }
-    if ((tag & 3) == 1) {  // copy1
-      s += 2;
-      if (s > slen) {
-        err = E_SNAPPY;
-        break;
-      }
-      uint32_t b1 = W.byte_at(src + s - 1);
-      length = 4 + ((tag >> 2) & 7);
-      offset = ((int64_t)(tag & 0xe0) << 3) | b1;
-    } else if ((tag & 3) == 2) {  // copy2
-      s += 3;
-      if (s > slen) {
-        err = E_SNAPPY;
-        break;
-      }
-      length = 1 + (tag >> 2);
-      offset = (int64_t)(W.byte_at(src + s - 2) | (W.byte_at(src + s - 1) << 8));
-    } else {  // copy4
-      s += 5;
-      if (s > slen) {
-        err = E_SNAPPY;
-        break;
-      }
-      length = 1 + (tag >> 2);
-      offset = (int64_t)W.u32_at(src + s - 4);
-    }
-    if (offset <= 0 || dpos < offset || length > dl - dpos) {
-      err = E_SNAPPY;
-      break;
-    }
-    if (write) {
-      if (pend_len) {
-        ring_fill(pend_src, pend_dpos, pend_len, ring, lane);
-        pend_len = 0;
-      }
-      // forward, possibly self-overlapping copy of <= 64 bytes
-      uint8_t b = 0;
-      bool act = lane < length;
-      int64_t from = dpos - offset + (offset >= length ? (int64_t)lane : (int64_t)lane % offset);
-      if (offset <= RING) {
-        if (act) b = ring[from & RING_MASK];
-      } else {
-        // far copy: make this wave's earlier stores visible, read through L2
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        const uint8_t *lit = nullptr;  // inside a deferred literal: read the payload instead
-        for (int k = 0; k < ndefer; k++) {
-          int64_t kd = (int64_t)shfl64((uint64_t)def_dst, k), kl = (int64_t)shfl64((uint64_t)def_len, k);
-          uint64_t ks = shfl64(def_src, k);
-          if (from >= kd && from < kd + kl) lit = (const uint8_t *)(uintptr_t)ks + (from - kd);
-        }
-        if (act) {
-          if (lit) {
-            b = *lit;
-          } else {
-            const uint32_t *wp = (const uint32_t *)((uintptr_t)(dst + from) & ~(uintptr_t)3);
-            uint32_t word = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            b = (uint8_t)(word >> (((uintptr_t)(dst + from) & 3) * 8));
-          }
-        }
-      }
-      if (act) {
-        dst[dpos + lane] = b;
-        ring[(dpos + lane) & RING_MASK] = b;
-      }
-    }
-    dpos += length;
   }
   if (err == E_OK && dpos != dl) err = E_SNAPPY;
+  if (err == E_OK && write)
+    for (int64_t p = F + lane; p < dl; p += 64) dst[p] = ring[p & RING_MASK];
   if (err == E_OK && !write) err = E_SIZE;  // compress.go:117-119
   if (a.max_jobs > 0 && lane == 0) a.njobs[gi] = err ? 0u : (uint32_t)ndefer;
   if (!err && ndefer > 0) {  // register the page's deferred literals in the compact list
@@ -502,10 +729,24 @@ constexpr int COPY_ITEMS = 4;     // work items per job slot and pass (64 KiB: a
 // a job longer than COPY_ITEMS chunks is covered in passes.  Every load of a
 // chunk is issued before its stores.
 __device__ __forceinline__ void copy_items(const KArgs &a, uint32_t blk, uint32_t nblk) {
-  const uint32_t items = a.copy_cnt[a.epoch & 1] * COPY_ITEMS;  // registered by k_snappy
+  // the count, index and job records were written by k_snappy in the previous
+  // launch: read them with vector loads at device scope (a uniform plain load
+  // becomes a scalar-cache load, which can return lines of an earlier decode
+  // that used the same addresses)
+  const uint32_t items =
+      __hip_atomic_load(&a.copy_cnt[a.epoch & 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * COPY_ITEMS;
   for (uint32_t it = blk; it < items; it += nblk) {
     const uint32_t c = it % COPY_ITEMS;
-    const CopyJob job = a.jobs[a.copy_idx[it / COPY_ITEMS]];
+    const uint32_t ji =
+        (uint32_t)__hip_atomic_load(&a.copy_idx[it / COPY_ITEMS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t *jw = (const uint64_t *)&a.jobs[ji];
+    CopyJob job;
+    job.src = (const uint8_t *)(uintptr_t)__hip_atomic_load(&jw[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    job.dst = (uint8_t *)(uintptr_t)__hip_atomic_load(&jw[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    job.len = (int64_t)__hip_atomic_load(&jw[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    PQ_CHK(a.in_end && (job.src < a.in || job.src + job.len > a.in_end || job.dst < a.stage ||
+                        job.dst + job.len > a.stage_end || job.len < 0),
+           20, (uintptr_t)job.src, job.len, return);
     const int t = threadIdx.x;
     const uintptr_t d0 = (uintptr_t)job.dst, d1 = d0 + (uintptr_t)job.len;
     const uintptr_t A = d0 & ~(uintptr_t)15;
@@ -2668,10 +2909,13 @@ struct pq_launch_args {
   const uint32_t *status0;
   const void *zr;
   int32_t nzr, npages;
+  const uint8_t *in_end, *stage_end;
 };
 
 static pq::KArgs to_k(const pq_launch_args *p) {
   pq::KArgs k;
+  k.in_end = p->in_end;
+  k.stage_end = p->stage_end;
   k.in = p->in;
   k.stage = p->stage;
   k.pages = (const pq::PageDesc *)p->pages;
