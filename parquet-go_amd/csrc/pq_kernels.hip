@@ -310,14 +310,25 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
                                              int64_t dl, bool write, int64_t &s, int64_t &dpos, int64_t &F,
                                              uint32_t &err, const uint8_t *pend_src, int64_t pend_dpos,
                                              int64_t &pend_len, int ndefer, int64_t def_dst, int64_t def_len,
-                                             uint64_t def_src, int lane, const uint8_t *in_end) {
-  // 1. stage the window (aligned base; `sh` = position of byte s)
+                                             uint64_t def_src, int lane, const uint8_t *in_end, int64_t &pf_s,
+                                             uint32_t &pg0, uint32_t &pg1, uint32_t &pg2) {
+  // 1. stage the window (aligned base; `sh` = position of byte s); the
+  // previous batch prefetched it into pg0..pg2 when it ended at s
   const uintptr_t abase = (uintptr_t)(src + s) & ~(uintptr_t)3;
   const int sh = (int)((uintptr_t)(src + s) & 3);
   const uint32_t *ga = (const uint32_t *)abase;
   PQ_CHK(in_end && abase + 528 > (uintptr_t)in_end, 10, abase, in_end, err = E_SNAPPY; return false);
-  const uint32_t g0 = ga[lane], g1 = ga[lane + 64];
-  const uint32_t g2 = lane < 4 ? ga[lane + 128] : 0u;
+  uint32_t g0, g1, g2;
+  if (pf_s == s) {
+    g0 = pg0;
+    g1 = pg1;
+    g2 = pg2;
+  } else {
+    g0 = ga[lane];
+    g1 = ga[lane + 64];
+    g2 = lane < 4 ? ga[lane + 128] : 0u;
+  }
+  pf_s = -1;
   L.win[lane] = g0;
   L.win[lane + 64] = g1;
   if (lane < 4) L.win[lane + 128] = g2;
@@ -387,8 +398,67 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
       ring_fill(pend_src, pend_dpos, pend_len, ring, lane);
       pend_len = 0;
     }
-    // 4. token table + start bitmap
-    if (act) L.tok[lane] = make_uint4((uint32_t)out_rel, len | (lit ? 0x80000000u : 0u), x, 0u);
+    // 4. far copies first: a copy token whose whole source is older than the
+    // history (staged output of earlier batches, or a deferred literal's
+    // payload) is loaded by its own lane and written to the history at its
+    // output position, all such loads in flight together
+    const int64_t near_lo = dpos + T - RING;  // older bytes may be overwritten by this batch
+    const int64_t S = dpos + out_rel - (int64_t)x;  // copy: absolute source start
+    bool pre = false;
+    if (ballot(act && !lit && S < near_lo)) {
+      // this wave's earlier staging stores must be visible to the loads below
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      pre = act && !lit && x >= len && S + (int64_t)len <= near_lo;
+      uintptr_t fsrc = pre ? (uintptr_t)(dst + S) : 0;
+      bool in_payload = false;
+      for (int k2 = 0; k2 < ndefer; k2++) {  // every lane active: readlane of the deferred-literal table
+        const int64_t kd =
+            (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)def_dst >> 32), k2) << 32) |
+                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)def_dst, k2));
+        const int64_t kl = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)def_len, k2);
+        const uint64_t ks = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(def_src >> 32), k2) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)def_src, k2);
+        if (pre && S < kd + kl && S + (int64_t)len > kd) {
+          if (S >= kd && S + (int64_t)len <= kd + kl) {
+            fsrc = (uintptr_t)ks + (uintptr_t)(S - kd);
+            in_payload = true;
+          } else {
+            pre = false;  // straddles a deferred literal: byte by byte below
+          }
+        }
+      }
+      if (pre) {
+        // <= 64 source bytes: up to 9 aligned qwords; staged output read at
+        // device scope (bypasses a possibly stale L1 line)
+        const uintptr_t b8 = fsrc & ~(uintptr_t)7;
+        const int sh8 = (int)(fsrc & 7);
+        const int64_t o = dpos + out_rel;
+#pragma unroll
+        for (int w = 0; w < 9; w++) {
+          if (w * 8 >= sh8 + (int)len) break;
+          const uint64_t *qp = (const uint64_t *)(b8 + 8 * (uintptr_t)w);
+          const uint64_t v = in_payload ? *qp : __hip_atomic_load(qp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+          for (int bb = 0; bb < 8; bb++) {
+            const int i2 = w * 8 + bb - sh8;
+            if (i2 >= 0 && i2 < (int)len) ring[(o + i2) & RING_MASK] = (uint8_t)(v >> (8 * bb));
+          }
+        }
+      }
+    }
+    // prefetch the next batch's window (its loads overlap this batch's byte passes)
+    {
+      const int64_t sn = s + (cur - sh);
+      if (sn < slen) {
+        const uint32_t *gn = (const uint32_t *)((uintptr_t)(src + sn) & ~(uintptr_t)3);
+        pg0 = gn[lane];
+        pg1 = gn[lane + 64];
+        pg2 = lane < 4 ? gn[lane + 128] : 0u;
+        pf_s = sn;
+      }
+    }
+    // token table + start bitmap
+    if (act) L.tok[lane] = make_uint4((uint32_t)out_rel, len | (lit ? 0x80000000u : 0u) | (pre ? 0x40000000u : 0u), x, 0u);
     if (lane < SB_OUT / 32) L.bmc[lane] = make_uint2(0u, 0u);
     wave_lds_sync();
     if (act) __hip_atomic_fetch_or(&L.bmc[out_rel >> 5].x, 1u << (out_rel & 31), __ATOMIC_RELAXED,
@@ -399,96 +469,82 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
     const int32_t before = wave_excl_scan32((int32_t)__builtin_popcount(bits), &tot2);
     if (lane < SB_OUT / 32) L.bmc[lane].y = (uint32_t)before;
     wave_lds_sync();
-    const int64_t near_lo = dpos + T - RING;  // older bytes may be overwritten by this batch
+    // 5. every output byte by its own lane, 64 bytes per pass: a copy byte is
+    // chased back to a literal, a prefilled far copy, a byte resolved by an
+    // earlier pass (already in the history), or a byte before the batch
     const uint8_t *winb = (const uint8_t *)L.win;
-    uint32_t farm = 0;  // iterations whose byte is older than the history
-    for (int it = 0, j = lane; j < T; it++, j += 64) {
-      int q = j;
-      uint8_t b = 0;
-      for (;;) {
-        const uint2 e = L.bmc[q >> 5];
-        const int k = (int)e.y + __builtin_popcount(e.x & (0xffffffffu >> (31 - (q & 31)))) - 1;
-        SNAP_GUARD(k < 0 || k >= ntok, 3, k, q);
-        const uint4 t = L.tok[k];
-        const int r = q - (int)t.x;
-        if (t.y >> 31) {
-          SNAP_GUARD(t.z + r >= 528u, 4, t.z, r);
-          b = winb[t.z + r];
-          break;
-        }
-        const uint32_t tl = t.y & 0x7fffffffu, off = t.z;
-        const int q2 = (int)t.x - (int)off + (int)(off >= tl ? (uint32_t)r : (uint32_t)r % off);
-        if (q2 >= 0) {
-          q = q2;
-          continue;
-        }
-        const int64_t p = dpos + q2;
-        if (p >= near_lo) b = ring[p & RING_MASK];
-        else farm |= 1u << it;
-        break;
-      }
-      if (!(farm >> it & 1)) ring[(dpos + j) & RING_MASK] = b;
-    }
-    if (ballot(farm != 0)) {
-      // rare: bytes older than the history come from HBM (this wave's earlier
-      // staging stores, made visible first) or from a deferred literal's
-      // payload; the deferred-literal table is read with readlane while every
-      // lane is active
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-      for (int it = 0; it * 64 < T; it++) {
-        const int j = lane + 64 * it;
-        int64_t p = -1;
-        if (j < T && (farm >> it & 1)) {
-          int q = j;
-          for (;;) {
-            const uint2 e = L.bmc[q >> 5];
-            const int k = (int)e.y + __builtin_popcount(e.x & (0xffffffffu >> (31 - (q & 31)))) - 1;
-            const uint4 t = L.tok[k];
-            const int r = q - (int)t.x;
-            const uint32_t tl = t.y & 0x7fffffffu, off = t.z;
-            const int q2 = (int)t.x - (int)off + (int)(off >= tl ? (uint32_t)r : (uint32_t)r % off);
-            if (q2 >= 0) {
-              q = q2;
-              continue;
-            }
-            p = dpos + q2;
+    for (int it = 0; it * 64 < T; it++) {
+      const int j = lane + 64 * it;
+      if (j < T) {
+        int q = j;
+        uint8_t b = 0;
+        for (;;) {
+          const uint2 e = L.bmc[q >> 5];
+          const int k = (int)e.y + __builtin_popcount(e.x & (0xffffffffu >> (31 - (q & 31)))) - 1;
+          SNAP_GUARD(k < 0 || k >= ntok, 3, k, q);
+          const uint4 t = L.tok[k];
+          const int r = q - (int)t.x;
+          if (t.y >> 31) {
+            SNAP_GUARD(t.z + r >= 528u, 4, t.z, r);
+            b = winb[t.z + r];
             break;
           }
-        }
-        uintptr_t from = (p >= 0 && p < F) ? (uintptr_t)(dst + p) : 0;  // staged output (p < F by construction)
-        bool payload = false;
-        for (int k = 0; k < ndefer; k++) {
-          // (readlane returns int: widen through uint32_t, no sign extension)
-          const int64_t kd =
-              (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)def_dst >> 32), k) << 32) |
-                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)def_dst, k));
-          const int64_t kl = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)def_len, k);
-          const uint64_t ks = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(def_src >> 32), k) << 32) |
-                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)def_src, k);
-          if (p >= kd && p < kd + kl) {
-            from = (uintptr_t)ks + (uintptr_t)(p - kd);
-            payload = true;
+          if (t.y & 0x40000000u) {  // far copy, prefilled
+            b = ring[(dpos + q) & RING_MASK];
+            break;
           }
-        }
-        PQ_CHK(p >= 0 && from && payload && (from < (uintptr_t)src || from >= (uintptr_t)(src + slen)), 11, from, p,
-               from = 0);
-        PQ_CHK(p >= 0 && from && !payload && (from < (uintptr_t)dst || from >= (uintptr_t)(dst + dl)), 12, from, p,
-               from = 0);
-        if (p >= 0 && from) {
-          uint8_t b;
-          if (payload) {
-            b = *(const uint8_t *)from;
+          const uint32_t tl = t.y & 0x3fffffffu, off = t.z;
+          const int q2 = (int)t.x - (int)off + (int)(off >= tl ? (uint32_t)r : (uint32_t)r % off);
+          if (q2 >= 0) {
+            if (q2 < 64 * it) {  // resolved by an earlier pass
+              b = ring[(dpos + q2) & RING_MASK];
+              break;
+            }
+            q = q2;
+            continue;
+          }
+          const int64_t p = dpos + q2;
+          if (p >= near_lo) {
+            b = ring[p & RING_MASK];
           } else {
-            const uint32_t word = __hip_atomic_load((const uint32_t *)(from & ~(uintptr_t)3), __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-            b = (uint8_t)(word >> ((from & 3) * 8));
+            // rare: one byte of a copy that straddles the history edge or a
+            // deferred literal
+            uintptr_t from = (p >= 0 && p < F) ? (uintptr_t)(dst + p) : 0;
+            bool payload = false;
+            for (int k2 = 0; k2 < ndefer; k2++) {
+              const int64_t kd = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
+                                                (int)(uint32_t)((uint64_t)def_dst >> 32), k2)
+                                            << 32) |
+                                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)def_dst, k2));
+              const int64_t kl = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)def_len, k2);
+              if (p >= kd && p < kd + kl) {
+                const uint64_t ks =
+                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(def_src >> 32), k2) << 32) |
+                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)def_src, k2);
+                from = (uintptr_t)ks + (uintptr_t)(p - kd);
+                payload = true;
+              }
+            }
+            PQ_CHK(from && payload && (from < (uintptr_t)src || from >= (uintptr_t)(src + slen)), 11, from, p, from = 0);
+            PQ_CHK(from && !payload && (from < (uintptr_t)dst || from >= (uintptr_t)(dst + dl)), 12, from, p, from = 0);
+            if (from) {
+              if (payload) {
+                b = *(const uint8_t *)from;
+              } else {
+                const uint32_t word = __hip_atomic_load((const uint32_t *)(from & ~(uintptr_t)3), __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+                b = (uint8_t)(word >> ((from & 3) * 8));
+              }
+            }
           }
-          ring[(dpos + j) & RING_MASK] = b;
+          break;
         }
+        ring[(dpos + j) & RING_MASK] = b;
       }
+      wave_lds_sync();
     }
     wave_lds_sync();
-    // 5. to HBM: bytes up to the next 16-byte boundary (F is unaligned after
+    // 6. to HBM: bytes up to the next 16-byte boundary (F is unaligned after
     // a long literal), then whole 16-byte chunks up to floor16(dpos + T)
     // (dst is 16-byte aligned)
     const int64_t end = dpos + T;
@@ -597,13 +653,16 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
   int64_t pend_dpos = 0, pend_len = 0;
   int64_t def_dst = 0, def_len = 0;
   uint64_t def_src = 0;
+  int64_t pf_s = -1;  // stream position of the window prefetched into pg0..pg2
+  uint32_t pg0 = 0, pg1 = 0, pg2 = 0;
   while (s < slen) {
-    uint32_t tag = W.byte_at(src + s);
+    const uint32_t tag = pf_s == s ? (__builtin_amdgcn_readlane(pg0, 0) >> (8 * ((uintptr_t)(src + s) & 3))) & 0xffu
+                                   : W.byte_at(src + s);
     if ((tag & 3) != 0 || (tag >> 2) < 60) {
       // ---- short tokens (copies, literals <= 60 bytes): one batch of up to
       // SB_TOK tokens / SB_OUT output bytes per pass (snappy_batch)
       if (!snappy_batch(L, ring, src, slen, dst, dl, write, s, dpos, F, err, pend_src, pend_dpos, pend_len, ndefer,
-                        def_dst, def_len, def_src, lane, a.in_end))
+                        def_dst, def_len, def_src, lane, a.in_end, pf_s, pg0, pg1, pg2))
         break;
       continue;
     }
