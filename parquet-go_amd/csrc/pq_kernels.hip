@@ -125,7 +125,7 @@ __device__ __forceinline__ const uint8_t *body_ptr(const KArgs &a, const PageDes
 // ===========================================================================
 // K1: Snappy (vendor/github.com/golang/snappy/decode.go:55-75, decode_other.go:14-101)
 // ===========================================================================
-constexpr int RING = 8192;  // per-wave LDS history (bytes)
+constexpr int RING = 4096;  // per-wave LDS history (bytes): 4 KB keeps six waves per SIMD resident (older bytes: HBM)
 constexpr int RING_MASK = RING - 1;
 constexpr int SNAPPY_WAVES = 4;
 
@@ -264,8 +264,13 @@ constexpr int SB_WIN = 512;   // compressed bytes staged per batch (walk covers 
 
 struct SnapLds {  // per wave
   uint32_t win[SB_WIN / 4 + 4];
-  uint4 tok[SB_TOK];        // {out_rel, len | literal << 31, literal: window byte / copy: offset, 0}
-  uint2 bmc[SB_OUT / 32];   // token-start bits, tokens starting in earlier words
+  union {
+    struct {
+      uint4 tok[SB_TOK];        // {out_rel, len | literal << 31 | prefilled << 30, literal: window byte / copy: offset, 0}
+      uint2 bmc[SB_OUT / 32];   // token-start bits, tokens starting in earlier words
+    };
+    uint16_t jt[2][320];        // chain walk: jump tables J_b, J_b+1 over window positions 0..256
+  };
 };
 
 #ifdef PQ_SNAP_GUARD
@@ -334,20 +339,51 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
   if (lane < 4) L.win[lane + 128] = g2;
   const uint32_t pk01 = snappy_tok_class(g0 & 0xff) | (snappy_tok_class((g0 >> 8) & 0xff) << 16);
   const uint32_t pk23 = snappy_tok_class((g0 >> 16) & 0xff) | (snappy_tok_class(g0 >> 24) << 16);
-  // 2. walk the chain over the first 256 window bytes
+  // 2. the token chain over the first 256 window positions by pointer
+  // jumping: J_0(i) = i + size(i) (256: stop), J_b+1 = J_b o J_b; lane m
+  // applies J_b for the set bits b of m starting at sh, so it lands on the
+  // m-th token (no serial walk on the scalar unit)
   const int64_t lim64 = (int64_t)sh + (slen - s) - 1;  // last position inside the block
   const int lim = lim64 < 255 ? (int)lim64 : 255;
-  int cur = sh, ntok = 0, T = 0;
-  uint32_t tokpos = 0;
-  while (ntok < SB_TOK && cur <= lim) {
-    const uint32_t w = (cur & 2) ? __builtin_amdgcn_readlane(pk23, cur >> 2) : __builtin_amdgcn_readlane(pk01, cur >> 2);
-    const uint32_t p = (cur & 1) ? (w >> 16) : (w & 0xffff);
-    if (p == 0 || T + (int)(p >> 8) > SB_OUT) break;
-    if (lane == ntok) tokpos = (uint32_t)cur;
-    ntok++;
-    T += (int)(p >> 8);
-    cur += (int)(p & 0xff);
+  uint16_t *ja = L.jt[0], *jb = L.jt[1];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int i = 4 * lane + j;
+    const uint32_t w = j < 2 ? pk01 : pk23;
+    const uint32_t p = (j & 1) ? (w >> 16) : (w & 0xffff);
+    const int nx = i + (int)(p & 0xff);
+    ja[i] = (uint16_t)((p == 0 || i > lim || nx > 256) ? 256 : nx);
   }
+  if (lane == 0) {
+    ja[256] = 256;
+    jb[256] = 256;
+  }
+  wave_lds_sync();
+  int pos = sh;
+#pragma unroll
+  for (int b = 0; b < 6; b++) {
+    if ((lane >> b) & 1) pos = ja[pos];
+    if (b < 5) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int i = 4 * lane + j;
+        jb[i] = ja[ja[i]];
+      }
+      wave_lds_sync();
+      uint16_t *t = ja;
+      ja = jb;
+      jb = t;
+    }
+  }
+  const uint32_t w01 = shfl32(pk01, (pos >> 2) & 63), w23 = shfl32(pk23, (pos >> 2) & 63);
+  const uint32_t wp = (pos & 2) ? w23 : w01;
+  const uint32_t pc = (pos & 1) ? (wp >> 16) : (wp & 0xffff);  // class of this lane's token
+  const bool valid = pos <= lim && pc != 0;
+  const int32_t incl = wave_incl_scan32(valid ? (int32_t)(pc >> 8) : 0);
+  const int ntok = __builtin_popcountll(ballot(valid && incl <= SB_OUT));  // a prefix of the lanes
+  const int T = (int)__builtin_amdgcn_readlane(incl, ntok - 1);
+  const int cur = (int)__builtin_amdgcn_readlane(pos, ntok - 1) + (int)(__builtin_amdgcn_readlane(pc, ntok - 1) & 0xff);
+  const uint32_t tokpos = (uint32_t)pos;
   wave_lds_sync();
   // 3. decode + check token `lane`
   const bool act = lane < ntok;
