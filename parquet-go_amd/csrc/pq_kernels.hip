@@ -775,7 +775,7 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
           for (int q = 0; q < hs; q++) ok &= src[cs + q] == t0[q];
         }
         const uint64_t okm = ballot(ok);
-        const int m = (int)__builtin_ctzll(~okm);
+        const int m = ~okm ? (int)__builtin_ctzll(~okm) : 64;
         if (m > 0) {
           if (lane < m) {
             a.jobs[a.job_base[gi] + ndefer + lane] = CopyJob{src + cs + hs, dst + dpos + (int64_t)lane * length, length};
@@ -901,6 +901,98 @@ __global__ __launch_bounds__(256) void k_reset(KArgs a) {
 // ===========================================================================
 // K2: dictionary pages (page_dict.go:30-64)
 // ===========================================================================
+// ===========================================================================
+// PLAIN BYTE_ARRAY length prefixes (type_bytearray.go:24-45): [u32 len][bytes]
+// ... for n entries.  The chain of entry positions is found 64 entries at a
+// time by pointer jumping over a 1 KiB window staged in LDS (J_0(i) = i + 4 +
+// len(i), 1024 = stop; lane m lands on entry m after 6 rounds), instead of a
+// serial walk.  emit(first entry, entry lane, value offset, length) is called
+// by every lane with the batch's entries in lanes < cnt.  Returns the first
+// error in entry order: E_EOF (header or bytes past the stream), E_BYTE_ARRAY
+// (negative length), or E_OK.
+// ===========================================================================
+constexpr int BA_WIN = 1024;  // k_dict_prepare's window (k_prepare: 448, in its run-walk LDS)
+struct BaLds {
+  uint32_t win[BA_WIN / 4 + 8];
+  uint16_t jt[2][BA_WIN + 8];
+};
+
+template <int WINB, class Emit>
+__device__ __forceinline__ uint32_t ba_walk(const uint8_t *vp, int64_t vlen, int64_t n, uint32_t *win, uint16_t *ja0,
+                                            uint16_t *jb0, Emit emit) {
+  static_assert(WINB % 64 == 0, "window: whole lanes");
+  const int lane = lane_id();
+  int64_t P = 0, done = 0;
+  while (done < n) {
+    const int64_t avail = vlen - P;
+    const uintptr_t ab = (uintptr_t)(vp + P) & ~(uintptr_t)3;
+    const int sh = (int)((uintptr_t)(vp + P) & 3);
+    const uint32_t *ga = (const uint32_t *)ab;
+#pragma unroll
+    for (int q = 0; q * 64 < WINB / 4 + 8; q++)
+      if (lane + 64 * q < WINB / 4 + 8) win[lane + 64 * q] = ga[lane + 64 * q];
+    wave_lds_sync();
+    uint16_t *ja = ja0, *jb = jb0;
+#pragma unroll
+    for (int q = 0; q < WINB / 64; q++) {
+      const int i = lane + 64 * q;
+      const int b = sh + i;
+      const uint64_t w2 = (uint64_t)win[b >> 2] | ((uint64_t)win[(b >> 2) + 1] << 32);
+      const int32_t l = (int32_t)(uint32_t)(w2 >> ((b & 3) * 8));
+      const bool ok = (int64_t)i + 4 <= avail && l >= 0 && (int64_t)i + 4 + l <= avail;
+      const int64_t nx = (int64_t)i + 4 + (int64_t)l;
+      ja[i] = (uint16_t)((ok && nx < WINB) ? nx : WINB);
+    }
+    if (lane == 0) {
+      ja[WINB] = WINB;
+      jb[WINB] = WINB;
+    }
+    wave_lds_sync();
+    int pos = 0;
+#pragma unroll
+    for (int bt = 0; bt < 6; bt++) {
+      if ((lane >> bt) & 1) pos = ja[pos];
+      if (bt < 5) {
+#pragma unroll
+        for (int q = 0; q < WINB / 64; q++) {
+          const int i = lane + 64 * q;
+          jb[i] = ja[ja[i]];
+        }
+        wave_lds_sync();
+        uint16_t *t = ja;
+        ja = jb;
+        jb = t;
+      }
+    }
+    // this lane's entry
+    const bool real = pos < WINB;
+    int32_t l = 0;
+    uint32_t code = E_OK;
+    if (real) {
+      const int b = sh + pos;
+      const uint64_t w2 = (uint64_t)win[b >> 2] | ((uint64_t)win[(b >> 2) + 1] << 32);
+      l = (int32_t)(uint32_t)(w2 >> ((b & 3) * 8));
+      if ((int64_t)pos + 4 > avail) code = E_EOF;
+      else if (l < 0) code = E_BYTE_ARRAY;
+      else if ((int64_t)pos + 4 + l > avail) code = E_EOF;
+    }
+    wave_lds_sync();
+    const int64_t left = n - done;
+    const bool mine = lane < left;
+    const uint64_t okm = ballot(mine && real && code == E_OK);
+    const int cnt = ~okm ? (int)__builtin_ctzll(~okm) : 64;  // leading valid entries
+    if (cnt < 64 && cnt < left && ballot(lane == cnt && real && code != E_OK)) {
+      return (uint32_t)__builtin_amdgcn_readlane(code, cnt);  // the first failing entry, in order
+    }
+    if (cnt == 0) return E_EOF;  // nothing readable (cannot happen for avail >= 4)
+    emit(done, lane, P + pos + 4, l, cnt);
+    const int lp = (int)__builtin_amdgcn_readlane(pos, cnt - 1), ll = (int)__builtin_amdgcn_readlane(l, cnt - 1);
+    P += (int64_t)lp + 4 + ll;
+    done += cnt;
+  }
+  return E_OK;
+}
+
 __global__ __launch_bounds__(256) void k_dict_prepare(KArgs a) {
   const int gi = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
   if (gi >= a.nlist) return;
@@ -915,33 +1007,14 @@ __global__ __launch_bounds__(256) void k_dict_prepare(KArgs a) {
     if (n * (int64_t)c.width > len) set_status(a.status, page, ST_DICT_VALUES, E_EOF);
     return;
   }
-  // serial length-prefix walk (type_bytearray.go:24-45); lane j of each
-  // 64-entry group collects its entry and stores it coalesced
-  Win W;
-  W.reset();
-  int64_t pos = 0;
-  for (int64_t base = 0; base < n; base += 64) {
-    int cnt = (int)min<int64_t>(64, n - base);
-    uint64_t mine = 0;
-    for (int j = 0; j < cnt; j++) {
-      if (pos + 4 > len) {
-        set_status(a.status, page, ST_DICT_VALUES, E_EOF);
-        return;
-      }
-      int32_t l = (int32_t)W.u32_at(body + pos);
-      if (l < 0) {
-        set_status(a.status, page, ST_DICT_VALUES, E_BYTE_ARRAY);
-        return;
-      }
-      if (pos + 4 + l > len) {
-        set_status(a.status, page, ST_DICT_VALUES, E_EOF);
-        return;
-      }
-      if (lane == j) mine = ((uint64_t)(pos + 4) << 32) | (uint32_t)l;
-      pos += 4 + l;
-    }
-    if (lane < cnt) a.dict_ent[d.dict_base + base + lane] = mine;
-  }
+  // length-prefix walk (type_bytearray.go:24-45): entry table (offset << 32 | length)
+  __shared__ BaLds ba_all[4];
+  BaLds &bl = ba_all[threadIdx.x >> 6];
+  const uint32_t e = ba_walk<BA_WIN>(body, len, n, bl.win, bl.jt[0], bl.jt[1],
+                             [&](int64_t first, int ln, int64_t voff, int32_t l, int cnt) {
+                               if (ln < cnt) a.dict_ent[d.dict_base + first + ln] = ((uint64_t)voff << 32) | (uint32_t)l;
+                             });
+  if (e) set_status(a.status, page, ST_DICT_VALUES, e);
 }
 
 // ===========================================================================
@@ -1303,7 +1376,7 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
         ok &= cand + hl + (cng - 1) * bw < slen;
       }
       const uint64_t okm = ballot(ok);
-      const int m = (int)__builtin_ctzll(~okm);  // leading accepted candidates (lanes 0..m-1)
+      const int m = ~okm ? (int)__builtin_ctzll(~okm) : 64;  // leading accepted candidates (lanes 0..m-1)
       if (m > 0) {
         if (lane < m) {
           R.runs[nr + lane] = make_uint2((uint32_t)cstart, (uint32_t)(cand + hl));
@@ -1544,27 +1617,18 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
   int64_t sbytes = 0;
   if (c.ptype == T_BYTE_ARRAY && nn > 0) {
     if (d.enc == ENC_PLAIN) {
-      Win W;
-      W.reset();
-      const uint8_t *vp = ps.body + ps.val_off;
-      int64_t pos = 0, vlen = ps.val_len;
-      for (int64_t i = 0; i < nn; i++) {
-        if (pos + 4 > vlen) {
-          set_status(a.status, page, ST_VALUES, E_EOF);
-          return;
-        }
-        int32_t l = (int32_t)W.u32_at(vp + pos);
-        if (l < 0) {
-          set_status(a.status, page, ST_VALUES, E_BYTE_ARRAY);
-          return;
-        }
-        if (pos + 4 + l > vlen) {
-          set_status(a.status, page, ST_VALUES, E_EOF);
-          return;
-        }
-        sbytes += l;
-        pos += 4 + l;
+      // length prefixes by pointer jumping (ba_walk), in the run walk's LDS
+      int64_t acc = 0;
+      const uint32_t e2 = ba_walk<448>(ps.body + ps.val_off, ps.val_len, nn, (uint32_t *)lbytes, lnx, lnx + 456,
+                                       [&](int64_t, int ln, int64_t, int32_t l, int cnt) {
+                                         const int64_t t = wave_incl_scan64(ln < cnt ? (int64_t)l : 0);
+                                         acc += (int64_t)ufirst64((int64_t)shfl64((uint64_t)t, 63));
+                                       });
+      if (e2) {
+        set_status(a.status, page, ST_VALUES, e2);
+        return;
       }
+      sbytes = acc;
     } else if (d.enc == ENC_RLE_DICT) {
       if (d.dict < 0) {
         // dictDecoder with no dictionary: the first key is out of range
