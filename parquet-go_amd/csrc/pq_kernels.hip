@@ -1841,6 +1841,40 @@ __device__ __forceinline__ uint64_t pick4_64(const uint64_t (&v)[4], int j) {
   return ((uint64_t)pick4(hi, j) << 32) | pick4(lo, j);
 }
 
+// One lane's string bytes [sp, sp + len) -> [op, op + len), a range no other
+// lane writes: byte head up to a dword-aligned destination, then 16 bytes a
+// pass from five dword loads issued together (v_alignbyte by the source skew),
+// whole dwords stored, the last partial dword bytewise.  Source reads run up
+// to 20 bytes past the string (device buffers carry kPad readable slack).
+__device__ __forceinline__ void copy_str(const uint8_t *sp, uint8_t *op, int64_t len) {
+  int64_t h = (int64_t)((4 - ((uintptr_t)op & 3)) & 3);
+  if (h > len) h = len;
+  for (int64_t b = 0; b < h; b++) op[b] = sp[b];
+  const uintptr_t sa = (uintptr_t)(sp + h);
+  const uint32_t *q = (const uint32_t *)(sa & ~(uintptr_t)3);
+  const uint32_t sk = (uint32_t)(sa & 3);
+  uint32_t *o = (uint32_t *)(op + h);
+  int64_t rem = len - h;
+  while (rem > 0) {
+    uint32_t w[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) w[i] = q[i];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint32_t x = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sk);
+      const int64_t r = rem - 4 * i;
+      if (r >= 4) o[i] = x;
+      else if (r > 0) {
+        uint8_t *ob = (uint8_t *)(o + i);
+        for (int j = 0; j < (int)r; j++) ob[j] = (uint8_t)(x >> (8 * j));
+      }
+    }
+    q += 4;
+    o += 4;
+    rem -= 16;
+  }
+}
+
 // Decode one data page with one wavefront, 256 level entries per step, four
 // consecutive entries per lane (page_v1.go:27-55 readValues + data_store.go
 // semantics for validity / list offsets).  For flat columns the steps are
@@ -1892,8 +1926,8 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
     const uint32_t sz = load_u32_unaligned(vals);
     keys.init(vals + 4, min<int64_t>((int64_t)sz, vlen - 4), 1);
   }
-  Win SW;  // string-length window (PLAIN BYTE_ARRAY)
-  SW.reset();
+  __shared__ BaLds ba_all[4];  // PLAIN BYTE_ARRAY length walk, one per wave
+  BaLds &bl = ba_all[threadIdx.x >> 6];
   int64_t spos = 0;
   // DELTA strings: lengths decoded and validated by k_prepare (scratch); suffix
   // bytes start at str_data.  DELTA_BYTE_ARRAY bytes are written by k_dba.
@@ -2136,35 +2170,30 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
         }
         sbase_ptr = vals;
       } else if (d.enc == ENC_PLAIN && is_ba) {
-        // serial length walk (type_bytearray.go:24-45); value j -> lane j>>2, element j&3
+        // length chain (type_bytearray.go:24-45) by pointer jumping, 64 entries a
+        // batch; entry j of the step goes to lane j>>2, element j&3
         uint32_t eo[4] = {0, 0, 0, 0}, el[4] = {0, 0, 0, 0};
-        for (int j = 0; j < m; j++) {
-          if (spos + 4 > vlen) {
-            err = E_EOF;
-            break;
-          }
-          int32_t l = (int32_t)SW.u32_at(vals + spos);
-          if (l < 0) {
-            err = E_BYTE_ARRAY;
-            break;
-          }
-          if (spos + 4 + l > vlen) {
-            err = E_EOF;
-            break;
-          }
-          if (lane == (j >> 2)) {
-            int k = j & 3;
-            if (k == 0) { eo[0] = (uint32_t)(spos + 4); el[0] = (uint32_t)l; }
-            else if (k == 1) { eo[1] = (uint32_t)(spos + 4); el[1] = (uint32_t)l; }
-            else if (k == 2) { eo[2] = (uint32_t)(spos + 4); el[2] = (uint32_t)l; }
-            else { eo[3] = (uint32_t)(spos + 4); el[3] = (uint32_t)l; }
-          }
-          spos += 4 + l;
-        }
+        int64_t adv = 0;
+        err = ba_walk<BA_WIN>(vals + spos, vlen - spos, m, bl.win, bl.jt[0], bl.jt[1],
+                              [&](int64_t first, int ln, int64_t voff, int32_t l, int cnt) {
+                                const uint32_t vo = (uint32_t)(spos + voff);
+#pragma unroll
+                                for (int k = 0; k < 4; k++) {
+                                  const int src = 4 * lane + k - (int)first;
+                                  const uint32_t o2 = (uint32_t)__shfl((int)vo, src & 63);
+                                  const uint32_t l2 = (uint32_t)__shfl((int)l, src & 63);
+                                  if (src >= 0 && src < cnt) {
+                                    eo[k] = o2;
+                                    el[k] = l2;
+                                  }
+                                }
+                                adv = (int64_t)shfl64((uint64_t)(voff + l), cnt - 1);
+                              });
         if (err) {
           err_stage = ST_VALUES;
           break;
         }
+        spos += adv;
         int vi = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -2200,11 +2229,7 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
         if (slot[k]) {
           start += ll[k];
           c.str_offsets[slot_base + slot_run + sbase + si + 1] = start;
-          if (valid[k] && !defer_bytes) {
-            const uint8_t *sp = sbase_ptr + soff[k];
-            uint8_t *op = c.values + start - ll[k];
-            for (int64_t b = 0; b < ll[k]; b++) op[b] = sp[b];
-          }
+          if (valid[k] && !defer_bytes) copy_str(sbase_ptr + soff[k], c.values + start - ll[k], ll[k]);
           si++;
         }
       }
