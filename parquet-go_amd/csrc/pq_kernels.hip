@@ -1841,6 +1841,32 @@ __device__ __forceinline__ uint64_t pick4_64(const uint64_t (&v)[4], int j) {
   return ((uint64_t)pick4(hi, j) << 32) | pick4(lo, j);
 }
 
+// Bits of one step of a nested column (≤ 256 positions starting at global bit
+// b0; this lane's four at relative positions rel[k], set where on[k]) gathered
+// in LDS with ds_or, then written a word per lane: plain stores for the words
+// the step covers whole, atomicOr for the partial first/last word (shared with
+// the neighbouring step or page).  Replaces one global atomic per set bit.
+__device__ __forceinline__ void wave_bitmap(uint32_t *lw, uint32_t *gbm, int64_t b0, int total, const int (&rel)[4],
+                                            const bool (&on)[4]) {
+  const int lane = lane_id();
+  const int sh = (int)(b0 & 31);
+  const int nw = (sh + total + 31) >> 5;  // <= 9
+  if (lane < 9) lw[lane] = 0;
+  wave_lds_sync();
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    if (on[k]) atomicOr(&lw[(sh + rel[k]) >> 5], 1u << ((sh + rel[k]) & 31));
+  wave_lds_sync();
+  if (lane < nw) {
+    const uint32_t wv = lw[lane];
+    uint32_t *g = gbm + (b0 >> 5) + lane;
+    const bool edge = (lane == 0 && sh != 0) || (lane == nw - 1 && ((sh + total) & 31) != 0);
+    if (!edge) *g = wv;
+    else if (wv) atomicOr(g, wv);
+  }
+  wave_lds_sync();
+}
+
 // One lane's string bytes [sp, sp + len) -> [op, op + len), a range no other
 // lane writes: byte head up to a dword-aligned destination, then 16 bytes a
 // pass from five dword loads issued together (v_alignbyte by the source skew),
@@ -1928,6 +1954,8 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
   }
   __shared__ BaLds ba_all[4];  // PLAIN BYTE_ARRAY length walk, one per wave
   BaLds &bl = ba_all[threadIdx.x >> 6];
+  __shared__ uint32_t bmw_all[4][12];  // nested-column bitmap words of a step
+  uint32_t *bmw = bmw_all[threadIdx.x >> 6];
   int64_t spos = 0;
   // DELTA strings: lengths decoded and validated by k_prepare (scratch); suffix
   // bytes start at str_data.  DELTA_BYTE_ARRAY bytes are written by k_dba.
@@ -1984,16 +2012,20 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
     if (!flat) {  // rows start where rep == 0 (data_store.go:188-202)
       const int32_t rbase = wave_excl_scan32(nr, &mrows);
       int ri = 0, si = 0;
+      int rrel[4];
+      bool lv[4];
 #pragma unroll
       for (int k = 0; k < 4; k++) {
+        rrel[k] = rbase + ri;
+        lv[k] = act[k] && r[k] == 0 && (int)dl[k] >= c.rep_def - 1;
         if (act[k] && r[k] == 0) {
           int64_t row = pi.row_base + row_run + rbase + ri;
           c.list_offsets[row] = (int32_t)(slot_base + slot_run + sbase + si);
-          if ((int)dl[k] >= c.rep_def - 1) atomicOr(&c.list_validity[row >> 5], 1u << (row & 31));
           ri++;
         }
         si += slot[k];
       }
+      if (c.list_validity) wave_bitmap(bmw, c.list_validity, pi.row_base + row_run, mrows, rrel, lv);
       row_run += mrows;
     }
 
@@ -2299,15 +2331,15 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
           }
         }
       } else {
-        int si = 0;
+        int si = 0, srel[4];
+        bool sv[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-          if (slot[k]) {
-            int64_t sl = slot_base + slot_run + sbase + si;
-            if (valid[k]) atomicOr(&c.validity[sl >> 5], 1u << (sl & 31));
-            si++;
-          }
+          srel[k] = sbase + si;
+          sv[k] = slot[k] && valid[k];
+          si += slot[k];
         }
+        wave_bitmap(bmw, c.validity, slot_base + slot_run, mslots, srel, sv);
       }
     }
     slot_run += mslots;
