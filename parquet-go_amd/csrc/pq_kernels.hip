@@ -911,11 +911,14 @@ __global__ __launch_bounds__(256) void k_reset(KArgs a) {
 // error in entry order: E_EOF (header or bytes past the stream), E_BYTE_ARRAY
 // (negative length), or E_OK.
 // ===========================================================================
-constexpr int BA_WIN = 1024;  // k_dict_prepare's window (k_prepare: 448, in its run-walk LDS)
-struct BaLds {
-  uint32_t win[BA_WIN / 4 + 8];
-  uint16_t jt[2][BA_WIN + 8];
+constexpr int BA_WIN = 1024;       // k_decode's window (k_prepare: 960, in its run-walk LDS)
+constexpr int BA_WIN_DICT = 2048;  // k_dict_prepare: ~64 entries a batch for ~27-byte strings
+template <int W>
+struct BaLdsT {
+  uint32_t win[W / 4 + 8];
+  uint16_t jt[2][W + 8];
 };
+using BaLds = BaLdsT<BA_WIN>;
 
 template <int WINB, class Emit>
 __device__ __forceinline__ uint32_t ba_walk(const uint8_t *vp, int64_t vlen, int64_t n, uint32_t *win, uint16_t *ja0,
@@ -1008,9 +1011,9 @@ __global__ __launch_bounds__(256) void k_dict_prepare(KArgs a) {
     return;
   }
   // length-prefix walk (type_bytearray.go:24-45): entry table (offset << 32 | length)
-  __shared__ BaLds ba_all[4];
-  BaLds &bl = ba_all[threadIdx.x >> 6];
-  const uint32_t e = ba_walk<BA_WIN>(body, len, n, bl.win, bl.jt[0], bl.jt[1],
+  __shared__ BaLdsT<BA_WIN_DICT> ba_all[4];
+  BaLdsT<BA_WIN_DICT> &bl = ba_all[threadIdx.x >> 6];
+  const uint32_t e = ba_walk<BA_WIN_DICT>(body, len, n, bl.win, bl.jt[0], bl.jt[1],
                              [&](int64_t first, int ln, int64_t voff, int32_t l, int cnt) {
                                if (ln < cnt) a.dict_ent[d.dict_base + first + ln] = ((uint64_t)voff << 32) | (uint32_t)l;
                              });
@@ -1588,29 +1591,34 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
   rep.init(ps.lvl + ps.rep_off, ps.rep_len, bits_len(c.max_rep));
   def.init(ps.lvl + ps.def_off, ps.def_len, bits_len(c.max_def));
   int64_t rows = 0, slots = 0, nn = 0;
-  for (int e0 = 0; e0 < n && c.max_rep > 0; e0 += 64) {
-    int cnt = min(64, n - e0);
-    uint32_t r;
-    e = rep.next(cnt, r);
+  // 256 entries a round, four per lane (entry 4 * lane + k in element k)
+  for (int e0 = 0; e0 < n && c.max_rep > 0; e0 += 256) {
+    const int cnt = min(256, n - e0);
+    uint32_t r[4];
+    e = rep.next4(cnt, r);
     if (e) {
       set_status(a.status, page, ST_REP, e);
       return;
     }
-    rows += __popcll(ballot(lane < cnt && r == 0));
+#pragma unroll
+    for (int k = 0; k < 4; k++) rows += __popcll(ballot(4 * lane + k < cnt && r[k] == 0));
   }
-  for (int e0 = 0; e0 < n; e0 += 64) {
-    int cnt = min(64, n - e0);
-    uint32_t dl = 0;
+  for (int e0 = 0; e0 < n; e0 += 256) {
+    const int cnt = min(256, n - e0);
+    uint32_t dl[4] = {0, 0, 0, 0};
     if (c.max_def > 0) {
-      e = def.next(cnt, dl);
+      e = def.next4(cnt, dl);
       if (e) {
         set_status(a.status, page, ST_DEF, e);
         return;
       }
     }
-    bool act = lane < cnt;
-    nn += __popcll(ballot(act && (int)dl == c.max_def));
-    slots += __popcll(ballot(act && (c.max_rep == 0 || (int)dl >= c.rep_def)));
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const bool act = 4 * lane + k < cnt;
+      nn += __popcll(ballot(act && (int)dl[k] == c.max_def));
+      slots += __popcll(ballot(act && (c.max_rep == 0 || (int)dl[k] >= c.rep_def)));
+    }
   }
   if (c.max_rep == 0) rows = n;
   // string bytes of the non-null values
@@ -1619,7 +1627,7 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
     if (d.enc == ENC_PLAIN) {
       // length prefixes by pointer jumping (ba_walk), in the run walk's LDS
       int64_t acc = 0;
-      const uint32_t e2 = ba_walk<448>(ps.body + ps.val_off, ps.val_len, nn, (uint32_t *)lbytes, lnx, lnx + 456,
+      const uint32_t e2 = ba_walk<960>(ps.body + ps.val_off, ps.val_len, nn, (uint32_t *)lbytes, lnx, lnx + 968,
                                        [&](int64_t, int ln, int64_t, int32_t l, int cnt) {
                                          const int64_t t = wave_incl_scan64(ln < cnt ? (int64_t)l : 0);
                                          acc += (int64_t)ufirst64((int64_t)shfl64((uint64_t)t, 63));
@@ -1720,7 +1728,7 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
 template <int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_prepare(KArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t wl_bytes[4][1024];  // run walk: window bytes
-  __shared__ __attribute__((aligned(16))) uint16_t wl_nx[4][1024];    // run walk: chain table
+  __shared__ __attribute__((aligned(16))) uint16_t wl_nx[4][2048];    // run walk: chain table (BYTE_ARRAY walk: two)
   const int wv = (int)ufirst(threadIdx.x >> 6);
   prepare_page(a, (int)blockIdx.x * 4 + wv, wl_bytes[wv], wl_nx[wv], MODE);
 }
@@ -1732,7 +1740,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
 // pages that do wait are prepared by k_prepare<1> after this launch.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_prepare_copy(KArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t wl_bytes[4][1024];
-  __shared__ __attribute__((aligned(16))) uint16_t wl_nx[4][1024];
+  __shared__ __attribute__((aligned(16))) uint16_t wl_nx[4][2048];
   const uint32_t pb = ((uint32_t)a.nlist + 3) / 4;
   if (blockIdx.x < pb) {
     const int wv = (int)ufirst(threadIdx.x >> 6);
