@@ -574,7 +574,9 @@ struct pqg_batch {
   std::vector<PageDesc> pages;
   std::vector<uint32_t> status0;  // host-side initial status per page
   std::vector<int32_t> snappy_list, dict_list, data_list;
-  std::vector<int32_t> general_list;  // data pages for k_decode (wave per page)
+  std::vector<int32_t> general_list;  // data pages for k_decode (wave per page): k_decode<0> pages, then
+  std::vector<int32_t> general_flat;  // k_decode<1> pages (appended to general_list after planning)
+  int32_t ngen_flat = 0;
   std::vector<int32_t> dba_list;      // DELTA_BYTE_ARRAY pages: value bytes by k_dba
   bool data_may_defer = false;        // some data page's Snappy body may hold a deferred literal
   std::vector<TileJob> tiles;         // k_expand work list (XCD-affine order)
@@ -1368,7 +1370,12 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
                  L.physical_type != T_BYTE_ARRAY && !(cp.flags & COL_EMIT_LEVELS) &&
                  (d.enc == ENC_PLAIN || d.enc == ENC_RLE_DICT);
     if (!tiled) {
-      B->general_list.push_back(pi);
+      // flat fixed-width pages (DELTA, nullable, PLAIN inside non-tiled
+      // columns) go to the k_decode<1> instance, the rest to k_decode<0>
+      const bool flat_fw = L.max_rep == 0 && (L.value_width == 4 || L.value_width == 8) &&
+                           L.physical_type != T_BYTE_ARRAY && L.physical_type != T_BOOLEAN &&
+                           !(cp.flags & COL_EMIT_LEVELS);
+      (flat_fw ? B->general_flat : B->general_list).push_back(pi);
       if (L.physical_type == T_BYTE_ARRAY && d.enc == ENC_DELTA_BA) B->dba_list.push_back(pi);
       continue;
     }
@@ -1601,6 +1608,9 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   if (npages) HIPCHK(hipMemcpy(B->d_pages, B->pages.data(), sizeof(PageDesc) * npages, hipMemcpyHostToDevice));
   // pages that fail before k_prepare contribute zero counts to the scans
   if (npages) HIPCHK(hipMemset(B->d_info, 0, sizeof(PageInfo) * npages));
+  B->ngen_flat = (int32_t)B->general_flat.size();
+  B->general_list.insert(B->general_list.end(), B->general_flat.begin(), B->general_flat.end());
+  B->general_flat.clear();
   {
     std::vector<int32_t> lists;
     lists.insert(lists.end(), B->snappy_list.begin(), B->snappy_list.end());
@@ -1813,8 +1823,11 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   mark(true);
   if (!upto_scan) {
     a.list = B->d_lists + ns + nd + ndata;
-    a.nlist = ngen;
-    e |= pq_launch(3, &a, s);
+    a.nlist = ngen - B->ngen_flat;
+    e |= pq_launch(3, &a, s);  // k_decode<0>: strings, lists, booleans, level output
+    a.list = B->d_lists + ns + nd + ndata + (ngen - B->ngen_flat);
+    a.nlist = B->ngen_flat;
+    e |= pq_launch(14, &a, s);  // k_decode<1>: flat fixed-width pages
     if (!B->dba_list.empty()) {  // DELTA_BYTE_ARRAY value bytes (after k_decode's offsets)
       a.list = B->d_lists + ns + nd + ndata + ngen;
       a.nlist = (int32_t)B->dba_list.size();

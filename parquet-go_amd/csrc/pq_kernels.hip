@@ -1914,6 +1914,7 @@ __device__ __forceinline__ void copy_str(const uint8_t *sp, uint8_t *op, int64_t
 // semantics for validity / list offsets).  For flat columns the steps are
 // aligned to 256 output slots so each lane owns a 16-byte-aligned slice of
 // the values and whole validity words.
+template <int FLATFW>
 __global__ __launch_bounds__(256) void k_decode(KArgs a) {
   const int gi = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
   if (gi >= a.nlist) return;
@@ -1931,8 +1932,13 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
   const uint8_t *vals = body_ptr(a, d, page) + pi.val_off;
   const int64_t vlen = pi.val_len;
   const int w = c.width;
-  const bool flat = c.max_rep == 0;
-  const bool is_ba = c.ptype == T_BYTE_ARRAY;
+  // FLATFW: the host routes only flat, fixed-width (4/8-byte) non-BOOLEAN
+  // columns here (no level output), so the string / list / boolean paths
+  // drop out of this instance and its register budget
+  const bool flat = FLATFW || c.max_rep == 0;
+  const bool is_ba = !FLATFW && c.ptype == T_BYTE_ARRAY;
+  const bool is_bool = !FLATFW && c.ptype == T_BOOLEAN;
+  const bool emit_lv = !FLATFW && (c.flags & COL_EMIT_LEVELS);
 
   Hyb rep, def;
   rep.init(lvl + pi.rep_off, pi.rep_len, bits_len(c.max_rep));
@@ -1954,7 +1960,7 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
   } else if (d.enc == ENC_DELTA_BP) {
     dz.init(vals, vlen, c.ptype == T_INT32);
     delta_prev = (uint64_t)dz.first;
-  } else if (d.enc == ENC_RLE && c.ptype == T_BOOLEAN) {
+  } else if (d.enc == ENC_RLE && is_bool) {
     // booleanRLEDecoder (type_boolean.go:97-117): u32 size, then a bit width 1
     // hybrid stream limited to it (checked >= 4 bytes in k_prepare)
     const uint32_t sz = load_u32_unaligned(vals);
@@ -1978,7 +1984,7 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
   while (e0 < n) {
     const int cnt = (int)min<int64_t>(n - e0, flat ? 256 - ((slot_base + e0) & 255) : 256);
     uint32_t r[4] = {0, 0, 0, 0}, dl[4] = {0, 0, 0, 0};
-    if (c.max_rep > 0) {
+    if (!flat) {
       err = rep.next4(cnt, r);
       if (err) {
         err_stage = ST_REP;
@@ -2009,7 +2015,7 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
     if (flat) mslots = cnt;
     const bool dense = m == cnt;  // no nulls in this step: entry j is dense value j
 
-    if (c.flags & COL_EMIT_LEVELS) {
+    if (emit_lv) {
 #pragma unroll
       for (int k = 0; k < 4; k++)
         if (act[k]) {
@@ -2042,7 +2048,7 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
     int64_t soff[4] = {0, 0, 0, 0}, slen[4] = {0, 0, 0, 0};
     const uint8_t *sbase_ptr = nullptr;
     if (m > 0) {
-      if (c.ptype == T_BOOLEAN) {
+      if (is_bool) {
         uint32_t bv[4] = {0, 0, 0, 0};
         if (d.enc == ENC_RLE) {  // type_boolean.go:106-117
           uint32_t kk[4];
@@ -2300,7 +2306,7 @@ __global__ __launch_bounds__(256) void k_decode(KArgs a) {
       for (int k = 0; k < 4; k++) {
         if (slot[k]) {
           int64_t sl = slot_base + slot_run + sbase + si;
-          if (c.ptype == T_BOOLEAN) c.values[sl] = valid[k] ? (uint8_t)v[k] : (uint8_t)0;
+          if (is_bool) c.values[sl] = valid[k] ? (uint8_t)v[k] : (uint8_t)0;
           else if (w == 4) *(uint32_t *)(c.values + sl * 4) = valid[k] ? (uint32_t)v[k] : 0u;
           else if (w == 8) *(uint64_t *)(c.values + sl * 8) = valid[k] ? v[k] : 0ull;
           else {
@@ -3225,7 +3231,8 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     case 1: hipLaunchKernelGGL(pq::k_dict_prepare, grid, block, 0, s, k); break;
     case 2: hipLaunchKernelGGL(pq::k_prepare<-1>, grid, block, 0, s, k); break;
     case 11: hipLaunchKernelGGL(pq::k_prepare<1>, grid, block, 0, s, k); break;
-    case 3: hipLaunchKernelGGL(pq::k_decode, grid, block, 0, s, k); break;
+    case 3: hipLaunchKernelGGL(pq::k_decode<0>, grid, block, 0, s, k); break;
+    case 14: hipLaunchKernelGGL(pq::k_decode<1>, grid, block, 0, s, k); break;
     case 5: hipLaunchKernelGGL(pq::k_level_check, grid, block, 0, s, k); break;
     case 10: hipLaunchKernelGGL(pq::k_dba, grid, block, 0, s, k); break;
     default: return 1;
