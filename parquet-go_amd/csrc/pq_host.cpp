@@ -576,7 +576,8 @@ struct pqg_batch {
   std::vector<int32_t> snappy_list, dict_list, data_list;
   std::vector<int32_t> general_list;  // data pages for k_decode (wave per page): k_decode<0> pages, then
   std::vector<int32_t> general_flat;  // k_decode<1> pages (appended to general_list after planning)
-  int32_t ngen_flat = 0;
+  std::vector<int32_t> general_str;   // k_decode<2> pages (flat BYTE_ARRAY), appended after those
+  int32_t ngen_flat = 0, ngen_str = 0;
   std::vector<int32_t> dba_list;      // DELTA_BYTE_ARRAY pages: value bytes by k_dba
   bool data_may_defer = false;        // some data page's Snappy body may hold a deferred literal
   std::vector<TileJob> tiles;         // k_expand work list (XCD-affine order)
@@ -1375,7 +1376,8 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
       const bool flat_fw = L.max_rep == 0 && (L.value_width == 4 || L.value_width == 8) &&
                            L.physical_type != T_BYTE_ARRAY && L.physical_type != T_BOOLEAN &&
                            !(cp.flags & COL_EMIT_LEVELS);
-      (flat_fw ? B->general_flat : B->general_list).push_back(pi);
+      const bool flat_ba = L.max_rep == 0 && L.physical_type == T_BYTE_ARRAY && !(cp.flags & COL_EMIT_LEVELS);
+      (flat_fw ? B->general_flat : flat_ba ? B->general_str : B->general_list).push_back(pi);
       if (L.physical_type == T_BYTE_ARRAY && d.enc == ENC_DELTA_BA) B->dba_list.push_back(pi);
       continue;
     }
@@ -1611,6 +1613,9 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   B->ngen_flat = (int32_t)B->general_flat.size();
   B->general_list.insert(B->general_list.end(), B->general_flat.begin(), B->general_flat.end());
   B->general_flat.clear();
+  B->ngen_str = (int32_t)B->general_str.size();
+  B->general_list.insert(B->general_list.end(), B->general_str.begin(), B->general_str.end());
+  B->general_str.clear();
   {
     std::vector<int32_t> lists;
     lists.insert(lists.end(), B->snappy_list.begin(), B->snappy_list.end());
@@ -1822,12 +1827,30 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   if (B->any_count) e |= pq_launch(4, &a, s);  // scans only feed lists / strings
   mark(true);
   if (!upto_scan) {
+    // the three k_decode instances run side by side: <1> and <2> on side
+    // streams forked here, joined before anything reads their output
+    const int32_t ng0 = ngen - B->ngen_flat - B->ngen_str;
+    pqg_ctx *ctx = B->ctx;
+    const bool fork = B->ngen_flat > 0 || B->ngen_str > 0;
+    if (fork) hipEventRecord(ctx->fork, s);
+    if (B->ngen_flat > 0) {
+      hipStreamWaitEvent(ctx->side[0], ctx->fork, 0);
+      a.list = B->d_lists + ns + nd + ndata + ng0;
+      a.nlist = B->ngen_flat;
+      e |= pq_launch(14, &a, ctx->side[0]);  // k_decode<1>: flat fixed-width pages
+      hipEventRecord(ctx->join[0], ctx->side[0]);
+    }
+    if (B->ngen_str > 0) {
+      hipStreamWaitEvent(ctx->side[1], ctx->fork, 0);
+      a.list = B->d_lists + ns + nd + ndata + ng0 + B->ngen_flat;
+      a.nlist = B->ngen_str;
+      e |= pq_launch(15, &a, ctx->side[1]);  // k_decode<2>: flat BYTE_ARRAY pages
+      hipEventRecord(ctx->join[1], ctx->side[1]);
+    }
     a.list = B->d_lists + ns + nd + ndata;
-    a.nlist = ngen - B->ngen_flat;
-    e |= pq_launch(3, &a, s);  // k_decode<0>: strings, lists, booleans, level output
-    a.list = B->d_lists + ns + nd + ndata + (ngen - B->ngen_flat);
-    a.nlist = B->ngen_flat;
-    e |= pq_launch(14, &a, s);  // k_decode<1>: flat fixed-width pages
+    a.nlist = ng0;
+    e |= pq_launch(3, &a, s);  // k_decode<0>: lists, booleans, level output
+    if (B->ngen_str > 0) hipStreamWaitEvent(s, ctx->join[1], 0);
     if (!B->dba_list.empty()) {  // DELTA_BYTE_ARRAY value bytes (after k_decode's offsets)
       a.list = B->d_lists + ns + nd + ndata + ngen;
       a.nlist = (int32_t)B->dba_list.size();
@@ -1835,6 +1858,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     }
     a.nlist = (int32_t)B->tiles.size();
     e |= pq_launch(9, &a, s);  // k_expand_mix (tiled pages)
+    if (B->ngen_flat > 0) hipStreamWaitEvent(s, ctx->join[0], 0);
     mark(true);
     a.list = B->d_lists + ns + nd;
     a.nlist = ndata;
