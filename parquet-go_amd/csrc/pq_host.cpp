@@ -577,7 +577,8 @@ struct pqg_batch {
   std::vector<int32_t> general_list;  // data pages for k_decode (wave per page): k_decode<0> pages, then
   std::vector<int32_t> general_flat;  // k_decode<1> pages (appended to general_list after planning)
   std::vector<int32_t> general_str;   // k_decode<2> pages (flat BYTE_ARRAY), appended after those
-  int32_t ngen_flat = 0, ngen_str = 0;
+  std::vector<int32_t> general_nest;  // k_decode<3> pages (lists of fixed-width values), appended last
+  int32_t ngen_flat = 0, ngen_str = 0, ngen_nest = 0;
   std::vector<int32_t> dba_list;      // DELTA_BYTE_ARRAY pages: value bytes by k_dba
   bool data_may_defer = false;        // some data page's Snappy body may hold a deferred literal
   std::vector<TileJob> tiles;         // k_expand work list (XCD-affine order)
@@ -1377,7 +1378,14 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
                            L.physical_type != T_BYTE_ARRAY && L.physical_type != T_BOOLEAN &&
                            !(cp.flags & COL_EMIT_LEVELS);
       const bool flat_ba = L.max_rep == 0 && L.physical_type == T_BYTE_ARRAY && !(cp.flags & COL_EMIT_LEVELS);
-      (flat_fw ? B->general_flat : flat_ba ? B->general_str : B->general_list).push_back(pi);
+      const bool nest_fw = L.max_rep > 0 && (L.value_width == 4 || L.value_width == 8) &&
+                           L.physical_type != T_BYTE_ARRAY && L.physical_type != T_BOOLEAN &&
+                           !(cp.flags & COL_EMIT_LEVELS);
+      (flat_fw   ? B->general_flat
+       : flat_ba ? B->general_str
+       : nest_fw ? B->general_nest
+                 : B->general_list)
+          .push_back(pi);
       if (L.physical_type == T_BYTE_ARRAY && d.enc == ENC_DELTA_BA) B->dba_list.push_back(pi);
       continue;
     }
@@ -1616,6 +1624,9 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   B->ngen_str = (int32_t)B->general_str.size();
   B->general_list.insert(B->general_list.end(), B->general_str.begin(), B->general_str.end());
   B->general_str.clear();
+  B->ngen_nest = (int32_t)B->general_nest.size();
+  B->general_list.insert(B->general_list.end(), B->general_nest.begin(), B->general_nest.end());
+  B->general_nest.clear();
   {
     std::vector<int32_t> lists;
     lists.insert(lists.end(), B->snappy_list.begin(), B->snappy_list.end());
@@ -1829,9 +1840,9 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   if (!upto_scan) {
     // the three k_decode instances run side by side: <1> and <2> on side
     // streams forked here, joined before anything reads their output
-    const int32_t ng0 = ngen - B->ngen_flat - B->ngen_str;
+    const int32_t ng0 = ngen - B->ngen_flat - B->ngen_str - B->ngen_nest;
     pqg_ctx *ctx = B->ctx;
-    const bool fork = B->ngen_flat > 0 || B->ngen_str > 0;
+    const bool fork = B->ngen_flat > 0 || B->ngen_str > 0 || B->ngen_nest > 0;
     if (fork) hipEventRecord(ctx->fork, s);
     if (B->ngen_flat > 0) {
       hipStreamWaitEvent(ctx->side[0], ctx->fork, 0);
@@ -1847,9 +1858,16 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
       e |= pq_launch(15, &a, ctx->side[1]);  // k_decode<2>: flat BYTE_ARRAY pages
       hipEventRecord(ctx->join[1], ctx->side[1]);
     }
+    if (B->ngen_nest > 0) {
+      hipStreamWaitEvent(ctx->side[2], ctx->fork, 0);
+      a.list = B->d_lists + ns + nd + ndata + ng0 + B->ngen_flat + B->ngen_str;
+      a.nlist = B->ngen_nest;
+      e |= pq_launch(16, &a, ctx->side[2]);  // k_decode<3>: lists of fixed-width values
+      hipEventRecord(ctx->join[2], ctx->side[2]);
+    }
     a.list = B->d_lists + ns + nd + ndata;
     a.nlist = ng0;
-    e |= pq_launch(3, &a, s);  // k_decode<0>: lists, booleans, level output
+    e |= pq_launch(3, &a, s);  // k_decode<0>: lists of strings, booleans, level output
     if (B->ngen_str > 0) hipStreamWaitEvent(s, ctx->join[1], 0);
     if (!B->dba_list.empty()) {  // DELTA_BYTE_ARRAY value bytes (after k_decode's offsets)
       a.list = B->d_lists + ns + nd + ndata + ngen;
@@ -1859,6 +1877,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     a.nlist = (int32_t)B->tiles.size();
     e |= pq_launch(9, &a, s);  // k_expand_mix (tiled pages)
     if (B->ngen_flat > 0) hipStreamWaitEvent(s, ctx->join[0], 0);
+    if (B->ngen_nest > 0) hipStreamWaitEvent(s, ctx->join[2], 0);
     mark(true);
     a.list = B->d_lists + ns + nd;
     a.nlist = ndata;

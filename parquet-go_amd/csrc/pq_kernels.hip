@@ -1914,8 +1914,8 @@ __device__ __forceinline__ void copy_str(const uint8_t *sp, uint8_t *op, int64_t
 // semantics for validity / list offsets).  For flat columns the steps are
 // aligned to 256 output slots so each lane owns a 16-byte-aligned slice of
 // the values and whole validity words.
-template <int FLATFW>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLATFW == 2 ? 3 : 1))) void k_decode(KArgs a) {
+template <int KIND>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 2 ? 3 : KIND == 3 ? 4 : 1))) void k_decode(KArgs a) {
   const int gi = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
   if (gi >= a.nlist) return;
   const int lane = lane_id();
@@ -1932,13 +1932,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLATFW == 2
   const uint8_t *vals = body_ptr(a, d, page) + pi.val_off;
   const int64_t vlen = pi.val_len;
   const int w = c.width;
-  // FLATFW 1: the host routes only flat, fixed-width (4/8-byte) non-BOOLEAN
-  // columns here, 2: only flat BYTE_ARRAY columns (neither with level
-  // output), so the other paths drop out of the instance and its registers
-  const bool flat = FLATFW || c.max_rep == 0;
-  const bool is_ba = FLATFW == 2 || (FLATFW == 0 && c.ptype == T_BYTE_ARRAY);
-  const bool is_bool = !FLATFW && c.ptype == T_BOOLEAN;
-  const bool emit_lv = !FLATFW && (c.flags & COL_EMIT_LEVELS);
+  // KIND (the host routes pages by column class, none with level output but
+  // KIND 0): 1 flat fixed-width (4/8-byte, non-BOOLEAN), 2 flat BYTE_ARRAY,
+  // 3 nested (lists) of fixed-width values, 0 everything else.  The other
+  // paths drop out of each instance and its register budget.
+  const bool flat = KIND == 1 || KIND == 2 || (KIND == 0 && c.max_rep == 0);
+  const bool is_ba = KIND == 2 || (KIND == 0 && c.ptype == T_BYTE_ARRAY);
+  const bool is_bool = KIND == 0 && c.ptype == T_BOOLEAN;
+  const bool emit_lv = KIND == 0 && (c.flags & COL_EMIT_LEVELS);
 
   Hyb rep, def;
   rep.init(lvl + pi.rep_off, pi.rep_len, bits_len(c.max_rep));
@@ -1957,7 +1958,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLATFW == 2
       dict_n = dp->num_values;
       dict_base = dp->dict_base;
     }
-  } else if (FLATFW != 2 && d.enc == ENC_DELTA_BP) {
+  } else if (KIND != 2 && d.enc == ENC_DELTA_BP) {
     dz.init(vals, vlen, c.ptype == T_INT32);
     delta_prev = (uint64_t)dz.first;
   } else if (d.enc == ENC_RLE && is_bool) {
@@ -2144,7 +2145,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FLATFW == 2
             }
           }
         sbase_ptr = dict_vals;
-      } else if (FLATFW != 2 && d.enc == ENC_DELTA_BP) {
+      } else if (KIND != 2 && d.enc == ENC_DELTA_BP) {
         uint64_t dv[4];
         err = dz.next4(m, dv);
         if (err) {
@@ -3234,6 +3235,7 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     case 3: hipLaunchKernelGGL(pq::k_decode<0>, grid, block, 0, s, k); break;
     case 14: hipLaunchKernelGGL(pq::k_decode<1>, grid, block, 0, s, k); break;
     case 15: hipLaunchKernelGGL(pq::k_decode<2>, grid, block, 0, s, k); break;
+    case 16: hipLaunchKernelGGL(pq::k_decode<3>, grid, block, 0, s, k); break;
     case 5: hipLaunchKernelGGL(pq::k_level_check, grid, block, 0, s, k); break;
     case 10: hipLaunchKernelGGL(pq::k_dba, grid, block, 0, s, k); break;
     default: return 1;
