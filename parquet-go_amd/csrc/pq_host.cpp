@@ -1274,6 +1274,11 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
       if (L.physical_type == T_BYTE_ARRAY && (d.enc == ENC_DELTA_LBA || d.enc == ENC_DELTA_BA)) {
         B->pages.back().lens_base = B->lens_entries;  // suffix lengths, then prefix lengths
         B->lens_entries += 2 * (int64_t)std::max(d.num_values, 0);
+      } else if (L.physical_type == T_BYTE_ARRAY && d.enc == ENC_PLAIN && L.value_width <= 0) {
+        // PLAIN strings: k_prepare's length walk leaves each value's offset and
+        // length here for k_decode (offsets, then lengths)
+        B->pages.back().lens_base = B->lens_entries;
+        B->lens_entries += 2 * (int64_t)std::max(d.num_values, 0);
       }
     }
     if (needs_device_codec) {

@@ -1626,11 +1626,18 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
   if (c.ptype == T_BYTE_ARRAY && nn > 0) {
     if (d.enc == ENC_PLAIN) {
       // length prefixes by pointer jumping (ba_walk), in the run walk's LDS
+      // each value's (offset, length) goes to the page's scratch for k_decode
       int64_t acc = 0;
+      int32_t *SO = d.lens_base >= 0 ? a.lens + d.lens_base : nullptr;
+      const int32_t nvp = max(d.num_values, 0);
       const uint32_t e2 = ba_walk<960>(ps.body + ps.val_off, ps.val_len, nn, (uint32_t *)lbytes, lnx, lnx + 968,
-                                       [&](int64_t, int ln, int64_t, int32_t l, int cnt) {
+                                       [&](int64_t first, int ln, int64_t voff, int32_t l, int cnt) {
                                          const int64_t t = wave_incl_scan64(ln < cnt ? (int64_t)l : 0);
                                          acc += (int64_t)ufirst64((int64_t)shfl64((uint64_t)t, 63));
+                                         if (SO && ln < cnt && first + ln < nvp) {
+                                           SO[first + ln] = (int32_t)voff;
+                                           SO[nvp + first + ln] = l;
+                                         }
                                        });
       if (e2) {
         set_status(a.status, page, ST_VALUES, e2);
@@ -2212,6 +2219,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 2 ?
           if (valid[k]) {
             soff[k] = oo;
             slen[k] = ll;
+          }
+          vi += valid[k];
+        }
+        sbase_ptr = vals;
+      } else if (d.enc == ENC_PLAIN && is_ba && d.lens_base >= 0) {
+        // offsets and lengths left by k_prepare's walk (which validated the
+        // whole chain); dense value nn_run + j -> lane j>>2, element j&3
+        const int32_t nvp = max(n, 0);
+        const int32_t *SO = a.lens + d.lens_base, *SL = SO + nvp;
+        uint32_t eo[4] = {0, 0, 0, 0}, el[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int t = 4 * lane + k;
+          if (t < m) {
+            eo[k] = (uint32_t)SO[nn_run + t];
+            el[k] = (uint32_t)SL[nn_run + t];
+          }
+        }
+        int vi = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          int j = valid[k] ? vbase + vi : 0;
+          uint32_t o = dense ? eo[k] : pick4(eo, j), l = dense ? el[k] : pick4(el, j);
+          if (valid[k]) {
+            soff[k] = o;
+            slen[k] = l;
           }
           vi += valid[k];
         }
