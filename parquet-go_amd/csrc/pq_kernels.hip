@@ -1922,7 +1922,7 @@ __device__ __forceinline__ void copy_str(const uint8_t *sp, uint8_t *op, int64_t
 // aligned to 256 output slots so each lane owns a 16-byte-aligned slice of
 // the values and whole validity words.
 template <int KIND>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 2 ? 3 : KIND == 3 ? 4 : 1))) void k_decode(KArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ? 5 : KIND == 2 ? 3 : KIND == 3 ? 4 : 1))) void k_decode(KArgs a) {
   const int gi = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
   if (gi >= a.nlist) return;
   const int lane = lane_id();
