@@ -15,7 +15,19 @@ A "step" decodes every page of the rank's shard once.  For N > 1 the file holds
 N x 100M rows and each rank decodes a contiguous, byte-balanced slice of its
 row groups (pqgpu.plan_row_group_shards) on its own GPU: weak scaling, no
 collective on the data path; value = decoded bytes of all ranks / max-over-ranks
-time.
+time.  `--allgather` additionally times the optional column all-gather over
+RCCL (pqgather, never inside the timed steps).
+
+Besides the timed loop (rank 0, N = 1), outside the timed region:
+  * every pipeline phase is timed with HIP events on a second batch of the
+    same shard (PQG_SEGMENT_TIMES=1); the longest phase is `roofline`'s, with
+    its own algorithmic bytes;
+  * a `rocprofv3 --kernel-trace --stats` child run gives per-kernel average
+    durations (`config.kernel_trace_us`; `roofline.kernel` = the longest kernel
+    of that phase) and two `--pmc` child runs give FETCH_SIZE / WRITE_SIZE per
+    kernel (`roofline.traffic` for the phase's kernels);
+  * one row group is decoded again and compared bit-exactly with the oracle;
+  * the CPU oracle decodes a bounded sample of the same file (cpu_baseline).
 
 Prints ONE JSON line (rank 0).
 """
@@ -23,6 +35,7 @@ import argparse
 import ctypes
 import json
 import os
+import platform
 import sys
 import time
 
@@ -36,25 +49,72 @@ import synth  # noqa: E402  (tools/synth.py: the configs' synthetic files)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
+# pipeline phases (pqg_batch_kernel_times names with PQG_SEGMENT_TIMES=1) and
+# the kernels each one launches
+PHASE_KERNELS = {
+    "k_snappy+k_copy": ("k_snappy", "k_copy"),
+    "k_dict_prepare": ("k_dict_prepare",),
+    "k_prepare": ("k_prepare",),
+    "k_scan": ("k_scan",),
+    "k_decode+k_expand": ("k_decode", "k_expand", "k_dba"),
+    "k_level_check": ("k_level_check",),
+}
 
-def cpu_baseline(path, budget_s=10.0, threads=None, min_s=1.0):
-    """The CPU oracle (a C port of the reference read path) on a bounded sample
-    of the same file: whole row groups, one per worker thread at a time (the
-    oracle releases the GIL inside its C calls), until ~budget_s of wall time.
-    `threads` defaults to the 16-core CPU share of a GPU box."""
+
+def phase_bytes(phase, st):
+    """Algorithmic HBM bytes of one launch of a phase:
+    snappy: compressed in + uncompressed out; dictionary prepare: dictionary
+    pages in + 8-byte entries out (bounded by the page bytes); prepare: the
+    data pages' stored bytes it walks; decode: encoded pages in + B_out."""
+    return {
+        "k_snappy+k_copy": st["snappy_in_bytes"] + st["staged_bytes"],
+        "k_dict_prepare": 2 * st["dict_bytes"],
+        "k_prepare": st["input_bytes"],
+        "k_scan": 24 * st["pages"],
+        "k_decode+k_expand": st["input_bytes"] + st["output_bytes"],
+        "k_level_check": 0,
+    }[phase]
+
+
+def cpu_cores():
+    """Cores this process may use: the affinity set, capped by a cgroup CPU
+    quota when one is set (the GPU box gives each GPU a share of the host)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(p)))
+    except Exception:
+        pass
+    return (min(n, quota) if quota else n), n, quota
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_decode_rate(path, threads, budget_s, min_s=1.0):
+    """The CPU oracle (a C port of the reference read path) on whole row
+    groups of the same file, one per worker thread at a time (the oracle
+    releases the GIL inside its C calls), until ~budget_s of wall time."""
     import concurrent.futures as cf
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     data = open(path, "rb").read()
     f = oracle.File(data)
     L = oracle.lib()
-    threads = threads or min(16, os.cpu_count() or 1)
-
     leaves = range(len(f.leaves()))
 
     def one(rg):
-        # every selected leaf of the row group; output bytes as the GPU counts
-        # them (values + validity + list offsets/validity + string offsets)
+        # every leaf of the row group; output bytes as the GPU counts them
+        # (values + validity + list offsets/validity + string offsets)
         nbytes, rows = 0, f.rg_num_rows(rg)
         for leaf in leaves:
             r = ctypes.c_void_p()
@@ -73,8 +133,6 @@ def cpu_baseline(path, budget_s=10.0, threads=None, min_s=1.0):
     t0 = time.perf_counter()
     with cf.ThreadPoolExecutor(threads) as ex:
         rg = 0
-        # whole passes over the file until ~min_s of wall (>= min_s x threads
-        # CPU-seconds), stopping early at budget_s
         while time.perf_counter() - t0 < budget_s and (rg < f.num_row_groups or time.perf_counter() - t0 < min_s):
             wave = [(rg + k) % f.num_row_groups for k in range(min(threads, f.num_row_groups))]
             for nb, nr in ex.map(one, wave):
@@ -82,18 +140,41 @@ def cpu_baseline(path, budget_s=10.0, threads=None, min_s=1.0):
                 rows += nr
             rgs += len(wave)
             rg += len(wave)
-    t_total = time.perf_counter() - t0
-    return {"value": out_bytes / t_total / 1e9, "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": "oracle/pqref.c on %d threads, %d row-group decodes over the file's %d row groups (%d rows), %.1f s wall"
-                      % (threads, rgs, f.num_row_groups, rows, t_total)}
+    dt = time.perf_counter() - t0
+    return out_bytes / dt / 1e9, rgs, rows, dt, f.num_row_groups
 
 
-def pmc_traffic(args, kernels=("k_expand", "k_decode", "k_dba")):
-    """HBM bytes per launch of the decode phase from rocprofv3 PMC counters,
-    collected in separate passes (FETCH_SIZE, then WRITE_SIZE) over a short
-    child run of this same bench; MI355X_MICROARCH.md: on gfx950 FETCH_SIZE
-    reports half of a wide streaming read, so it is doubled.  None when the
-    profiler is unavailable or a pass fails."""
+def cpu_baseline(path, budget_s=8.0):
+    """CPU oracle on all usable host cores and on one core (SURVEY.md §8(d):
+    T = all host cores, plus the single-thread figure; the Go reference
+    itself cannot run here — no Go toolchain)."""
+    cores, affinity, quota = cpu_cores()
+    v, rgs, rows, dt, nrg = cpu_decode_rate(path, cores, budget_s)
+    v1, rgs1, rows1, dt1, _ = cpu_decode_rate(path, 1, budget_s / 2)
+    return {"value": round(v, 3), "unit": "GB/s", "cores": cores, "kind": "port",
+            "value_1_thread": round(v1, 3),
+            "cpu_model": cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+            "sample": "oracle/pqref.c (C port of the reference read path): %d threads, %d row-group decodes over "
+                      "the file's %d row groups (%d rows), %.1f s wall; 1 thread: %d row groups, %.1f s"
+                      % (cores, rgs, nrg, rows, dt, rgs1, dt1)}
+
+
+def _kname(s):
+    """'void pq::k_decode<2>(pq::KArgs)' -> 'k_decode<2>'"""
+    return s.split("(")[0].replace("void ", "").replace("pq::", "").strip()
+
+
+def _child_cmd(args, steps=3):
+    cmd = [sys.executable, os.path.abspath(__file__), "--child", "--steps", str(steps), "--warmup", "1",
+           "--config", args.config, "--rows", str(args.rows), "--rg-rows", str(args.rg_rows), "--bw", str(args.bw)]
+    if args.file:
+        cmd += ["--file", args.file]
+    return cmd
+
+
+def kernel_trace(args):
+    """Per-kernel average duration (us) and calls from a rocprofv3
+    --kernel-trace --stats child run of this same bench (None if unavailable)."""
     import csv
     import glob
     import shutil
@@ -101,34 +182,102 @@ def pmc_traffic(args, kernels=("k_expand", "k_decode", "k_dba")):
     import tempfile
     if not shutil.which("rocprofv3"):
         return None
-    base = [sys.executable, os.path.abspath(__file__), "--no-cpu", "--no-pmc", "--steps", "3", "--warmup", "1",
-            "--config", args.config, "--rows", str(args.rows), "--rg-rows", str(args.rg_rows), "--bw", str(args.bw)]
-    if args.file:
-        base += ["--file", args.file]
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+        cmd = ["timeout", "-s", "KILL", "150", "rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv",
+               "-d", td, "-o", "run", "--"] + _child_cmd(args)
+        try:
+            subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, check=True, timeout=180)
+        except Exception:
+            return None
+        out = {}
+        for f in glob.glob(os.path.join(td, "**", "*kernel_stats.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                name = _kname(r["Name"])
+                out[name] = {"avg_us": float(r["AverageNs"]) / 1e3, "calls": int(r["Calls"])}
+        return out or None
+
+
+def pmc_traffic(args):
+    """HBM bytes per launch of every kernel from rocprofv3 PMC counters,
+    collected in separate passes (FETCH_SIZE, then WRITE_SIZE) over a short
+    child run of this same bench; MI355X_MICROARCH.md: on gfx950 FETCH_SIZE
+    reports half of a wide streaming read, so it is doubled.  Returns
+    {kernel: {"fetch": B, "write": B}} or None."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    if not shutil.which("rocprofv3"):
+        return None
     per = {}
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
             out = os.path.join(td, ctr)
             cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", ctr, "--output-format", "csv",
-                   "-d", out, "-o", "run", "--"] + base
+                   "-d", out, "-o", "run", "--"] + _child_cmd(args)
             try:
                 subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, check=True, timeout=150)
             except Exception:
                 return None
-            vals = {}
             for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
                 for r in csv.DictReader(open(f)):
-                    if any(k in r["Kernel_Name"] for k in kernels) and r["Counter_Name"] == ctr:
-                        vals.setdefault(r["Dispatch_Id"], 0.0)
-                        vals[r["Dispatch_Id"]] += float(r["Counter_Value"])
-            if not vals:
-                return None
-            per[ctr] = sorted(vals.values())
-    # kilobytes per dispatch; one launch of the phase may be several dispatches (k_expand<4>, <8>, k_decode)
-    n_launch = 4  # 1 warmup + 3 timed steps of the child run
-    fetch = sum(per["FETCH_SIZE"]) / n_launch * 1024 * 2
-    write = sum(per["WRITE_SIZE"]) / n_launch * 1024
-    return fetch + write
+                    if r["Counter_Name"] != ctr:
+                        continue
+                    name = _kname(r["Kernel_Name"])
+                    per.setdefault(name, {}).setdefault(ctr, []).append(float(r["Counter_Value"]) * 1024)
+    res = {}
+    for name, c in per.items():
+        f, w = c.get("FETCH_SIZE", []), c.get("WRITE_SIZE", [])
+        # kilobytes per dispatch, averaged over the kernel's dispatches
+        res[name] = {"fetch": 2 * float(np.mean(f)) if f else 0.0, "write": float(np.mean(w)) if w else 0.0}
+    return res or None
+
+
+def segment_times(reader, rg0, rg1, decodes=6):
+    """Every pipeline phase timed with HIP events (PQG_SEGMENT_TIMES=1) on a
+    second batch of the same shard, outside the timed loop (each event adds a
+    launch gap, so the timed loop brackets only the decode phase)."""
+    os.environ["PQG_SEGMENT_TIMES"] = "1"
+    try:
+        b = reader.batch(rg0, rg1)
+    finally:
+        del os.environ["PQG_SEGMENT_TIMES"]
+    try:
+        b.decode()
+        b.sync()
+        b.kernel_times()
+        for _ in range(decodes):
+            b.decode()
+        b.sync()
+        return b.kernel_times()
+    finally:
+        b.close()
+
+
+def parity_check(reader, rg):
+    """Row group `rg` of the bench file decoded again on the GPU (outside the
+    timed region) and compared bit-exactly, buffer by buffer, with the oracle."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    cols = reader.Columns()
+    b = reader.batch(rg, rg + 1, list(range(len(cols))))
+    try:
+        b.decode()
+        b.sync()
+        o = oracle.File(open(reader.path, "rb").read())
+        for i, info in enumerate(cols):
+            got, want = b.column(i), o.decode(i, rg, rg + 1)
+            for k in ("values", "validity", "list_offsets", "list_validity", "str_offsets"):
+                if k == "validity" and info["max_def"] == 0:
+                    continue
+                if k in ("list_offsets", "list_validity") and info["max_rep"] != 1:
+                    continue
+                if not np.array_equal(got[k], want[k]):
+                    return "MISMATCH in row group %d leaf %s buffer %s" % (rg, info["name"], k)
+        return "bit-exact vs oracle: row group %d, %d leaves, every buffer" % (rg, len(cols))
+    finally:
+        b.close()
 
 
 def main():
@@ -140,13 +289,18 @@ def main():
     ap.add_argument("--rows", type=int, default=0, help="rows per GPU (default: the config's)")
     ap.add_argument("--rg-rows", type=int, default=0, help="rows per row group (default: the config's)")
     ap.add_argument("--file", default=None)
-    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--cpu-budget", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes behind roofline.traffic")
+    ap.add_argument("--no-prof", action="store_true", help="skip the rocprofv3 child runs (kernel trace, PMC)")
+    ap.add_argument("--no-pmc", action="store_true", help="(compat) same as --no-prof")
+    ap.add_argument("--child", action="store_true", help="internal: a profiled child run (timed loop only)")
+    ap.add_argument("--allgather", action="store_true", help="N > 1: time the optional column all-gather (RCCL)")
     ap.add_argument("--bw", type=int, default=0, help="analysis: one dictionary bit width for every row group")
     args = ap.parse_args()
     args.rows = args.rows or synth.DEFAULTS[args.config][0]
     args.rg_rows = args.rg_rows or synth.DEFAULTS[args.config][1]
+    if args.child:
+        args.no_cpu = args.no_prof = True
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -172,6 +326,7 @@ def main():
 
     ctx = pqgpu.Context(local if world > 1 else 0)
     reader = pqgpu.FileReader(path, ctx=ctx)
+    reader.path = path
     sizes = [reader.RowGroupByteSize(i) for i in range(reader.RowGroupCount())]
     rg0, rg1 = pqgpu.plan_row_group_shards(sizes, world)[rank]
     reader.batch(rg0, rg1).close()  # first use: HIP runtime and pinned ring set-up
@@ -200,8 +355,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     batch.sync()  # raises if any page failed to decode
-    # per-kernel HIP-event times recorded on the decode stream during the timed steps
-    kern = {k: [v] for k, v in batch.kernel_times().items()}
+    decode_ms = batch.kernel_times()  # HIP-event time of the decode phase during the timed steps
     out_b, in_b = stats["output_bytes"], stats["input_bytes"]
     job_out = out_b
     if dist is not None:
@@ -212,17 +366,29 @@ def main():
         nb = torch.tensor([out_b], dtype=torch.float64, device="cuda")
         dist.all_reduce(nb, op=dist.ReduceOp.SUM)  # every rank's decoded bytes
         job_out = float(nb.item())
-
     per_step = dt / args.steps
     value = job_out * args.steps / dt / 1e9
-    avg = {k: float(np.mean(v)) for k, v in kern.items()}
-    dom = max(avg, key=avg.get)
-    # algorithmic bytes per launch of each kernel
-    alg = {
-        "k_snappy+k_copy": stats["input_bytes"] + stats["staged_bytes"],     # compressed in + uncompressed out
-        "k_decode+k_expand": in_b + out_b,                                         # encoded pages in + decoded values out
-    }
-    ach = alg.get(dom, in_b + out_b) / (avg[dom] * 1e-3) / 1e9
+
+    allgather = None
+    if dist is not None and args.allgather:
+        import torch
+        import pqgather
+        dev = torch.device("cuda", local)
+        shard = pqgather.shard_tensors(batch, 0, dev)
+        torch.cuda.synchronize(dev)
+        barrier()
+        ta = time.perf_counter()
+        col = pqgather.allgather_column(shard)
+        torch.cuda.synchronize(dev)
+        ta = time.perf_counter() - ta
+        gb = sum(v.numel() * v.element_size() for v in col.values() if hasattr(v, "numel")) / 1e9
+        allgather = {"leaf": 0, "GB_per_rank": round(gb, 4), "ms": round(ta * 1e3, 3), "GBps_per_rank": round(gb / ta, 1)}
+    batch.close()
+    if args.child:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
     line = {
         "metric": "decoded GB/s (uncompressed output) per GPU + node at 1/2/4/8 MI355X, % HBM peak",
         "value": round(value, 3),
@@ -240,24 +406,57 @@ def main():
                    "rows_per_gpu": args.rows, "row_groups": [rg0, rg1],
                    "pages": stats["data_pages"], "dict_pages": stats["dict_pages"],
                    "B_in": in_b, "B_out": out_b, "staged": stats["staged_bytes"],
-                   "pipeline_hbm_frac": round((in_b + out_b) / per_step / 1e9 / HBM_PEAK_GBPS, 4),
-                   "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
+                   "snappy_in": stats["snappy_in_bytes"],
+                   "decode_phase_ms_timed": {k: round(v, 4) for k, v in decode_ms.items()},
                    # PCIe-inclusive rate (not `value`): host planning + H2D upload + one step
                    "e2e": {"batch_create_ms": round(t_create * 1e3, 2),
                            "GBps_incl_plan_and_h2d": round(out_b / (t_create + per_step) / 1e9, 1)},
                    "parallelism": "row-group shards, one process per GPU, no data-path collective"},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
-                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None},
     }
+    if allgather:
+        line["config"]["allgather"] = allgather
+    if rank == 0 and world == 1:
+        seg = segment_times(reader, rg0, rg1)
+        line["config"]["phase_ms"] = {k: round(v, 4) for k, v in seg.items()}
+        dom = max(seg, key=seg.get)
+        ach = phase_bytes(dom, stats) / (seg[dom] * 1e-3) / 1e9
+        trace = None if args.no_prof or args.no_pmc else kernel_trace(args)
+        kern = dom
+        if trace:
+            line["config"]["kernel_trace_us"] = {k: round(v["avg_us"], 2) for k, v in
+                                                 sorted(trace.items(), key=lambda kv: -kv[1]["avg_us"])}
+            mine = {k: v for k, v in trace.items() if k.startswith(PHASE_KERNELS[dom])}
+            if mine:
+                kern = max(mine, key=lambda k: mine[k]["avg_us"])
+        line["roofline"] = {"bound": "hbm", "kernel": kern, "phase": dom, "phase_ms": round(seg[dom], 4),
+                            "algorithmic_bytes": phase_bytes(dom, stats),
+                            "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                            "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                            "pipeline_frac": round((in_b + out_b) / per_step / 1e9 / HBM_PEAK_GBPS, 4)}
+        if not (args.no_prof or args.no_pmc):
+            pmc = pmc_traffic(args)
+            if pmc:
+                line["config"]["pmc_MB_per_launch"] = {k: {"fetch": round(v["fetch"] / 1e6, 1),
+                                                           "write": round(v["write"] / 1e6, 1)}
+                                                       for k, v in sorted(pmc.items())}
+                ks = [k for k in pmc if k.startswith(PHASE_KERNELS[dom])]
+                if ks:
+                    line["roofline"]["traffic"] = round(sum(pmc[k]["fetch"] + pmc[k]["write"] for k in ks) / 1e6, 1)
+                    line["roofline"]["traffic_unit"] = "MB per launch of the phase's kernels (FETCH_SIZE x 2 + WRITE_SIZE)"
+        line["config"]["parity"] = parity_check(reader, rg0)
+    if "roofline" not in line:
+        # N > 1: the decode phase, HIP events over the timed steps (per rank)
+        dms = sum(decode_ms.values())
+        if dms > 0:
+            ach = (in_b + out_b) / (dms * 1e-3) / 1e9
+            line["roofline"] = {"bound": "hbm", "kernel": "k_decode+k_expand", "phase": "k_decode+k_expand",
+                                "phase_ms": round(dms, 4), "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
+                                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                                "pipeline_frac": round((in_b + out_b) / per_step / 1e9 / HBM_PEAK_GBPS, 4)}
     if rank == 0 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(path, args.cpu_budget)
-    if rank == 0 and world == 1 and not args.no_pmc:
-        tr = pmc_traffic(args)
-        line["roofline"]["traffic"] = None if tr is None else round(tr / 1e6, 1)
-        line["roofline"]["traffic_unit"] = "MB per launch (FETCH_SIZE x 2 + WRITE_SIZE)"
     if rank == 0:
         print(json.dumps(line), flush=True)
-    batch.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -165,6 +165,8 @@ typedef struct {
   int64_t staged_bytes;     /* uncompressed bytes the snappy kernel writes to HBM staging */
   int64_t output_bytes;     /* B_out: values + validity + offsets + string bytes */
   int64_t h2d_bytes;        /* bytes uploaded by pqg_batch_create */
+  int64_t snappy_in_bytes;  /* compressed bytes of the Snappy pages (k_snappy's input) */
+  int64_t dict_bytes;       /* uncompressed bytes of the dictionary pages */
 } pqg_batch_stats;
 
 int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const int *leaves, int nleaves, int flags,

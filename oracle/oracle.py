@@ -103,7 +103,7 @@ class File:
         for i in range(lib().pqref_num_leaves(self._h)):
             L = Leaf()
             lib().pqref_leaf_info(self._h, i, ctypes.byref(L))
-            out.append({"name": L.name.decode(), "physical_type": L.physical_type,
+            out.append({"name": L.name.decode(errors="surrogateescape"), "physical_type": L.physical_type,
                         "type_length": L.type_length, "max_def": L.max_def, "max_rep": L.max_rep,
                         "rep_def": L.rep_def, "converted_type": L.converted_type,
                         "unsigned": L.unsigned_int})

@@ -67,7 +67,8 @@ struct PageDesc {
   int32_t tile_base;     // tiled page: first entry of its tile -> first-run index table
   int32_t job_base;      // tiled page: first entry of its job -> position table (page_jobs)
   int32_t alias_any;     // dictionary page: k_snappy may alias it at any alignment (LDS-group chunks)
-  int64_t lens_base;     // DELTA_(LENGTH_)BYTE_ARRAY page: its 2 x num_values length scratch (-1: none)
+  int64_t lens_base;     // BYTE_ARRAY page scratch, 2 x num_values int32 (-1: none): DELTA_(LENGTH_)BYTE_ARRAY
+                         // suffix / prefix lengths; PLAIN (offset, length) per value from k_prepare's walk
   int32_t sidx;          // index in the Snappy page list (-1: not decoded by k_snappy)
   int32_t pad2;
 };

@@ -588,6 +588,7 @@ struct pqg_batch {
   int64_t input_bytes = 0, staged_bytes = 0, h2d_bytes = 0, host_inflated = 0, dict_entries = 0;
   // device
   uint8_t *d_in = nullptr, *d_stage = nullptr;
+  uint8_t *d_in_alloc = nullptr;  // the allocation d_in lives in (PQG_DEBUG_INPUT_HIGH_WORD shifts d_in inside it)
   size_t in_alloc = 0, stage_alloc = 0;  // bytes incl. pad
   PageDesc *d_pages = nullptr;
   PageInfo *d_info = nullptr;
@@ -1303,20 +1304,10 @@ static int alloc_dev(void **p, size_t n) {
 
 static int launch_all(pqg_batch *B, bool upto_scan, bool timed);
 
-int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const int *leaves, int nleaves, int flags,
-                     pqg_batch **out) {
-  *out = nullptr;
-  if (!ctx || !f || rg_begin < 0 || rg_end > (int)f->rgs.size() || rg_begin > rg_end || nleaves < 0) {
-    set_err("bad batch arguments");
-    return PQG_ERR_ARG;
-  }
-  HIPCHK(hipSetDevice(ctx->device));
-  pqg_batch *B = new pqg_batch();
-  B->ctx = ctx;
-  B->file = f;
-  B->rg_begin = rg_begin;
-  B->rg_end = rg_end;
-  B->flags = flags;
+// Everything after the batch object exists: any failure returns a status and
+// pqg_batch_create releases the partial batch (device buffers, pinned status)
+static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const int *leaves,
+                      int nleaves, int flags) {
   {
     const char *st = getenv("PQG_SEGMENT_TIMES");
     B->seg_times = st && st[0] == '1';
@@ -1329,7 +1320,6 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   }
   for (int l : sel) {
     if (l < 0 || l >= (int)f->leaves.size()) {
-      delete B;
       set_err("leaf %d out of range", l);
       return PQG_ERR_ARG;
     }
@@ -1356,10 +1346,6 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   int64_t stage_off = 0;
   for (size_t ci = 0; ci < B->cols.size(); ci++) {
     B->cols[ci].page_begin = (int32_t)B->pages.size();
-    if (B->cols[ci].info.max_rep > 1) {
-      // deeper nesting: levels and dense values only are outside this build's layout
-      B->chunk_errors.push_back({rg_begin, B->cols[ci].leaf, -1, 0, PQG_ERR_UNSUPPORTED});
-    }
     for (int rg = rg_begin; rg < rg_end; rg++) plan_chunk(B, in, host_bodies, stage_off, (int)ci, rg);
     B->cols[ci].page_end = (int32_t)B->pages.size();
   }
@@ -1541,7 +1527,21 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   // device buffers
   int rc = 0;
   size_t in_bytes = in.n;
-  rc |= alloc_dev((void **)&B->d_in, in_bytes);
+  if (getenv("PQG_DEBUG_INPUT_HIGH_WORD") && in_bytes + kPad < (1u << 30)) {
+    // test knob: place the input buffer where every payload address has bit
+    // 31 of its low word set (an oversized allocation, d_in shifted inside
+    // it), so a 32-bit lane value widened without a uint32_t cast shows up
+    // as a wrong address (the round-1 readlane sign-extension fault)
+    rc |= alloc_dev((void **)&B->d_in_alloc, in_bytes + (size_t{1} << 32));
+    if (!rc) {
+      const uint32_t lw = (uint32_t)(uintptr_t)B->d_in_alloc;
+      const bool ok = lw >= 0x80000000u && (uint64_t)lw + in_bytes + kPad <= 0xFFFFFFFFull;
+      B->d_in = B->d_in_alloc + (ok ? 0 : (size_t)(uint32_t)(0x80000000u - lw));
+    }
+  } else {
+    rc |= alloc_dev((void **)&B->d_in, in_bytes);
+    B->d_in_alloc = B->d_in;
+  }
   rc |= alloc_dev((void **)&B->d_stage, (size_t)stage_off);
   B->in_alloc = in_bytes + kPad;
   B->stage_alloc = (size_t)stage_off + kPad;
@@ -1596,12 +1596,8 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   rc |= alloc_dev((void **)&B->d_dbg, sizeof(uint64_t) * 8 * 4 * (B->tiles.size() + 1));
   rc |= alloc_dev((void **)&B->d_dbg2, sizeof(uint64_t) * (8 * (npages + 1) + 256));
 #endif
-  if (rc) {
-    pqg_batch_destroy(B);
-    return PQG_ERR_DEVICE;
-  }
+  if (rc) return PQG_ERR_DEVICE;
   if (hipHostMalloc((void **)&B->h_status, sizeof(uint32_t) * (npages + 1), hipHostMallocDefault) != hipSuccess) {
-    pqg_batch_destroy(B);
     set_err("hipHostMalloc failed");
     return PQG_ERR_DEVICE;
   }
@@ -1655,7 +1651,9 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
     c.width = cp.info.value_width;
     c.max_def = cp.info.max_def;
     c.max_rep = cp.info.max_rep;
-    c.rep_def = cp.info.rep_def;
+    // deeper nesting (max_rep >= 2): the column store's own layout — def/rep
+    // levels and the dense values (data_store.go:15-31); a slot is a value
+    c.rep_def = cp.info.max_rep >= 2 ? cp.info.max_def : cp.info.rep_def;
     c.page_begin = cp.page_begin;
     c.page_end = cp.page_end;
     c.flags = cp.flags;
@@ -1670,10 +1668,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   if (any_count) {
     // counting pass: snappy + prepare + scan once to size list/string outputs
     rc = launch_all(B, true, false);
-    if (rc) {
-      pqg_batch_destroy(B);
-      return rc;
-    }
+    if (rc) return rc;
     HIPCHK(hipStreamSynchronize(s));
     std::vector<ColDesc> tmp(B->cols.size());
     HIPCHK(hipMemcpy(tmp.data(), B->d_cols, sizeof(ColDesc) * tmp.size(), hipMemcpyDeviceToHost));
@@ -1681,6 +1676,13 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
       B->hcols[ci].total_rows = tmp[ci].total_rows;
       B->hcols[ci].total_slots = tmp[ci].total_slots;
       B->hcols[ci].total_str = tmp[ci].total_str;
+      // list offsets are int32 (Arrow List): a batch whose element count does
+      // not fit must be split into fewer row groups
+      if (B->hcols[ci].max_rep == 1 && tmp[ci].total_slots > (int64_t)INT32_MAX) {
+        set_err("leaf %d: %lld list elements overflow int32 offsets; decode fewer row groups per batch",
+                B->cols[ci].leaf, (long long)tmp[ci].total_slots);
+        return PQG_ERR_SIZE;
+      }
     }
   }
   // outputs
@@ -1691,6 +1693,12 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
       c.total_slots = cp.levels;
       c.total_rows = cp.info.max_rep == 0 ? cp.levels : 0;
       c.total_str = 0;
+    } else if (cp.info.max_rep == 0) {
+      // a flat column's slot of level i is i (k_decode indexes its slot
+      // outputs by the page's level base): size them by the levels even when
+      // a page failed before its counts were taken (its counts are zero)
+      c.total_slots = cp.levels;
+      c.total_rows = cp.levels;
     }
     cp.slots = c.total_slots;
     cp.rows = c.total_rows;
@@ -1724,10 +1732,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
     c.def_out = (uint8_t *)cp.def_out;
     c.rep_out = (uint8_t *)cp.rep_out;
   }
-  if (rc) {
-    pqg_batch_destroy(B);
-    return PQG_ERR_DEVICE;
-  }
+  if (rc) return PQG_ERR_DEVICE;
   if (!B->cols.empty())
     HIPCHK(hipMemcpy(B->d_cols, B->hcols.data(), sizeof(ColDesc) * B->cols.size(), hipMemcpyHostToDevice));
   // k_expand jobs: output pointers now that the outputs exist
@@ -1742,7 +1747,6 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
     HIPCHK(hipMemcpy(B->d_tiles, B->tiles.data(), sizeof(TileJob) * B->tiles.size(), hipMemcpyHostToDevice));
   for (int k = 0; k < pqg_batch::kRing; k++)
     for (int i = 0; i < 8; i++) hipEventCreate(&B->ev[k][i]);
-  *out = B;
   {  // the validity bitmaps k_reset zeroes in every decode
     std::vector<ZeroRange> zr;
     for (auto &cp : B->cols) {
@@ -1760,6 +1764,29 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   }
   HIPCHK(hipDeviceSynchronize());  // null-stream set-up done before the first decode on the context stream
   phase("outputs+tables");
+  return PQG_OK;
+}
+
+int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const int *leaves, int nleaves, int flags,
+                     pqg_batch **out) {
+  *out = nullptr;
+  if (!ctx || !f || rg_begin < 0 || rg_end > (int)f->rgs.size() || rg_begin > rg_end || nleaves < 0) {
+    set_err("bad batch arguments");
+    return PQG_ERR_ARG;
+  }
+  HIPCHK(hipSetDevice(ctx->device));
+  pqg_batch *B = new pqg_batch();
+  B->ctx = ctx;
+  B->file = f;
+  B->rg_begin = rg_begin;
+  B->rg_end = rg_end;
+  B->flags = flags;
+  const int rc = batch_init(B, ctx, f, rg_begin, rg_end, leaves, nleaves, flags);
+  if (rc != PQG_OK) {
+    pqg_batch_destroy(B);
+    return rc;
+  }
+  *out = B;
   return PQG_OK;
 }
 
@@ -2033,6 +2060,9 @@ int pqg_batch_stats_get(const pqg_batch *B, pqg_batch_stats *o) {
     bin += (int64_t)d.comp_len + lsize;
   }
   o->input_bytes = bin;
+  for (int32_t pi : B->snappy_list) o->snappy_in_bytes += B->pages[(size_t)pi].comp_len;
+  for (auto &d : B->pages)
+    if (d.kind == PAGE_DICT) o->dict_bytes += d.body_len;
   int64_t bout = 0;
   for (auto &cp : B->cols) {
     bout += (int64_t)cp.values_bytes;
@@ -2085,7 +2115,7 @@ void pqg_batch_destroy(pqg_batch *B) {
     hipFree(cp.def_out);
     hipFree(cp.rep_out);
   }
-  hipFree(B->d_in);
+  hipFree(B->d_in_alloc);
   hipFree(B->d_stage);
   hipFree(B->d_pages);
   hipFree(B->d_info);

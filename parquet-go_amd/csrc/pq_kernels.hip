@@ -2042,7 +2042,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
         lv[k] = act[k] && r[k] == 0 && (int)dl[k] >= c.rep_def - 1;
         if (act[k] && r[k] == 0) {
           int64_t row = pi.row_base + row_run + rbase + ri;
-          c.list_offsets[row] = (int32_t)(slot_base + slot_run + sbase + si);
+          if (c.list_offsets) c.list_offsets[row] = (int32_t)(slot_base + slot_run + sbase + si);
           ri++;
         }
         si += slot[k];
@@ -2229,13 +2229,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
         const int32_t nvp = max(n, 0);
         const int32_t *SO = a.lens + d.lens_base, *SL = SO + nvp;
         uint32_t eo[4] = {0, 0, 0, 0}, el[4] = {0, 0, 0, 0};
+        bool oob = false;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
           const int t = 4 * lane + k;
           if (t < m) {
             eo[k] = (uint32_t)SO[nn_run + t];
             el[k] = (uint32_t)SL[nn_run + t];
+            oob |= (int64_t)eo[k] + (int64_t)el[k] > vlen;
           }
+        }
+        // the walk validated the chain: a pair outside the values section is
+        // stale scratch (never trusted for the copies below)
+        if (ballot(oob)) {
+          err = E_EOF;
+          err_stage = ST_VALUES;
+          break;
         }
         int vi = 0;
 #pragma unroll

@@ -14,8 +14,9 @@ rank the whole column, assembled in row-group order from the ranks' shards.
   (data_store.go:15-31).
 
 The collective is whatever `torch.distributed` was initialised with: RCCL over
-xGMI for device tensors ("nccl"), gloo for the CPU tests.  Time it separately
-from decode (bench.py reports it as `config.allgather`).
+xGMI for device tensors ("nccl"), gloo for the CPU tests.  It is never part of
+the decode timing: `bench.py --gpus N --allgather` times it separately after
+the timed steps and reports it as `config.allgather`.
 """
 import ctypes
 
@@ -47,11 +48,13 @@ def shard_tensors(batch, i, device):
                                ("list_offsets", pqgpu.BUF_LIST_OFFSETS, v.list_offsets, torch.int32),
                                ("list_validity", pqgpu.BUF_LIST_VALIDITY, v.list_validity, torch.uint8),
                                ("str_offsets", pqgpu.BUF_STR_OFFSETS, v.str_offsets, torch.int64)):
-        n = ctypes.c_size_t()
-        pqgpu._check(pqgpu.lib().pqg_batch_copy(batch._h, i, buf, None, 0, ctypes.byref(n)))
-        if not ptr or (n.value == 0 and name != "values"):
+        # a buffer exists when the column's schema has it (the view pointer),
+        # even when this shard holds no rows of it (an empty shard)
+        if not ptr:
             out[name] = None
             continue
+        n = ctypes.c_size_t()
+        pqgpu._check(pqgpu.lib().pqg_batch_copy(batch._h, i, buf, None, 0, ctypes.byref(n)))
         isz = torch.empty(0, dtype=dt).element_size()
         t = torch.empty(n.value // isz, dtype=dt, device=device)
         if n.value:

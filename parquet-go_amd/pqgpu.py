@@ -23,7 +23,9 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "libpqgpu.so")
+# PQGPU_LIB selects another in-tree build of the same ABI (the guarded build
+# libpqgpu_guard.so in tests/test_gpu_guard.py); default: libpqgpu.so
+_LIB_PATH = os.path.join(_HERE, os.path.basename(os.environ.get("PQGPU_LIB", "libpqgpu.so")))
 _LIB = None
 _LOCK = threading.Lock()
 
@@ -72,7 +74,7 @@ class ColumnInfo(ctypes.Structure):
                 ("value_width", ctypes.c_int32)]
 
     def as_dict(self):
-        return {f: (getattr(self, f).decode() if f == "name" else getattr(self, f)) for f, _ in self._fields_}
+        return {f: (getattr(self, f).decode(errors="surrogateescape") if f == "name" else getattr(self, f)) for f, _ in self._fields_}
 
 
 class ColumnView(ctypes.Structure):
@@ -86,7 +88,7 @@ class ColumnView(ctypes.Structure):
 class BatchStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in ("pages", "data_pages", "dict_pages", "snappy_pages",
                                               "host_inflated_pages", "input_bytes", "staged_bytes",
-                                              "output_bytes", "h2d_bytes")]
+                                              "output_bytes", "h2d_bytes", "snappy_in_bytes", "dict_bytes")]
 
 
 DECOMPRESS_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t,
@@ -99,7 +101,7 @@ def lib():
     with _LOCK:
         if _LIB is None:
             if not os.path.exists(_LIB_PATH):
-                raise RuntimeError("libpqgpu.so is not built (run `make -C parquet-go_amd/csrc`)")
+                raise RuntimeError("%s is not built (run `make -C parquet-go_amd/csrc`)" % os.path.basename(_LIB_PATH))
             L = ctypes.CDLL(_LIB_PATH)
             vp, i32, i64, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_size_t
             P = ctypes.POINTER

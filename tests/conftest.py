@@ -5,7 +5,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
-for p in (os.path.join(ROOT, "parquet-go_amd"), os.path.join(ROOT, "oracle"), ROOT):
+for p in (os.path.join(ROOT, "parquet-go_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tools"), ROOT):
     if p not in sys.path:
         sys.path.insert(0, p)
 

@@ -254,6 +254,46 @@ def test_tiled_dictionary_fallback_to_plain():
                "dict fallback")
 
 
+def test_tiled_dictionary_fallback_to_plain_strings():
+    """BYTE_ARRAY chunks whose dictionary overflows mid-way (chunk_reader.go:206-283,
+    type_bytearray.go:13-55): RLE_DICTIONARY string pages, then PLAIN string pages,
+    flat required / nullable and beside a fixed-width fallback column."""
+    pa = pytest.importorskip("pyarrow")
+    rng = np.random.default_rng(24)
+    rows = 120000
+    words = ["%08x-%s" % (v, "q" * int(v % 23)) for v in rng.integers(0, 1 << 32, rows)]
+    t = pa.table({"s": pa.array(words), "n": pa.array(words, mask=rng.random(rows) < 0.2),
+                  "i": pa.array(rng.integers(-(1 << 40), 1 << 40, rows))})
+    for ver in ("1.0", "2.0"):
+        check_file(_pq_bytes(t, compression="snappy", dictionary_pagesize_limit=48 << 10, row_group_size=50000,
+                             data_page_version=ver), "string dict fallback v" + ver)
+
+
+def _c5_bytes(tmp_path, rows, rg_rows, **kw):
+    import synth
+    path = str(tmp_path / "c5_small.parquet")
+    synth.make("c5", path, rows, rg_rows, **kw)
+    return open(path, "rb").read()
+
+
+def test_c5_lineitem_shape(tmp_path):
+    """Config C5's file shape at small scale (tools/synth.py c5: 16 leaves, 4 INT64 /
+    4 DOUBLE / 4 INT32 / 4 dictionary STRING): small dictionary pages make
+    l_comment (and the high-cardinality numeric columns) fall back from
+    RLE_DICTIONARY to PLAIN mid-chunk; every leaf bit-exact against the oracle."""
+    pytest.importorskip("pyarrow")
+    check_file(_c5_bytes(tmp_path, 90000, 30000, dictionary_pagesize_limit=64 << 10, data_page_size=256 << 10),
+               "c5 small dict")
+
+
+def test_c5_lineitem_large_string_dictionary(tmp_path):
+    """C5 with the writer's default 1 MiB dictionary limit: l_comment's
+    dictionary page holds ~30k strings (k_dict_prepare on a large string
+    dictionary) before the PLAIN fallback; 16 leaves side by side."""
+    pytest.importorskip("pyarrow")
+    check_file(_c5_bytes(tmp_path, 80000, 40000), "c5 default dict")
+
+
 def test_tiled_rle_heavy_keys():
     """Bit width 1 and 2 key streams that alternate RLE and short bit-packed
     runs (the run walk's chain mode; k_expand's general rows)."""
@@ -386,3 +426,76 @@ def test_delta_strings_corrupted_match_oracle(enc):
             p = int(rng.integers(lo + 8, hi))
             data[p] ^= int(rng.integers(1, 256))
         check_file(bytes(data), "%s corrupt %d" % (enc, trial))
+
+
+@pytest.mark.parametrize("shape", ["flat", "list"])
+def test_plain_strings_corrupted_match_oracle(shape):
+    """Seeded corruption of uncompressed PLAIN BYTE_ARRAY pages, flat and
+    list<string> (type_bytearray.go:24-45: u32 length prefixes; a negative
+    length is an error, a chain running past the page is EOF): the GPU
+    reports the oracle's first error or decodes the same bytes.  k_decode
+    reads the (offset, length) pairs k_prepare's walk left in page scratch,
+    so this pins that a failed walk never lets stale scratch through."""
+    pq = pytest.importorskip("pyarrow.parquet")
+    pa = pytest.importorskip("pyarrow")
+    rng = np.random.default_rng(44 if shape == "flat" else 45)
+    n = 4000
+    words = ["w%05d%s" % (rng.integers(0, 99999), "z" * int(rng.integers(0, 12))) for _ in range(n)]
+    if shape == "flat":
+        t = pa.table({"s": pa.array(words, mask=rng.random(n) < 0.1)})
+    else:
+        lists = [None if rng.random() < 0.05 else words[i:i + int(rng.integers(0, 4))] for i in range(0, n, 2)]
+        t = pa.table({"s": pa.array(lists, pa.list_(pa.string()))})
+    base = _pq_bytes(t, compression="none", use_dictionary=False, data_page_size=2 << 10)
+    cc = pq.ParquetFile(io.BytesIO(base)).metadata.row_group(0).column(0)
+    lo, hi = cc.data_page_offset, cc.data_page_offset + cc.total_compressed_size
+    outcomes = set()
+    for trial in range(24):
+        data = bytearray(base)
+        for _ in range(int(rng.integers(1, 4))):
+            p = int(rng.integers(lo + 8, hi))
+            data[p] ^= int(rng.integers(1, 256))
+        check_file(bytes(data), "plain strings %s corrupt %d" % (shape, trial))
+        try:
+            oracle.File(bytes(data)).decode(0)
+            outcomes.add(0)
+        except oracle.OracleError as e:
+            outcomes.add(e.code)
+    assert len(outcomes) >= 2, outcomes
+
+
+# ---------------------------------------------------------------------------
+# the reference's own vectors (tests/golden/make_ref_vectors.py)
+# ---------------------------------------------------------------------------
+import test_reference_vectors as refvec  # noqa: E402
+
+
+@pytest.mark.parametrize("name", sorted(refvec.KAT))
+def test_level_kats_gpu(name):
+    """Dremel level KATs (data_store_test.go:18-477) through libpqgpu.so: the
+    GPU's def / rep levels and dense values equal the reference's asserted
+    arrays, maxR 0, 1 and 2 alike, and every buffer equals the oracle's."""
+    data = refvec.kat_file(name)
+    rc, got, cols = gpu_decode_all(data, levels=True)
+    assert rc == 0, (name, pqgpu.last_error())
+    for leaf, c in enumerate(cols):
+        want = refvec.KAT[name]["columns"][c["name"]]
+        g = got[leaf]
+        assert g["def"].tolist() == want["def"], (name, c["name"])
+        assert g["rep"].tolist() == want["rep"], (name, c["name"])
+        assert refvec.dense_values(g, c["max_def"], c["max_rep"]) == want["values"], (name, c["name"])
+    check_file(data, "kat " + name)
+
+
+@pytest.mark.parametrize("case", refvec.CRASH, ids=[c["test"] for c in refvec.CRASH])
+def test_crash_inputs_gpu(case):
+    """The reference's fuzz-crash inputs (readAllData) through the whole GPU
+    pipeline: no fault, and the first error class equals the oracle's."""
+    data = open(os.path.join(GOLDEN, "crash", case["file"]), "rb").read()
+    kind, res = refvec.oracle_outcome(data)
+    if kind == "open_error":
+        with pytest.raises(pqgpu.PqgError) as ei:
+            pqgpu.FileReader(data)
+        assert ei.value.code == res
+        return
+    check_file(data, case["test"])

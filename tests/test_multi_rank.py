@@ -111,11 +111,22 @@ def _gather_main(rank, world, port, path, leaf, out_dir):
     r = pqgpu.FileReader(data)
     sizes = [r.RowGroupByteSize(i) for i in range(r.RowGroupCount())]
     rg0, rg1 = pqgpu.plan_row_group_shards(sizes, world)[rank]
-    got = oracle.File(data).decode(leaf, rg0, rg1)  # this rank's shard (the checker stands in for the GPU)
+    o = oracle.File(data)
+    got = o.decode(leaf, rg0, rg1)  # this rank's shard (the checker stands in for the GPU)
+    info = o.leaves()[leaf]
+    # buffers present by schema (as the GPU column view has them), even when the shard is empty
+    present = {"validity": info["max_def"] > 0, "list_offsets": info["max_rep"] == 1,
+               "list_validity": info["max_rep"] == 1, "str_offsets": info["physical_type"] == 6}
 
     def t(name, dt):
+        if not present[name]:
+            return None
         a = got[name]
-        return torch.from_numpy(a.view(dt).copy()) if a.size else None
+        if name == "list_offsets" and a.size == 0:
+            a = np.zeros(4, np.uint8)  # rows + 1 offsets of an empty shard
+        if name == "str_offsets" and a.size == 0:
+            a = np.zeros(8, np.uint8)
+        return torch.from_numpy(a.view(dt).copy())
 
     shard = {"slots": int(got["slots"]), "rows": int(got["rows"]), "values": torch.from_numpy(got["values"].copy()),
              "validity": t("validity", np.uint8), "list_offsets": t("list_offsets", np.int32),
@@ -128,7 +139,9 @@ def _gather_main(rank, world, port, path, leaf, out_dir):
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("name,leaf,world", [("c4_list_str", 0, 2), ("c4_list_str", 1, 3), ("c3_delta_v2", 1, 2),
-                                             ("plain_strings", 0, 3), ("c2_dict_bw8", 0, 2)])
+                                             ("plain_strings", 0, 3), ("c2_dict_bw8", 0, 2),
+                                             # more ranks than row groups: the last ranks hold empty shards
+                                             ("c4_list_str", 0, 4), ("gzip_int64", 0, 5)])
 def test_allgather_column_gloo(tmp_path, name, leaf, world):
     """The optional all-gather over gloo: every rank ends with
     the whole column, equal to the whole-file decode (bitmaps re-packed at odd
@@ -141,5 +154,53 @@ def test_allgather_column_gloo(tmp_path, name, leaf, world):
     got = np.load(str(tmp_path / "gathered.npz"))
     whole = oracle.File(open(path, "rb").read()).decode(leaf)
     assert int(got["slots"]) == whole["slots"] and int(got["rows"]) == whole["rows"]
+    info = oracle.File(open(path, "rb").read()).leaves()[leaf]
     for k in ("values", "validity", "list_offsets", "list_validity", "str_offsets"):
+        if k == "validity" and info["max_def"] == 0:
+            continue  # a required column has no bitmap on the GPU (the oracle's is all ones)
+        assert np.array_equal(got[k].view(np.uint8).ravel(), whole[k]), k
+
+
+def _gpu_shard_main(rank, world, port, path, leaf, out_dir):
+    import torch
+    import torch.distributed as dist
+    sys.path[:0] = [os.path.join(ROOT, "parquet-go_amd")]
+    import pqgather
+    import pqgpu
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    r = pqgpu.FileReader(path)
+    sizes = [r.RowGroupByteSize(i) for i in range(r.RowGroupCount())]
+    rg0, rg1 = pqgpu.plan_row_group_shards(sizes, world)[rank]
+    b = r.batch(rg0, rg1, [leaf])  # this rank's shard, decoded by libpqgpu.so on cuda:0
+    b.decode()
+    dev = torch.device("cuda", 0)
+    shard = pqgather.shard_tensors(b, 0, dev)  # device-to-device copies out of the batch
+    b.close()
+    host = {k: (v.cpu() if hasattr(v, "cpu") else v) for k, v in shard.items()}  # gloo gathers host tensors
+    col = pqgather.to_numpy(pqgather.allgather_column(host))
+    if rank == 0:
+        np.savez(os.path.join(out_dir, "gathered.npz"), **{k: np.asarray(v) for k, v in col.items()})
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("name,leaf,world", [("c4_list_str", 0, 2), ("c4_list_str", 1, 4), ("c3_delta_v2", 1, 2)])
+def test_gpu_shards_allgather(tmp_path, name, leaf, world):
+    """The N > 1 data path with the product decoder: each rank plans its
+    row-group shard, decodes it with libpqgpu.so on the (one) GPU, copies the
+    buffers device to device (pqgather.shard_tensors) and all-gathers them;
+    the result equals the whole-file oracle decode.  `world` ranks share
+    cuda:0 here; the 8-GPU bench runs one rank per GPU over RCCL."""
+    import torch.multiprocessing as mp
+    import oracle
+    path = os.path.join(GOLDEN, name + ".parquet")
+    mp.spawn(_gpu_shard_main, args=(world, _free_port(), path, leaf, str(tmp_path)), nprocs=world, join=True)
+    got = np.load(str(tmp_path / "gathered.npz"))
+    o = oracle.File(open(path, "rb").read())
+    whole, info = o.decode(leaf), o.leaves()[leaf]
+    assert int(got["slots"]) == whole["slots"]
+    for k in ("values", "validity", "list_offsets", "list_validity", "str_offsets"):
+        if k == "validity" and info["max_def"] == 0:
+            continue
         assert np.array_equal(got[k].view(np.uint8).ravel(), whole[k]), k

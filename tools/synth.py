@@ -52,7 +52,10 @@ def _write(path, schema, gen, rows, rg_rows, **kw):
     os.replace(tmp, path)
 
 
-def make(cfg, path, rows, rg_rows, fixed_bw=0):
+def make(cfg, path, rows, rg_rows, fixed_bw=0, **writer_kw):
+    """Write config `cfg` to `path`.  `writer_kw` overrides pyarrow writer
+    options (tests use a small dictionary_pagesize_limit to force the PLAIN
+    fallback of l_comment inside a small file)."""
     import pyarrow as pa
     import pyarrow.compute as pc
 
@@ -152,6 +155,8 @@ def make(cfg, path, rows, rg_rows, fixed_bw=0):
                 "l_comment": comment,
             }
             return pa.table(t, schema=schema)
-        _write(path, schema, gen, rows, rg_rows, compression="snappy", data_page_version="1.0")
+        kw = dict(compression="snappy", data_page_version="1.0")
+        kw.update(writer_kw)
+        _write(path, schema, gen, rows, rg_rows, **kw)
     else:
         raise ValueError("unknown config %r" % cfg)
