@@ -192,6 +192,8 @@ struct Hyb {
   uint32_t rle_val;
   int32_t bw;
   int32_t rle;
+  int32_t got;     // values the last next4 / next produced (before an error: the ones the
+                   // reference read successfully, value by value, hybrid_decoder.go:82-114)
   Win W;
 
   __device__ __forceinline__ void init(const uint8_t *ptr, int64_t n, int bitw) {
@@ -204,6 +206,7 @@ struct Hyb {
     rle_val = 0;
     bw = bitw;
     rle = 0;
+    got = 0;
     W.reset();
   }
 
@@ -243,18 +246,31 @@ struct Hyb {
 
   // Produce the next n (<= 256) values, four per lane: value j goes to lane
   // j >> 2, element j & 3.
+  // Bit-packed values [vi, vi + take) of the current run that the reference can
+  // read: every 8-value group must start inside the stream (a short last group
+  // is zero-filled, readBitPackedRun :133-141).
+  __device__ __forceinline__ int readable(int take) const {
+    const int64_t last_group = (vi + take - 1) >> 3;
+    if (data + last_group * bw < len) return take;
+    const int64_t groups = len > data ? (len - data + bw - 1) / bw : 0;  // groups starting inside
+    return (int)max<int64_t>(0, min<int64_t>((int64_t)take, groups * 8 - vi));
+  }
+
   __device__ uint32_t next4(int n, uint32_t (&out)[4]) {
     const int lane = lane_id();
 #pragma unroll
     for (int k = 0; k < 4; k++) out[k] = 0;
-    if (bw == 0) return E_OK;
-    int got = 0;
+    got = 0;
+    if (bw == 0) {
+      got = n;
+      return E_OK;
+    }
     while (got < n) {
       if (rem == 0) {
         uint32_t e = header();
         if (e) return e;
       }
-      const int take = (int)min<int64_t>(rem, (int64_t)(n - got));
+      int take = (int)min<int64_t>(rem, (int64_t)(n - got));
       if (rle) {
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -262,13 +278,16 @@ struct Hyb {
           if (j >= got && j < got + take) out[k] = rle_val;
         }
       } else {
-        int64_t last_group = (vi + take - 1) >> 3;
-        if (data + last_group * bw >= len) return E_EOF;
+        const int ok = readable(take);
         const int64_t bit0 = data * 8 + (vi - got) * (int64_t)bw;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
           int j = 4 * lane + k;
-          if (j >= got && j < got + take) out[k] = unpack_u32(p, len, bit0 + (int64_t)j * bw, bw);
+          if (j >= got && j < got + ok) out[k] = unpack_u32(p, len, bit0 + (int64_t)j * bw, bw);
+        }
+        if (ok < take) {  // a group starting at the end of the stream: io.EOF
+          got += ok;
+          return E_EOF;
         }
         vi += take;
       }
@@ -282,8 +301,11 @@ struct Hyb {
   __device__ uint32_t next(int n, uint32_t &out) {
     int lane = lane_id();
     out = 0;
-    if (bw == 0) return E_OK;  // hybrid_decoder.go:84-86
-    int got = 0;
+    got = 0;
+    if (bw == 0) {  // hybrid_decoder.go:84-86
+      got = n;
+      return E_OK;
+    }
     while (got < n) {
       if (rem == 0) {
         uint32_t e = header();
@@ -295,9 +317,12 @@ struct Hyb {
         if (mine) out = rle_val;
       } else {
         // every bit-packed group needed must start inside the stream (:133-141)
-        int64_t last_group = (vi + take - 1) >> 3;
-        if (data + last_group * bw >= len) return E_EOF;
-        if (mine) out = unpack_u32(p, len, data * 8 + (vi + (lane - got)) * (int64_t)bw, bw);
+        const int ok = readable(take);
+        if (lane >= got && lane < got + ok) out = unpack_u32(p, len, data * 8 + (vi + (lane - got)) * (int64_t)bw, bw);
+        if (ok < take) {
+          got += ok;
+          return E_EOF;
+        }
         vi += take;
       }
       rem -= take;

@@ -1523,6 +1523,15 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   B->tiles = std::move(slot_tiles);
   B->tiles.insert(B->tiles.end(), ld_tiles.begin(), ld_tiles.end());
 
+  // k_snappy takes pages in list order, one wave each: the longest bodies
+  // first (longest-processing-time order), so that the long serial token
+  // chains of big pages start with the launch instead of trailing it
+  if (!getenv("PQG_SNAPPY_LIST_ORDER")) {
+    std::stable_sort(B->snappy_list.begin(), B->snappy_list.end(), [&](int32_t x, int32_t y) {
+      return B->pages[(size_t)x].body_len > B->pages[(size_t)y].body_len;
+    });
+    for (size_t q = 0; q < B->snappy_list.size(); q++) B->pages[(size_t)B->snappy_list[q]].sidx = (int32_t)q;
+  }
   phase("plan");
   // device buffers
   int rc = 0;

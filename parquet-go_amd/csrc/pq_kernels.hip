@@ -1664,7 +1664,8 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
         uint32_t k;
         e = keys.next(cnt, k);
         if (e) {
-          set_status(a.status, page, ST_VALUES, e);
+          // keys read before the stream error are range-checked first (type_dict.go:44-53)
+          set_status(a.status, page, ST_VALUES, ballot(lane < keys.got && (int64_t)k >= dn) ? E_DICT : e);
           return;
         }
         bool act = lane < cnt;
@@ -2113,6 +2114,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
         uint32_t kk[4];
         err = keys.next4(m, kk);
         if (err) {
+          // decodeValues checks each key as it reads it (type_dict.go:44-53): an
+          // out-of-range key among those read before the stream error comes first
+          bool oob = false;
+#pragma unroll
+          for (int k = 0; k < 4; k++) oob |= 4 * lane + k < keys.got && (int64_t)kk[k] >= dict_n;
+          if (ballot(oob)) err = E_DICT;
           err_stage = ST_VALUES;
           break;
         }
