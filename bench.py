@@ -190,7 +190,11 @@ def kernel_trace(args):
         except Exception:
             return None
         out = {}
+        keep = os.environ.get("PQG_BENCH_PROF_DIR")  # keep the rocprofv3 summary (profiles/)
         for f in glob.glob(os.path.join(td, "**", "*kernel_stats.csv"), recursive=True):
+            if keep:
+                os.makedirs(keep, exist_ok=True)
+                shutil.copy(f, os.path.join(keep, "rocprof_kernel_stats_%s.csv" % args.config))
             for r in csv.DictReader(open(f)):
                 name = _kname(r["Name"])
                 out[name] = {"avg_us": float(r["AverageNs"]) / 1e3, "calls": int(r["Calls"])}

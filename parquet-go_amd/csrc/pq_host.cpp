@@ -69,8 +69,14 @@ struct pq_launch_args {
   const void *zr;
   int32_t nzr, npages;
   const uint8_t *in_end, *stage_end;  // allocation ends (incl. pad): bounds of the guarded debug build
+  const void *sitems;                 // k_snappy work items {Snappy-list position, segment}
+  int32_t nitems, nwalk;
+  const int32_t *walk, *seg_base;
+  int64_t *segs;
+  uint32_t *seg_flag;
 };
 int pq_launch(int which, const pq_launch_args *p, hipStream_t s);
+static constexpr int64_t kSnapSeg = 65536;  // pq_kernels.hip SNAP_SEG
 }
 
 namespace {
@@ -472,6 +478,7 @@ bool codec_builtin(int codec, bool *registered) {
 // ===========================================================================
 struct pqg_ctx {
   int device = 0;
+  int cus = 256;  // compute units (k_snappy's segmentation threshold)
   hipStream_t stream = nullptr;
   hipStream_t side[3] = {nullptr, nullptr, nullptr};  // concurrent size-class decode launches
   hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr};
@@ -574,6 +581,15 @@ struct pqg_batch {
   std::vector<PageDesc> pages;
   std::vector<uint32_t> status0;  // host-side initial status per page
   std::vector<int32_t> snappy_list, dict_list, data_list;
+  // Snappy segments: pages longer than kSnapSeg are decoded by one wave per
+  // 64 KiB segment (k_snappy_walk finds the segment starts)
+  std::vector<int32_t> seg_base;      // per Snappy-list position (+1): first segment
+  std::vector<int32_t> snap_items;    // {position, segment} pairs, longest first
+  std::vector<int32_t> walk_list;     // positions of the segmented pages
+  int32_t n_whole_items = 0;          // snap_items of unsegmented pages (they come first)
+  int32_t *d_sitems = nullptr, *d_seg_base = nullptr, *d_walk = nullptr;
+  int64_t *d_segs = nullptr;
+  uint32_t *d_seg_flag = nullptr;
   std::vector<int32_t> general_list;  // data pages for k_decode (wave per page): k_decode<0> pages, then
   std::vector<int32_t> general_flat;  // k_decode<1> pages (appended to general_list after planning)
   std::vector<int32_t> general_str;   // k_decode<2> pages (flat BYTE_ARRAY), appended after those
@@ -680,6 +696,8 @@ int pqg_ctx_create(int device, pqg_ctx **out) {
   HIPCHK(hipSetDevice(device));
   pqg_ctx *c = new pqg_ctx();
   c->device = device;
+  hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device);
+  if (c->cus <= 0) c->cus = 256;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     set_err("hipStreamCreate failed");
@@ -1532,6 +1550,46 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     });
     for (size_t q = 0; q < B->snappy_list.size(); q++) B->pages[(size_t)B->snappy_list[q]].sidx = (int32_t)q;
   }
+  {  // segments and k_snappy work items (PQG_SNAPPY_SEGMENTS=0: one wave per page)
+    const char *se = getenv("PQG_SNAPPY_SEGMENTS");
+    const bool use_seg = !(se && se[0] == '0');
+    // a page is cut when its serial chain would outlast the launch: its body
+    // beyond 1.5x the average body bytes per k_snappy wave slot (20 per CU),
+    // and at least 4 segments long
+    int64_t staged = 0;
+    for (int32_t pi : B->snappy_list) staged += B->pages[(size_t)pi].body_len;
+    const int64_t avg_slot = staged / std::max<int64_t>(1, (int64_t)B->ctx->cus * 20);
+    const int64_t seg_min = getenv("PQG_SNAPPY_SEG_MIN") ? std::max<int64_t>(atoll(getenv("PQG_SNAPPY_SEG_MIN")), kSnapSeg + 1)
+                                                         : std::max<int64_t>(4 * kSnapSeg, avg_slot * 3 / 2);
+    struct It {
+      int32_t q, k;
+      int64_t bytes;
+    };
+    std::vector<It> items;
+    B->seg_base.assign(B->snappy_list.size() + 1, 0);
+    for (size_t q = 0; q < B->snappy_list.size(); q++) {
+      const int64_t body = B->pages[(size_t)B->snappy_list[q]].body_len;
+      // long pages only: their serial token chains set k_snappy's critical
+      // path, while the walk that finds segment starts costs a pass over the
+      // compressed bytes (PQG_SNAPPY_SEG_MIN: the threshold, bytes)
+      const int32_t nseg = use_seg && body >= seg_min ? (int32_t)((body + kSnapSeg - 1) / kSnapSeg) : 1;
+      B->seg_base[q + 1] = B->seg_base[q] + nseg;
+      if (nseg > 1) B->walk_list.push_back((int32_t)q);
+      for (int32_t k = 0; k < nseg; k++)
+        items.push_back({(int32_t)q, k, nseg > 1 ? std::min<int64_t>(kSnapSeg, body - (int64_t)k * kSnapSeg) : body});
+    }
+    // whole pages first (one launch), then the segments (a second launch,
+    // after k_snappy_walk on a side stream): each part longest first
+    std::stable_sort(items.begin(), items.end(), [&](const It &x, const It &y) {
+      const bool sx = B->seg_base[x.q + 1] - B->seg_base[x.q] > 1, sy = B->seg_base[y.q + 1] - B->seg_base[y.q] > 1;
+      return sx != sy ? sy : x.bytes > y.bytes;
+    });
+    for (const It &it : items) {
+      B->snap_items.push_back(it.q);
+      B->snap_items.push_back(it.k);
+      if (B->seg_base[it.q + 1] - B->seg_base[it.q] == 1) B->n_whole_items++;
+    }
+  }
   phase("plan");
   // device buffers
   int rc = 0;
@@ -1596,13 +1654,26 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   rc |= alloc_dev((void **)&B->d_copy_cnt, 16);
   rc |= alloc_dev((void **)&B->d_copy_idx, 4 * (job_owner.size() + 1));
   rc |= alloc_dev((void **)&B->d_lens, 4 * (size_t)(B->lens_entries + 1));
+  rc |= alloc_dev((void **)&B->d_sitems, 4 * (B->snap_items.size() + 2));
+  rc |= alloc_dev((void **)&B->d_seg_base, 4 * B->seg_base.size());
+  rc |= alloc_dev((void **)&B->d_walk, 4 * (B->walk_list.size() + 1));
+  rc |= alloc_dev((void **)&B->d_segs, 8 * (size_t)(B->seg_base.back() + 1));
+  rc |= alloc_dev((void **)&B->d_seg_flag, 4 * (B->snappy_list.size() + 1));
+  if (!rc) {
+    if (!B->snap_items.empty())
+      hipMemcpy(B->d_sitems, B->snap_items.data(), 4 * B->snap_items.size(), hipMemcpyHostToDevice);
+    hipMemcpy(B->d_seg_base, B->seg_base.data(), 4 * B->seg_base.size(), hipMemcpyHostToDevice);
+    if (!B->walk_list.empty())
+      hipMemcpy(B->d_walk, B->walk_list.data(), 4 * B->walk_list.size(), hipMemcpyHostToDevice);
+    hipMemset(B->d_seg_flag, 0, 4 * (B->snappy_list.size() + 1));
+  }
   if (!rc) {
     hipMemset(B->d_copy_cnt, 0, 16);
     hipMemcpy(B->d_job_base, job_base.data(), 4 * job_base.size(), hipMemcpyHostToDevice);
     if (!job_owner.empty()) hipMemcpy(B->d_job_owner, job_owner.data(), 4 * job_owner.size(), hipMemcpyHostToDevice);
   }
 #ifdef PQ_STAMPS
-  rc |= alloc_dev((void **)&B->d_dbg, sizeof(uint64_t) * 8 * 4 * (B->tiles.size() + 1));
+  rc |= alloc_dev((void **)&B->d_dbg, sizeof(uint64_t) * std::max(8 * 4 * (B->tiles.size() + 1), 4 * (npages + 1)));
   rc |= alloc_dev((void **)&B->d_dbg2, sizeof(uint64_t) * (8 * (npages + 1) + 256));
 #endif
   if (rc) return PQG_ERR_DEVICE;
@@ -1854,7 +1925,38 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   mark(false);
   a.list = B->d_lists;
   a.nlist = ns;
-  e |= pq_launch(0, &a, s);
+  a.sitems = B->d_sitems;
+  a.nitems = (int32_t)(B->snap_items.size() / 2);
+  a.walk = B->d_walk;
+  a.nwalk = (int32_t)B->walk_list.size();
+  a.seg_base = B->d_seg_base;
+  a.segs = B->d_segs;
+  a.seg_flag = B->d_seg_flag;
+  {
+    // k_snappy_walk (segment starts of the long pages) and then their segments
+    // run on a side stream beside the whole pages on the context stream: the
+    // walk is a few waves of serial work that would otherwise idle the GPU
+    const int32_t nall = (int32_t)(B->snap_items.size() / 2), nwhole = B->n_whole_items;
+    pqg_ctx *ctx = B->ctx;
+    const bool side = nall > nwhole && !B->seg_times;
+    hipStream_t ss = side ? ctx->side[0] : s;
+    if (side) {
+      hipEventRecord(ctx->fork, s);
+      hipStreamWaitEvent(ss, ctx->fork, 0);
+    }
+    e |= pq_launch(17, &a, ss);  // k_snappy_walk
+    pq_launch_args aw = a;
+    aw.sitems = B->d_sitems + 2 * (size_t)nwhole;
+    aw.nitems = nall - nwhole;
+    e |= pq_launch(0, &aw, ss);  // k_snappy: segments
+    a.nitems = nwhole;
+    e |= pq_launch(0, &a, s);    // k_snappy: whole pages
+    if (side) {
+      hipEventRecord(ctx->join[0], ss);
+      hipStreamWaitEvent(s, ctx->join[0], 0);
+    }
+    e |= pq_launch(18, &a, s);  // serial fallback for pages whose segments did not decode alone
+  }
   // without BYTE_ARRAY dictionaries nothing k_prepare reads waits on k_copy
   // except data pages with deferred literals: k_prepare runs beside the copies
   // in one launch and those pages after it
@@ -2149,6 +2251,11 @@ void pqg_batch_destroy(pqg_batch *B) {
   hipFree(B->d_recs);
   hipFree(B->d_page_jobs);
   hipFree(B->d_lgroups);
+  hipFree(B->d_sitems);
+  hipFree(B->d_seg_base);
+  hipFree(B->d_walk);
+  hipFree(B->d_segs);
+  hipFree(B->d_seg_flag);
   if (B->h_status) hipHostFree(B->h_status);
   for (int k = 0; k < pqg_batch::kRing; k++)
     for (int i = 0; i < 8; i++)
@@ -2182,6 +2289,9 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
   rc |= alloc_dev((void **)&d_jo, 4 * (size_t)(max_jobs + 1));
   uint32_t *d_cc = nullptr;
   int32_t *d_ci = nullptr;
+  int32_t *d_sitems = nullptr, *d_sbase = nullptr, *d_walk = nullptr;
+  int64_t *d_segs = nullptr;
+  uint32_t *d_sflag = nullptr;
   rc |= alloc_dev((void **)&d_cc, 16);
   rc |= alloc_dev((void **)&d_ci, 4 * (size_t)(max_jobs + 1));
   if (!rc) hipMemsetAsync(d_cc, 0, 16, s);
@@ -2223,12 +2333,37 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
     a.copy_cnt = d_cc;
     a.copy_idx = d_ci;
     a.dbg = nullptr;
+    // one page, cut into segments like a batch's long pages
+    const int32_t nseg = expect > (size_t)kSnapSeg ? (int32_t)((expect + kSnapSeg - 1) / kSnapSeg) : 1;
+    std::vector<int32_t> items;
+    for (int32_t k = 0; k < nseg; k++) items.push_back(0), items.push_back(k);
+    const int32_t seg_base[2] = {0, nseg}, walk0 = 0;
+    rc |= alloc_dev((void **)&d_sitems, 4 * items.size());
+    rc |= alloc_dev((void **)&d_sbase, 8);
+    rc |= alloc_dev((void **)&d_walk, 4);
+    rc |= alloc_dev((void **)&d_segs, 8 * (size_t)nseg);
+    rc |= alloc_dev((void **)&d_sflag, 4);
+    if (!rc) {
+      hipMemcpy(d_sitems, items.data(), 4 * items.size(), hipMemcpyHostToDevice);
+      hipMemcpy(d_sbase, seg_base, 8, hipMemcpyHostToDevice);
+      hipMemcpy(d_walk, &walk0, 4, hipMemcpyHostToDevice);
+      hipMemset(d_sflag, 0, 4);
+    }
+    a.sitems = d_sitems;
+    a.nitems = nseg;
+    a.walk = d_walk;
+    a.nwalk = nseg > 1 ? 1 : 0;
+    a.seg_base = d_sbase;
+    a.segs = d_segs;
+    a.seg_flag = d_sflag;
     PageInfo *d_info = nullptr;
     rc |= alloc_dev((void **)&d_info, sizeof(PageInfo));
     hipMemsetAsync(d_info, 0, sizeof(PageInfo), s);
     a.info = d_info;
     hipDeviceSynchronize();  // null-stream set-up before the launches on the non-blocking stream
+    rc |= pq_launch(17, &a, s);
     rc |= pq_launch(0, &a, s);
+    rc |= pq_launch(18, &a, s);
     rc |= pq_launch(6, &a, s);
     const hipError_t e1 = hipStreamSynchronize(s);
     if (e1 != hipSuccess) {
@@ -2260,6 +2395,11 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
   hipFree(d_ci);
   hipFree(d_jb);
   hipFree(d_jo);
+  hipFree(d_sitems);
+  hipFree(d_sbase);
+  hipFree(d_walk);
+  hipFree(d_segs);
+  hipFree(d_sflag);
   if (rc) {
     if (g_err.empty()) set_err("device snappy failed");
     return PQG_ERR_DEVICE;
@@ -2269,9 +2409,24 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
 
 #ifdef PQ_STAMPS
 // diagnostic build only (not part of include/pqgpu.h): copy the stamp buffer
+// diagnostic: zero the stamp buffers (before the decode a tool reads back)
+extern "C" int pqg_diag_reset(pqg_batch *B) {
+  hipStreamSynchronize(B->ctx->stream);
+  const size_t n1 = std::max(8 * 4 * (B->tiles.size() + 1), 4 * (B->pages.size() + 1));
+  const size_t n2 = 8 * (B->pages.size() + 1) + 256;
+  if (B->d_dbg) hipMemset(B->d_dbg, 0, 8 * n1);
+  if (B->d_dbg2) hipMemset(B->d_dbg2, 0, 8 * n2);
+  return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+// diagnostic: per page (column << 8 | kind), for the stamp tools
+extern "C" int pqg_diag_page_cols(pqg_batch *B, int32_t *out, size_t n) {
+  size_t k = 0;
+  for (; k < n && k < B->pages.size(); k++) out[k] = (B->pages[k].col << 8) | B->pages[k].kind;
+  return (int)k;
+}
 extern "C" int pqg_diag_stamps(pqg_batch *B, uint64_t *out, size_t n) {
   hipStreamSynchronize(B->ctx->stream);
-  size_t cap = 8 * 4 * (B->tiles.size() + 1);
+  size_t cap = std::max(8 * 4 * (B->tiles.size() + 1), 4 * (B->pages.size() + 1));
   if (n > cap) n = cap;
   return hipMemcpy(out, B->d_dbg, n * 8, hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
 }

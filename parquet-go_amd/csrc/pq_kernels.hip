@@ -81,6 +81,14 @@ struct KArgs {
   const TileJob *tiles;   // k_expand: one workgroup per entry
   const LdsGroup *lgroups;  // k_expand_ld: one workgroup per entry
   const uint8_t *in_end, *stage_end;  // allocation ends (PQ_SNAP_GUARD build)
+  // Snappy segments (pages longer than SNAP_SEG are decoded by several waves)
+  const int2 *sitems;     // k_snappy work items {Snappy-list position, segment}
+  int32_t nitems;
+  int32_t nwalk;          // k_snappy_walk / fallback: pages in `walk`
+  const int32_t *walk;    // Snappy-list positions of the segmented pages
+  const int32_t *seg_base;  // per Snappy-list position: first entry in segs (nseg = next - this)
+  int64_t *segs;          // per segment: stream offset of its first token (k_snappy_walk)
+  uint32_t *seg_flag;     // per Snappy-list position: 0 segments ok, 1 serial fallback, 2 nothing to do
 };
 
 #ifdef PQ_STAMPS
@@ -263,6 +271,10 @@ constexpr int SB_OUT = 1024;  // output bytes per batch (token-start bitmap: 32 
 constexpr int SB_WIN = 512;   // compressed bytes staged per batch (walk covers the first 256)
 
 struct SnapLds {  // per wave
+#ifdef PQ_SNAP_STAMPS
+  uint64_t acc[8];  // diagnostic build: shader cycles per batch phase, batches
+  uint64_t tprev;
+#endif
   uint32_t win[SB_WIN / 4 + 4];
   union {
     struct {
@@ -272,6 +284,23 @@ struct SnapLds {  // per wave
     uint16_t jt[2][320];        // chain walk: jump tables J_b, J_b+1 over window positions 0..256
   };
 };
+
+// diagnostic build (-DPQ_SNAP_STAMPS, tools/diag_snappy.py): shader cycles of
+// each phase of a batch, accumulated per wave and written per page to dbg2
+#ifdef PQ_SNAP_STAMPS
+#define SNAP_T(i)                                                  \
+  do {                                                             \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();              \
+    if (lane == 0) {                                               \
+      if ((i) >= 0) L.acc[(i) < 0 ? 0 : (i)] += t_ - L.tprev;      \
+      L.tprev = t_;                                                \
+    }                                                              \
+  } while (0)
+#else
+#define SNAP_T(i) \
+  do {            \
+  } while (0)
+#endif
 
 #ifdef PQ_SNAP_GUARD
 #define PQ_CHK(c, id, u, v, onfail)                                                                   \
@@ -312,11 +341,12 @@ __device__ __forceinline__ void wave_lds_sync() {
 // One batch starting at the short token at s.  Returns false on a corrupt
 // token (err set); advances s / dpos / F otherwise.
 __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const uint8_t *src, int64_t slen, uint8_t *dst,
-                                             int64_t dl, bool write, int64_t &s, int64_t &dpos, int64_t &F,
+                                             int64_t dl, int64_t seg_lo, bool write, int64_t &s, int64_t &dpos, int64_t &F,
                                              uint32_t &err, const uint8_t *pend_src, int64_t pend_dpos,
                                              int64_t &pend_len, int ndefer, int64_t def_dst, int64_t def_len,
                                              uint64_t def_src, int lane, const uint8_t *in_end, int64_t &pf_s,
                                              uint32_t &pg0, uint32_t &pg1, uint32_t &pg2) {
+  SNAP_T(-1);
   // 1. stage the window (aligned base; `sh` = position of byte s); the
   // previous batch prefetched it into pg0..pg2 when it ended at s
   const uintptr_t abase = (uintptr_t)(src + s) & ~(uintptr_t)3;
@@ -339,6 +369,7 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
   if (lane < 4) L.win[lane + 128] = g2;
   const uint32_t pk01 = snappy_tok_class(g0 & 0xff) | (snappy_tok_class((g0 >> 8) & 0xff) << 16);
   const uint32_t pk23 = snappy_tok_class((g0 >> 16) & 0xff) | (snappy_tok_class(g0 >> 24) << 16);
+  SNAP_T(0);
   // 2. the token chain over the first 256 window positions by pointer
   // jumping: J_0(i) = i + size(i) (256: stop), J_b+1 = J_b o J_b; lane m
   // applies J_b for the set bits b of m starting at sh, so it lands on the
@@ -380,11 +411,19 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
   const uint32_t pc = (pos & 1) ? (wp >> 16) : (wp & 0xffff);  // class of this lane's token
   const bool valid = pos <= lim && pc != 0;
   const int32_t incl = wave_incl_scan32(valid ? (int32_t)(pc >> 8) : 0);
-  const int ntok = __builtin_popcountll(ballot(valid && incl <= SB_OUT));  // a prefix of the lanes
+  // a prefix of the lanes: tokens that fit the batch and start before the end
+  // of the output (of the segment: a later token belongs to the next one)
+  const int64_t room = dl - dpos;
+  const int ntok = __builtin_popcountll(ballot(valid && incl <= SB_OUT && (int64_t)incl - (int64_t)(pc >> 8) < room));
+  if (ntok == 0) {  // output complete but tokens remain, or a token crosses the segment end
+    err = E_SNAPPY;
+    return false;
+  }
   const int T = (int)__builtin_amdgcn_readlane(incl, ntok - 1);
   const int cur = (int)__builtin_amdgcn_readlane(pos, ntok - 1) + (int)(__builtin_amdgcn_readlane(pc, ntok - 1) & 0xff);
   const uint32_t tokpos = (uint32_t)pos;
   wave_lds_sync();
+  SNAP_T(1);
   // 3. decode + check token `lane`
   const bool act = lane < ntok;
   uint32_t len = 0, x = 0;
@@ -423,12 +462,13 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
   if (act) {
     const int64_t d = dpos + out_rel;
     bad |= (int64_t)len > dl - d;
-    if (!lit) bad |= x == 0 || (int64_t)x > d;
+    if (!lit) bad |= x == 0 || (int64_t)x > d - seg_lo;  // a segment's copies stay inside it
   }
   if (ballot(act && bad)) {
     err = E_SNAPPY;
     return false;
   }
+  SNAP_T(2);
   if (write) {
     if (pend_len) {  // the history must hold the last deferred literal's tail
       ring_fill(pend_src, pend_dpos, pend_len, ring, lane);
@@ -493,6 +533,7 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
         pf_s = sn;
       }
     }
+    SNAP_T(3);
     // token table + start bitmap
     if (act) L.tok[lane] = make_uint4((uint32_t)out_rel, len | (lit ? 0x80000000u : 0u) | (pre ? 0x40000000u : 0u), x, 0u);
     if (lane < SB_OUT / 32) L.bmc[lane] = make_uint2(0u, 0u);
@@ -505,6 +546,7 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
     const int32_t before = wave_excl_scan32((int32_t)__builtin_popcount(bits), &tot2);
     if (lane < SB_OUT / 32) L.bmc[lane].y = (uint32_t)before;
     wave_lds_sync();
+    SNAP_T(4);
     // 5. every output byte by its own lane, 64 bytes per pass: a copy byte is
     // chased back to a literal, a prefilled far copy, a byte resolved by an
     // earlier pass (already in the history), or a byte before the batch
@@ -580,6 +622,7 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
       wave_lds_sync();
     }
     wave_lds_sync();
+    SNAP_T(5);
     // 6. to HBM: bytes up to the next 16-byte boundary (F is unaligned after
     // a long literal), then whole 16-byte chunks up to floor16(dpos + T)
     // (dst is 16-byte aligned)
@@ -597,26 +640,59 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
     }
     SNAP_GUARD(e16 > dl, 5, e16, dl);
     if (e16 > F) F = e16;
+    SNAP_T(6);
   }
+#ifdef PQ_SNAP_STAMPS
+  if (lane == 0) L.acc[7] += 1;
+#endif
   dpos += total;
   s += cur - sh;
   return true;
 }
 
+// Work modes of k_snappy.  A page whose body is longer than SNAP_SEG is cut at
+// every SNAP_SEG-th output byte: Snappy encoders compress 64 KiB blocks
+// independently (google snappy's kBlockSize, golang/snappy's maxBlockSize),
+// so a token starts there and no copy reaches back across it.  k_snappy_walk
+// finds those tokens; each segment is then its own work item.  A stream
+// without that structure (or a corrupt one) falls back to the serial
+// one-wave-per-page decode (SNAP_FALLBACK), which is exact for any stream.
+constexpr int64_t SNAP_SEG = 65536;
+enum { SNAP_ITEMS = 0, SNAP_FALLBACK = 1 };
+
+template <int MODE>
 __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t ring_all[SNAPPY_WAVES][RING];
   __shared__ SnapLds sl_all[SNAPPY_WAVES];
   const int lane = lane_id();
   const int wv = (int)ufirst(threadIdx.x >> 6);  // wave-uniform (keeps per-wave state in SGPRs)
-  const int gi = blockIdx.x * SNAPPY_WAVES + wv;
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.copy_cnt[(a.epoch + 1) & 1] = 0;  // the next decode's list
-  if (gi >= a.nlist) return;
+  const int wi = blockIdx.x * SNAPPY_WAVES + wv;
+  if (MODE == SNAP_ITEMS && blockIdx.x == 0 && threadIdx.x == 0) a.copy_cnt[(a.epoch + 1) & 1] = 0;  // the next decode's list
+  int gi, seg_k = 0;
+  bool seg = false;
+  if (MODE == SNAP_FALLBACK) {
+    if (wi >= a.nwalk) return;
+    gi = ufirst(a.walk[wi]);
+    if (__hip_atomic_load(&a.seg_flag[gi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1u) return;
+  } else {
+    if (wi >= a.nitems) return;
+    const int2 it = a.sitems[wi];
+    gi = ufirst(it.x);
+    seg_k = ufirst(it.y);
+    seg = a.seg_base[gi + 1] - a.seg_base[gi] > 1;
+    // written by k_snappy_walk in the previous launch: read at device scope
+    if (seg && __hip_atomic_load(&a.seg_flag[gi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
+  }
   const int page = ufirst(a.list[gi]);
   const PageDesc d = a.pages[page];
-  if (a.max_jobs > 0 && lane == 0) a.njobs[gi] = 0u;  // no deferred jobs unless written below
+  if (!seg && a.max_jobs > 0 && lane == 0) a.njobs[gi] = 0u;  // no deferred jobs unless written below
   if (page_status(a.status, page) < make_status(ST_DECOMPRESS, 0)) return;
   uint8_t *ring = ring_all[wv];
   SnapLds &L = sl_all[wv];
+#ifdef PQ_SNAP_STAMPS
+  if (lane < 8) L.acc[lane] = 0;
+  const uint64_t t_page0 = __builtin_amdgcn_s_memtime();
+#endif
 
   const int64_t lsize = d.kind == PAGE_V2 ? (int64_t)d.v2_rep_len + d.v2_def_len : 0;
   const uint8_t *src = a.in + d.src + lsize;
@@ -628,61 +704,72 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
 
   Win W;
   W.reset();
-  // decodedLen: binary.Uvarint over the block (n <= 0 or > 0xffffffff -> ErrCorrupt)
-  int64_t s = 0;
-  uint64_t dlen = 0;
-  {
-    uint32_t sh = 0;
-    bool ok = false;
-    for (int i = 0; s < slen; i++) {
-      uint32_t b = W.byte_at(src + s);
-      s++;
-      if (b < 0x80) {
-        if (i > 9 || (i == 9 && b > 1)) break;
-        dlen |= (uint64_t)b << (sh & 63);
-        ok = true;
-        break;
-      }
-      if (sh < 64) dlen |= (uint64_t)(b & 0x7f) << sh;
-      sh += 7;
-    }
-    if (!ok || dlen > 0xffffffffull) {
-      set_status(a.status, page, ST_DECOMPRESS, E_SNAPPY);
-      return;
-    }
-  }
-  // when the decoded length disagrees with the page header we still run the
-  // decoder (validate only, no stores) to tell ErrCorrupt from a size mismatch
-  const bool write = dlen == (uint64_t)expect;
-  const int64_t dl = (int64_t)dlen;
-  // a block that is exactly one literal is its own content: leave it in place
-  if (write && lane == 0) a.info[page].alias1 = 0;
-  // (a dictionary page only when 8-byte aligned — L1/L2 gathers read aligned
-  // entries — unless its chunk copies it into LDS, which funnel-shifts)
-  if (write && dl > 0 && s < slen) {
-    uint32_t tag = W.byte_at(src + s);
-    if ((tag & 3) == 0) {
-      uint32_t x = tag >> 2;
-      int64_t hs = 1;
-      bool ok = true;
-      if (x >= 60) {
-        int extra = (int)x - 59;
-        hs = 1 + extra;
-        if (s + hs > slen) ok = false;
-        else {
-          x = 0;
-          for (int k = 0; k < extra; k++) x |= W.byte_at(src + s + 1 + k) << (8 * k);
+  int64_t s = 0, seg_lo = 0, dl;
+  bool write;
+  if (seg) {
+    // k_snappy_walk checked the preamble (decoded length == page size) and
+    // found the segment's first token
+    s = __hip_atomic_load(&a.segs[a.seg_base[gi] + seg_k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s = (int64_t)ufirst64(s);
+    seg_lo = (int64_t)seg_k * SNAP_SEG;
+    dl = min(seg_lo + SNAP_SEG, expect);
+    write = true;
+  } else {
+    // decodedLen: binary.Uvarint over the block (n <= 0 or > 0xffffffff -> ErrCorrupt)
+    uint64_t dlen = 0;
+    {
+      uint32_t sh = 0;
+      bool ok = false;
+      for (int i = 0; s < slen; i++) {
+        uint32_t b = W.byte_at(src + s);
+        s++;
+        if (b < 0x80) {
+          if (i > 9 || (i == 9 && b > 1)) break;
+          dlen |= (uint64_t)b << (sh & 63);
+          ok = true;
+          break;
         }
+        if (sh < 64) dlen |= (uint64_t)(b & 0x7f) << sh;
+        sh += 7;
       }
-      if (ok && (int64_t)x + 1 == dl && s + hs + dl == slen &&
-          (d.kind != PAGE_DICT || d.alias_any || ((d.src + lsize + s + hs) & 7) == 0)) {
-        if (lane == 0) a.info[page].alias1 = 1 + (int64_t)(d.src + lsize + s + hs);
+      if (!ok || dlen > 0xffffffffull) {
+        set_status(a.status, page, ST_DECOMPRESS, E_SNAPPY);
         return;
       }
     }
+    // when the decoded length disagrees with the page header we still run the
+    // decoder (validate only, no stores) to tell ErrCorrupt from a size mismatch
+    write = dlen == (uint64_t)expect;
+    dl = (int64_t)dlen;
+    // a block that is exactly one literal is its own content: leave it in place
+    if (write && lane == 0) a.info[page].alias1 = 0;
+    // (a dictionary page only when 8-byte aligned — L1/L2 gathers read aligned
+    // entries — unless its chunk copies it into LDS, which funnel-shifts)
+    if (write && dl > 0 && s < slen) {
+      uint32_t tag = W.byte_at(src + s);
+      if ((tag & 3) == 0) {
+        uint32_t x = tag >> 2;
+        int64_t hs = 1;
+        bool ok = true;
+        if (x >= 60) {
+          int extra = (int)x - 59;
+          hs = 1 + extra;
+          if (s + hs > slen) ok = false;
+          else {
+            x = 0;
+            for (int k = 0; k < extra; k++) x |= W.byte_at(src + s + 1 + k) << (8 * k);
+          }
+        }
+        if (ok && (int64_t)x + 1 == dl && s + hs + dl == slen &&
+            (d.kind != PAGE_DICT || d.alias_any || ((d.src + lsize + s + hs) & 7) == 0)) {
+          if (lane == 0) a.info[page].alias1 = 1 + (int64_t)(d.src + lsize + s + hs);
+          return;
+        }
+      }
+    }
   }
-  int64_t dpos = 0;
-  int64_t F = 0;  // staged output below F is in HBM; [F, dpos) only in the history
+  int64_t dpos = seg_lo;
+  int64_t F = seg_lo;  // staged output below F is in HBM; [F, dpos) only in the history
   uint32_t err = E_OK;
   int ndefer = 0;                      // deferred literals: lane k holds entry k
   const uint8_t *pend_src = nullptr;   // last deferred literal whose tail is not yet in the history
@@ -691,13 +778,13 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
   uint64_t def_src = 0;
   int64_t pf_s = -1;  // stream position of the window prefetched into pg0..pg2
   uint32_t pg0 = 0, pg1 = 0, pg2 = 0;
-  while (s < slen) {
+  while (s < slen && (!seg || dpos < dl)) {
     const uint32_t tag = pf_s == s ? (__builtin_amdgcn_readlane(pg0, 0) >> (8 * ((uintptr_t)(src + s) & 3))) & 0xffu
                                    : W.byte_at(src + s);
     if ((tag & 3) != 0 || (tag >> 2) < 60) {
       // ---- short tokens (copies, literals <= 60 bytes): one batch of up to
       // SB_TOK tokens / SB_OUT output bytes per pass (snappy_batch)
-      if (!snappy_batch(L, ring, src, slen, dst, dl, write, s, dpos, F, err, pend_src, pend_dpos, pend_len, ndefer,
+      if (!snappy_batch(L, ring, src, slen, dst, dl, seg_lo, write, s, dpos, F, err, pend_src, pend_dpos, pend_len, ndefer,
                         def_dst, def_len, def_src, lane, a.in_end, pf_s, pg0, pg1, pg2))
         break;
       continue;
@@ -730,7 +817,7 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
       }
       if (write) {
         bool deferred = false;
-        if (length >= BIG_LITERAL && ndefer < MAX_DEFER && a.max_jobs > 0) {
+        if (!seg && length >= BIG_LITERAL && ndefer < MAX_DEFER && a.max_jobs > 0) {
           // deterministic slot in this page's region (sized by the host: body_len / BIG_LITERAL)
           const uint32_t slot = (uint32_t)(a.job_base[gi] + ndefer);
           const uint32_t region_end = (gi + 1 < a.nlist) ? (uint32_t)a.job_base[gi + 1] : a.max_jobs;
@@ -803,7 +890,13 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
   if (err == E_OK && write)
     for (int64_t p = F + lane; p < dl; p += 64) dst[p] = ring[p & RING_MASK];
   if (err == E_OK && !write) err = E_SIZE;  // compress.go:117-119
-  if (a.max_jobs > 0 && lane == 0) a.njobs[gi] = err ? 0u : (uint32_t)ndefer;
+  if (seg) {
+    // a segment that does not decode on its own: the page is decoded again
+    // serially (which also finds the exact error of a corrupt stream)
+    if (err && lane == 0) atomicMax(&a.seg_flag[gi], 1u);
+    err = E_OK;
+  }
+  if (!seg && a.max_jobs > 0 && lane == 0) a.njobs[gi] = err ? 0u : (uint32_t)ndefer;
   if (!err && ndefer > 0) {  // register the page's deferred literals in the compact list
     uint32_t base = 0;
     if (lane == 0) base = atomicAdd(&a.copy_cnt[a.epoch & 1], (uint32_t)ndefer);
@@ -811,6 +904,277 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
     if (lane < ndefer) a.copy_idx[base + lane] = a.job_base[gi] + lane;
   }
   if (err) set_status(a.status, page, ST_DECOMPRESS, err);
+#ifdef PQ_SNAP_STAMPS
+  // per page (segments add up): phase cycles and batches; wave lifetimes
+  if (a.dbg2 && lane < 8) atomicAdd((unsigned long long *)&a.dbg2[(size_t)page * 8 + lane], (unsigned long long)L.acc[lane]);
+  if (a.dbg && lane == 0) {
+    atomicAdd((unsigned long long *)&a.dbg[(size_t)page * 4 + 0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_page0));
+    atomicMax((unsigned long long *)&a.dbg[(size_t)page * 4 + 1], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_page0));
+    a.dbg[(size_t)page * 4 + 2] = (uint64_t)expect;
+    a.dbg[(size_t)page * 4 + 3] = (uint64_t)slen;
+  }
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// k_snappy_walk: wave per page longer than SNAP_SEG.  Checks the preamble,
+// detects a single-literal page (aliased in place, as k_snappy does), and
+// finds the stream offset of the token that starts at each SNAP_SEG-th output
+// byte.  seg_flag: 0 = segments found, 1 = serial fallback (no token at a
+// boundary, a decoded length that differs from the page header, a stream
+// that ends early), 2 = nothing to decode.
+//
+// The token chain is walked lane-parallel, WALK_CHUNK compressed bytes at a
+// time, staged in LDS by LDS-DMA.  Lane l owns region [64 l, 64 l + 64) and
+// walks WALK_K chains from its first WALK_K bytes, which gives the exact exit
+// and output count for every entry a stream of short tokens can have (a
+// single speculative start phase-locks on periodic data such as a dictionary
+// of increasing integers).  The true chain then visits lanes 0 -> lane of
+// exit(0) -> ... (a scalar loop over <= 64 lanes, the entry offset picking the
+// chain); a lane entered further in (a literal spanning its region start)
+// walks again from its true entry, and if its exit differs from the guess the
+// path is retraced.  Output positions are an exclusive scan; a lane holding a
+// boundary walks its region once more to find the token that starts there.
+// ---------------------------------------------------------------------------
+constexpr int WALK_R = 256;                  // region bytes per lane (speculative chains converge well inside)
+constexpr int WALK_K = 2;                    // exact chains per region (entry offsets 0 .. WALK_K - 1)
+constexpr int WALK_CHUNK = 64 * WALK_R;      // compressed bytes per step
+constexpr int WALK_STAGE = WALK_CHUNK + 1024;  // staged by LDS-DMA in 1 KiB pieces (header lookahead, alignment)
+
+// size in the stream and output length of the token at LDS byte b[r]
+__device__ __forceinline__ void walk_token(const uint8_t *b, int r, int32_t &adv, int32_t &len) {
+  const uint32_t tag = b[r];
+  const uint32_t c = snappy_tok_class(tag);  // size | output << 8, 0: long literal
+  if (c) {
+    adv = (int32_t)(c & 0xff);
+    len = (int32_t)(c >> 8);
+  } else {
+    const int extra = (int)(tag >> 2) - 59;
+    uint32_t v = 0;
+    for (int k = 0; k < extra; k++) v |= (uint32_t)b[r + 1 + k] << (8 * k);
+    // lengths past 2^30 do not fit a page (page sizes are int32): clamp, the
+    // walk then leaves the page and the segments report it
+    len = v >= 0x3fffffffu ? 0x3fffffff : (int32_t)v + 1;
+    adv = 1 + extra + len;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_snappy_walk(KArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t wbuf_all[4][WALK_STAGE];
+  const int lane = lane_id();
+  const int wv = (int)ufirst(threadIdx.x >> 6);
+  const int wi = blockIdx.x * 4 + wv;
+  if (wi >= a.nwalk) return;
+  uint8_t *wbuf = wbuf_all[wv];
+  const int gi = ufirst(a.walk[wi]);
+  const int page = ufirst(a.list[gi]);
+  const PageDesc d = a.pages[page];
+  const int32_t sb = a.seg_base[gi], nseg = a.seg_base[gi + 1] - sb;
+  if (a.max_jobs > 0 && lane == 0) a.njobs[gi] = 0u;  // the fallback writes its own
+  uint32_t flag = 1;
+  if (page_status(a.status, page) < make_status(ST_DECOMPRESS, 0)) {
+    flag = 2;
+  } else {
+    const int64_t lsize = d.kind == PAGE_V2 ? (int64_t)d.v2_rep_len + d.v2_def_len : 0;
+    const uint8_t *src = a.in + d.src + lsize;
+    const int64_t slen = d.comp_len, expect = d.body_len;
+    Win W;
+    W.reset();
+    int64_t s = 0;
+    uint64_t dlen = 0;
+    bool ok = false;
+    for (int i = 0, sh = 0; s < slen; i++, sh += 7) {
+      const uint32_t b = W.byte_at(src + s);
+      s++;
+      if (b < 0x80) {
+        ok = !(i > 9 || (i == 9 && b > 1));
+        dlen |= (uint64_t)b << (sh & 63);
+        break;
+      }
+      if (sh < 64) dlen |= (uint64_t)(b & 0x7f) << sh;
+    }
+    if (lane == 0) a.info[page].alias1 = 0;
+    if (ok && dlen == (uint64_t)expect && s < slen) {
+      // one literal covering the page: k_snappy's alias (no copy)
+      const uint32_t tag = W.byte_at(src + s);
+      if ((tag & 3) == 0) {
+        uint32_t x = tag >> 2;
+        int64_t hs = 1;
+        bool lok = true;
+        if (x >= 60) {
+          const int extra = (int)x - 59;
+          hs = 1 + extra;
+          if (s + hs > slen) lok = false;
+          else {
+            x = 0;
+            for (int k = 0; k < extra; k++) x |= W.byte_at(src + s + 1 + k) << (8 * k);
+          }
+        }
+        if (lok && (int64_t)x + 1 == expect && s + hs + expect == slen &&
+            (d.kind != PAGE_DICT || d.alias_any || ((d.src + lsize + s + hs) & 7) == 0)) {
+          if (lane == 0) a.info[page].alias1 = 1 + (int64_t)(d.src + lsize + s + hs);
+          flag = 2;
+        }
+      }
+      if (flag != 2) {
+        if (lane == 0) a.segs[sb] = s;
+        int64_t out = 0, nb = SNAP_SEG;  // output before s; next boundary
+        int32_t kb = 1;
+        bool fail = false;
+
+        while (kb < nseg && !fail) {
+          if (s >= slen) {  // the stream ended before the last boundary
+            fail = true;
+            break;
+          }
+          if (out == nb) {  // a boundary exactly at the chunk base
+            if (lane == 0) a.segs[sb + kb] = s;
+            kb++;
+            nb += SNAP_SEG;
+            continue;
+          }
+          // stage [s, s + WALK_CHUNK + lookahead) by LDS-DMA, 1 KiB a piece (lane
+          // l's 16 bytes at +16 l); readable slack follows every chunk (kPad)
+          const uintptr_t A = (uintptr_t)(src + s) & ~(uintptr_t)15;
+          const uintptr_t lim = (uintptr_t)a.in_end;  // never past the input allocation (its pad included)
+#pragma unroll
+          for (int off = 0; off < WALK_STAGE; off += 1024)
+            if (A + off + 16 * (uintptr_t)lane + 16 <= lim)
+              __builtin_amdgcn_global_load_lds((const void *)(A + off + 16 * (uintptr_t)lane),
+                                               (__attribute__((address_space(3))) void *)(wbuf + off), 16, 0, 0);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          wave_lds_sync();
+          const uint8_t *b = wbuf + ((uintptr_t)(src + s) - A);
+          // positions relative to s; the chunk holds regions of lanes below
+          // nreg (its end is the page end when that comes first)
+          const int64_t rest = slen - s;
+          const int cend = (int)min<int64_t>(rest, (int64_t)WALK_CHUNK);
+          const int r0 = WALK_R * lane, r1 = min(r0 + WALK_R, cend);
+          // pass 1: WALK_K chains per lane, from each of the first WALK_K bytes
+          // of my region, walked together (independent LDS reads in flight):
+          // exact exits and output counts for entries that close to the region
+          // start — every entry of a stream of short tokens (copies, literals
+          // under WALK_K bytes), where speculation could phase-lock on
+          // periodic data (e.g. a dictionary of increasing integers)
+          int32_t yk[WALK_K], ok[WALK_K];
+#pragma unroll
+          for (int k = 0; k < WALK_K; k++) {
+            yk[k] = r0 + k;
+            ok[k] = 0;
+          }
+          if (r0 < cend) {
+            for (;;) {
+              bool more = false;
+#pragma unroll
+              for (int k = 0; k < WALK_K; k++) {
+                if (yk[k] < r1) {
+                  int32_t adv, len;
+                  walk_token(b, yk[k], adv, len);
+                  yk[k] += adv;
+                  ok[k] += len;
+                  more |= yk[k] < r1;
+                }
+              }
+              if (!ballot(more)) break;
+            }
+          }
+          // a later entry (inside a literal that spans the region start) uses
+          // the last chain as a guess, checked below
+          int32_t y = yk[WALK_K - 1];
+          // passes 2 + 3 until the true path agrees with the exits used
+          int32_t entry = -1, tx = 0, tout = 0;  // my true entry, exit, output bytes
+          int32_t last = 0, guard = 0;
+          for (;;) {
+            // the true chain's lanes: 0 -> lane(exit(0)) -> ... (exits >= region ends)
+            int cur = 0, ein = 0;
+            entry = -1;
+            bool exact = false;
+            while (true) {
+              const int e = ein - WALK_R * cur;
+              int32_t ex = __builtin_amdgcn_readlane(y, cur), eo = -1;  // a guess unless an exact chain starts there
+#pragma unroll
+              for (int k = 0; k < WALK_K; k++)
+                if (e == k) {  // scalar: the entry offset picks the chain
+                  ex = __builtin_amdgcn_readlane(yk[k], cur);
+                  eo = __builtin_amdgcn_readlane(ok[k], cur);
+                }
+              if (lane == cur) {
+                entry = ein;
+                exact = eo >= 0;
+                if (exact) {
+                  tx = ex;
+                  tout = eo;
+                }
+              }
+              last = cur;
+              if (ex >= cend) break;
+              ein = ex;
+              cur = ex / WALK_R;
+            }
+            // pass 3: path lanes with a guessed exit walk from their true entry
+            bool bad = false;
+            if (entry >= 0 && !exact) {
+              int32_t adv, len;
+              tout = 0;
+              tx = entry;
+              while (tx < r1) {
+                walk_token(b, tx, adv, len);
+                tx += adv;
+                tout += len;
+              }
+              bad = tx != y;
+            }
+            const uint64_t badm = ballot(bad);
+            if (!badm || ++guard > 64) {
+              if (badm) fail = true;
+              break;
+            }
+            if (bad) y = tx;  // correct the exits and retrace the path
+          }
+          if (entry >= 0) y = tx;  // the path lanes' true exits
+          if (fail) break;
+          // output positions of the path lanes' first tokens
+          int32_t ctot;
+          const int32_t ex = wave_excl_scan32(entry >= 0 ? tout : 0, &ctot);
+          const int64_t o0 = out + ex;
+          // lanes holding boundaries find the token that starts there
+          bool bfail = false;
+          if (entry >= 0 && o0 + tout > nb) {
+            int64_t bnext = nb;
+            while (bnext < o0) bnext += SNAP_SEG;  // the first boundary at or after my first token
+            int64_t o = o0;
+            int32_t r = entry, adv, len;
+            while (r < r1 && bnext < o0 + tout) {
+              walk_token(b, r, adv, len);
+              if (o == bnext) {
+                const int64_t k = bnext / SNAP_SEG;
+                if (k < nseg) a.segs[sb + k] = s + r;
+                bnext += SNAP_SEG;
+              } else if (o < bnext && o + len > bnext) {
+                bfail = true;  // a token spans the boundary
+                break;
+              }
+              o += len;
+              r += adv;
+            }
+          }
+          if (ballot(bfail)) {
+            fail = true;
+            break;
+          }
+          out += ctot;
+          while (nb < out) {  // boundaries passed inside this chunk
+            nb += SNAP_SEG;
+            kb++;
+          }
+          s += __builtin_amdgcn_readlane(y, last);
+          wave_lds_sync();
+        }
+        flag = (!fail && kb >= nseg) ? 0u : 1u;
+      }
+    }
+  }
+  if (lane == 0) a.seg_flag[gi] = flag;
 }
 
 // ===========================================================================
@@ -3190,10 +3554,22 @@ struct pq_launch_args {
   const void *zr;
   int32_t nzr, npages;
   const uint8_t *in_end, *stage_end;
+  const void *sitems;
+  int32_t nitems, nwalk;
+  const int32_t *walk, *seg_base;
+  int64_t *segs;
+  uint32_t *seg_flag;
 };
 
 static pq::KArgs to_k(const pq_launch_args *p) {
   pq::KArgs k;
+  k.sitems = (const int2 *)p->sitems;
+  k.nitems = p->nitems;
+  k.nwalk = p->nwalk;
+  k.walk = p->walk;
+  k.seg_base = p->seg_base;
+  k.segs = p->segs;
+  k.seg_flag = p->seg_flag;
   k.in_end = p->in_end;
   k.stage_end = p->stage_end;
   k.in = p->in;
@@ -3274,10 +3650,20 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     }
     return hipGetLastError() == hipSuccess ? 0 : 17;
   }
+  if (which == 0) {  // k_snappy over work items (pages, or segments of long pages)
+    if (k.nitems <= 0) return 0;
+    hipLaunchKernelGGL(pq::k_snappy<pq::SNAP_ITEMS>, dim3((k.nitems + 3) / 4), dim3(256), 0, s, k);
+    return hipGetLastError() == hipSuccess ? 0 : 17;
+  }
+  if (which == 17 || which == 18) {  // k_snappy_walk / serial fallback over the segmented pages
+    if (k.nwalk <= 0) return 0;
+    if (which == 17) hipLaunchKernelGGL(pq::k_snappy_walk, dim3((k.nwalk + 3) / 4), dim3(256), 0, s, k);
+    else hipLaunchKernelGGL(pq::k_snappy<pq::SNAP_FALLBACK>, dim3((k.nwalk + 3) / 4), dim3(256), 0, s, k);
+    return hipGetLastError() == hipSuccess ? 0 : 17;
+  }
   if (k.nlist <= 0) return 0;
   dim3 grid((k.nlist + 3) / 4), block(256);
   switch (which) {
-    case 0: hipLaunchKernelGGL(pq::k_snappy, grid, block, 0, s, k); break;
     case 1: hipLaunchKernelGGL(pq::k_dict_prepare, grid, block, 0, s, k); break;
     case 2: hipLaunchKernelGGL(pq::k_prepare<-1>, grid, block, 0, s, k); break;
     case 11: hipLaunchKernelGGL(pq::k_prepare<1>, grid, block, 0, s, k); break;

@@ -155,6 +155,56 @@ def test_snappy_block_roundtrip():
     assert pqgpu.DecompressBlock(pqgpu.CompressionCodec_SNAPPY, comp, len(data)) == data
 
 
+def _uvarint(v):
+    out = bytearray()
+    while True:
+        b = v & 0x7f
+        v >>= 7
+        out.append(b | (0x80 if v else 0))
+        if not v:
+            return bytes(out)
+
+
+def test_snappy_segments_and_fallback():
+    """Blocks longer than 64 KiB are decoded by one wave per 64 KiB segment
+    (k_snappy_walk finds the token at each boundary); streams without that
+    structure fall back to the serial decode.  Every case against the oracle."""
+    pa = pytest.importorskip("pyarrow")
+    rng = np.random.default_rng(9)
+
+    def both(stream, n, expect_n=None):
+        expect_n = n if expect_n is None else expect_n
+        rc_o, got_o, n_o = oracle.snappy_decode(stream, max(n, expect_n) + 64)
+        want = rc_o if rc_o else (pqgpu.ERR_SIZE if n_o != expect_n else 0)
+        try:
+            got = pqgpu.DecompressBlock(pqgpu.CompressionCodec_SNAPPY, stream, expect_n)
+            rc_g = 0
+        except pqgpu.PqgError as e:
+            rc_g, got = e.code, None
+        assert rc_g == want, (rc_g, want)
+        if want == 0:
+            assert got == got_o[:expect_n]
+    # google snappy output (64 KiB blocks): segments
+    for n in (65536, 65537, 200000, 1 << 20, (1 << 20) + 12345):
+        data = (np.round(rng.standard_normal(n // 8 + 1), 2).tobytes() + b"x" * 7)[:n]
+        both(pa.compress(data, codec="snappy", asbytes=True), n)
+    # a copy that reaches back across the 64 KiB boundary (a token starts there): fallback
+    lit = rng.integers(0, 256, 65536, dtype=np.uint8).tobytes()
+    stream = _uvarint(65536 + 64) + bytes([62 << 2]) + (65536 - 1).to_bytes(3, "little") + lit
+    stream += bytes([((64 - 1) << 2) | 2]) + (60000).to_bytes(2, "little")
+    both(stream, 65536 + 64)
+    # a token crossing the boundary: fallback
+    stream = _uvarint(65600) + bytes([62 << 2]) + (65530 - 1).to_bytes(3, "little") + lit[:65530]
+    stream += bytes([60 << 2, 70 - 1]) + lit[:70]
+    both(stream, 65600)
+    # corrupt inside the second segment (offset 0), and a size mismatch
+    good = pa.compress(lit + lit[:40000], codec="snappy", asbytes=True)
+    bad = bytearray(good)
+    bad[-3:] = bytes([0x01, 0x00, 0x00])
+    both(bytes(bad), len(lit) + 40000)
+    both(good, len(lit) + 40000, expect_n=len(lit) + 39999)
+
+
 def test_snappy_block_errors_match_oracle():
     """DecompressBlock = snappy.Decode + the exact-size check of newBlockReader
     (compress.go:112-119): class SNAPPY if the stream is corrupt, else SIZE if
@@ -282,8 +332,16 @@ def test_c5_lineitem_shape(tmp_path):
     l_comment (and the high-cardinality numeric columns) fall back from
     RLE_DICTIONARY to PLAIN mid-chunk; every leaf bit-exact against the oracle."""
     pytest.importorskip("pyarrow")
-    check_file(_c5_bytes(tmp_path, 90000, 30000, dictionary_pagesize_limit=64 << 10, data_page_size=256 << 10),
-               "c5 small dict")
+    data = _c5_bytes(tmp_path, 90000, 30000, dictionary_pagesize_limit=64 << 10, data_page_size=256 << 10)
+    check_file(data, "c5 small dict")
+    # every Snappy page over 64 KiB in segments (k_snappy_walk + one wave per
+    # segment), and none (one wave per page)
+    for env, val in (("PQG_SNAPPY_SEG_MIN", "65537"), ("PQG_SNAPPY_SEGMENTS", "0")):
+        os.environ[env] = val
+        try:
+            check_file(data, "c5 small dict %s=%s" % (env, val))
+        finally:
+            del os.environ[env]
 
 
 def test_c5_lineitem_large_string_dictionary(tmp_path):

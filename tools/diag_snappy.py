@@ -1,0 +1,66 @@
+"""Diagnostic: where k_snappy's time goes, per column, from the phase stamps
+of the libpqgpu_snapdiag.so build (make -C parquet-go_amd/csrc snapdiag).
+
+usage: python tools/diag_snappy.py CONFIG [ROWS] [RG_ROWS]
+Per page the build accumulates shader cycles (s_memtime) of each step of a
+short-token batch (window, chain, decode, far copies, tables, byte passes,
+flush) and counts batches; per column this prints the sums and per-batch
+means, plus page start / end spread."""
+import ctypes
+import os
+import sys
+
+os.environ["PQGPU_LIB"] = "libpqgpu_snapdiag.so"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "parquet-go_amd"), os.path.join(ROOT, "tools")]
+import numpy as np  # noqa: E402
+
+import pqgpu  # noqa: E402
+import synth  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c5"
+rows = int(sys.argv[2]) if len(sys.argv) > 2 else synth.DEFAULTS[cfg][0]
+rgr = int(sys.argv[3]) if len(sys.argv) > 3 else synth.DEFAULTS[cfg][1]
+path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "pqgpu_bench_%s_%d_%d_0.parquet" % (cfg, rows, rgr))
+if not os.path.exists(path):
+    synth.make(cfg, path, rows, rgr)
+r = pqgpu.FileReader(path)
+b = r.batch()
+for _ in range(2):
+    b.decode()
+b.sync()
+L = pqgpu.lib()
+L.pqg_diag_reset.argtypes = [ctypes.c_void_p]
+L.pqg_diag_reset(b._h)  # the stamps below are of exactly one decode
+b.decode()
+b.sync()
+for fn in ("pqg_diag_stamps", "pqg_diag_stamps2"):
+    getattr(L, fn).argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+L.pqg_diag_page_cols.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+npg = b.stats()["pages"]
+pc = np.zeros(npg, np.int32)
+L.pqg_diag_page_cols(b._h, pc.ctypes.data, npg)
+ph = np.zeros(8 * (npg + 1) + 256, np.uint64)
+L.pqg_diag_stamps2(b._h, ph.ctypes.data, ph.size)
+pg = np.zeros(4 * (npg + 1), np.uint64)
+L.pqg_diag_stamps(b._h, pg.ctypes.data, pg.size)
+ph = ph[:8 * npg].reshape(npg, 8).astype(np.float64)
+pg = pg[:4 * npg].reshape(npg, 4).astype(np.float64)  # per page: wave-cycles (all segments), longest wave, bytes out, in
+names = [c["name"] for c in r.Columns()]
+print("%s: %d pages; longest wave %.0f kcycles" % (cfg, npg, pg[:, 1].max() / 1e3))
+steps = ["window", "chain", "decode", "far", "tables", "bytes", "flush"]
+print("%-16s %6s %8s %8s %9s | %s | %s" % ("column", "pages", "batches", "MB out", "kcyc/pg", " ".join("%7s" % s for s in steps),
+                                           "cyc/batch"))
+for ci in sorted(set((pc >> 8).tolist())):
+    m = (pc >> 8) == ci
+    m &= pg[:, 2] > 0
+    if not m.any():
+        continue
+    nb = ph[m, 7].sum()
+    tot = ph[m, :7].sum(0)
+    life = pg[m, 1]
+    print("%-16s %6d %8d %8.1f %9.0f | %s | %6.0f" % (
+        names[ci][:16], m.sum(), nb, pg[m, 2].sum() / 1e6, pg[m, 0].mean() / 1e3,
+        " ".join("%6.1f%%" % (100 * x / max(tot.sum(), 1)) for x in tot), tot.sum() / max(nb, 1)))
+    print("%16s longest wave kcyc: median %.0f p90 %.0f max %.0f; batches/page max %d" % (
+        "", np.median(life) / 1e3, np.percentile(life, 90) / 1e3, life.max() / 1e3, ph[m, 7].max()))

@@ -8,5 +8,5 @@ IFS=';' read -ra GROUPS_ <<< "${PASSES:-$DEFAULT}"
 i=0
 for P in "${GROUPS_[@]}"; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d gpurun_out/${TAG}_pmc$i -o run -- python3 bench.py --no-cpu --no-pmc "$@" > gpurun_out/${TAG}_pmc$i.log 2>&1 || { echo "pass $i failed" >> gpurun_out/${TAG}_pmc$i.log; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d gpurun_out/${TAG}_pmc$i -o run -- python3 bench.py --child "$@" > gpurun_out/${TAG}_pmc$i.log 2>&1 || { echo "pass $i failed" >> gpurun_out/${TAG}_pmc$i.log; exit 1; }
 done

@@ -8,7 +8,7 @@ tag = sys.argv[1]
 want = sys.argv[2:] or None
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
 dur = collections.defaultdict(list)
-for f in sorted(glob.glob("%s_pmc*/run_counter_collection.csv" % tag)):
+for f in sorted(glob.glob("%s_pmc*/**/*counter_collection.csv" % tag, recursive=True)):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "")
         acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
