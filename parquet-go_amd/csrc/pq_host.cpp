@@ -586,7 +586,8 @@ struct pqg_batch {
   std::vector<int32_t> seg_base;      // per Snappy-list position (+1): first segment
   std::vector<int32_t> snap_items;    // {position, segment} pairs, longest first
   std::vector<int32_t> walk_list;     // positions of the segmented pages
-  int32_t n_whole_items = 0;          // snap_items of unsegmented pages (they come first)
+  int32_t n_whole_items = 0;          // snap_items of whole data pages (first), then whole dictionary pages,
+  int32_t n_dict_items = 0;           // then segments
   int32_t *d_sitems = nullptr, *d_seg_base = nullptr, *d_walk = nullptr;
   int64_t *d_segs = nullptr;
   uint32_t *d_seg_flag = nullptr;
@@ -1578,16 +1579,23 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
       for (int32_t k = 0; k < nseg; k++)
         items.push_back({(int32_t)q, k, nseg > 1 ? std::min<int64_t>(kSnapSeg, body - (int64_t)k * kSnapSeg) : body});
     }
-    // whole pages first (one launch), then the segments (a second launch,
-    // after k_snappy_walk on a side stream): each part longest first
+    // three launches: whole data pages (context stream); then, on a side
+    // stream, the segments (after k_snappy_walk) and the whole dictionary
+    // pages, which k_dict_prepare follows there.  Each part longest first.
+    auto part = [&](const It &x) {
+      if (B->seg_base[x.q + 1] - B->seg_base[x.q] > 1) return 2;
+      return B->pages[(size_t)B->snappy_list[(size_t)x.q]].kind == PAGE_DICT ? 1 : 0;
+    };
     std::stable_sort(items.begin(), items.end(), [&](const It &x, const It &y) {
-      const bool sx = B->seg_base[x.q + 1] - B->seg_base[x.q] > 1, sy = B->seg_base[y.q + 1] - B->seg_base[y.q] > 1;
-      return sx != sy ? sy : x.bytes > y.bytes;
+      const int px = part(x), py = part(y);
+      return px != py ? px < py : x.bytes > y.bytes;
     });
     for (const It &it : items) {
       B->snap_items.push_back(it.q);
       B->snap_items.push_back(it.k);
-      if (B->seg_base[it.q + 1] - B->seg_base[it.q] == 1) B->n_whole_items++;
+      const int pt = part(it);
+      if (pt == 0) B->n_whole_items++;
+      if (pt == 1) B->n_dict_items++;
     }
   }
   phase("plan");
@@ -1643,7 +1651,10 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   std::vector<int32_t> job_base(B->snappy_list.size() + 1), job_owner;
   for (size_t q = 0; q < B->snappy_list.size(); q++) {
     job_base[q] = (int32_t)job_owner.size();
-    int32_t cap = std::min(64, B->pages[(size_t)B->snappy_list[q]].body_len / (16 * 1024));
+    // dictionary pages copy their long literals themselves: k_dict_prepare
+    // runs beside the data pages' Snappy decode, before k_copy
+    const PageDesc &sp = B->pages[(size_t)B->snappy_list[q]];
+    int32_t cap = sp.kind == PAGE_DICT ? 0 : std::min(64, sp.body_len / (16 * 1024));
     for (int32_t k = 0; k < cap; k++) job_owner.push_back((int32_t)q);
   }
   B->max_jobs = (uint32_t)job_owner.size();
@@ -1674,7 +1685,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   }
 #ifdef PQ_STAMPS
   rc |= alloc_dev((void **)&B->d_dbg, sizeof(uint64_t) * std::max(8 * 4 * (B->tiles.size() + 1), 4 * (npages + 1)));
-  rc |= alloc_dev((void **)&B->d_dbg2, sizeof(uint64_t) * (8 * (npages + 1) + 256));
+  rc |= alloc_dev((void **)&B->d_dbg2, sizeof(uint64_t) * (16 * (npages + 1) + 256));  // + k_snappy_walk stamps
 #endif
   if (rc) return PQG_ERR_DEVICE;
   if (hipHostMalloc((void **)&B->h_status, sizeof(uint32_t) * (npages + 1), hipHostMallocDefault) != hipSuccess) {
@@ -1933,33 +1944,60 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.segs = B->d_segs;
   a.seg_flag = B->d_seg_flag;
   {
-    // k_snappy_walk (segment starts of the long pages) and then their segments
-    // run on a side stream beside the whole pages on the context stream: the
-    // walk is a few waves of serial work that would otherwise idle the GPU
-    const int32_t nall = (int32_t)(B->snap_items.size() / 2), nwhole = B->n_whole_items;
+    // Two streams: k_snappy_walk (segment starts of the long pages), their
+    // segments, the serial fallback, the whole dictionary pages and
+    // k_dict_prepare — a few waves of serial work each, which would idle the
+    // GPU on their own — beside the whole data pages.  Only the whole data
+    // pages defer literals to k_copy (after the join).
+    const int32_t nall = (int32_t)(B->snap_items.size() / 2), nwhole = B->n_whole_items, ndict = B->n_dict_items;
     pqg_ctx *ctx = B->ctx;
-    const bool side = nall > nwhole && !B->seg_times;
-    hipStream_t ss = side ? ctx->side[0] : s;
+    const bool side = (nall > nwhole || nd > 0) && !B->seg_times;
+    // the serial chain (walk -> segments -> ...) goes on the context stream,
+    // dispatched first, and the whole data pages on the side stream: a chain
+    // on the side stream was dispatched after the whole pages had taken the
+    // CUs (PQG_WALK_SIDE=1 restores that order for comparison)
+    static const bool walk_side = [] {
+      const char *v = getenv("PQG_WALK_SIDE");
+      return v && v[0] == '1';
+    }();
+    hipStream_t ss = side && walk_side ? ctx->side[0] : s;   // the serial chain
+    hipStream_t sw = side && !walk_side ? ctx->side[0] : s;  // whole data pages
     if (side) {
       hipEventRecord(ctx->fork, s);
-      hipStreamWaitEvent(ss, ctx->fork, 0);
+      hipStreamWaitEvent(ctx->side[0], ctx->fork, 0);
     }
     e |= pq_launch(17, &a, ss);  // k_snappy_walk
+    if (!walk_side) {
+      a.nitems = nwhole;
+      e |= pq_launch(0, &a, sw);  // k_snappy: whole data pages (side stream)
+    }
     pq_launch_args aw = a;
-    aw.sitems = B->d_sitems + 2 * (size_t)nwhole;
-    aw.nitems = nall - nwhole;
+    aw.sitems = B->d_sitems + 2 * (size_t)(nwhole + ndict);
+    aw.nitems = nall - nwhole - ndict;
     e |= pq_launch(0, &aw, ss);  // k_snappy: segments
-    a.nitems = nwhole;
-    e |= pq_launch(0, &a, s);    // k_snappy: whole pages
+    e |= pq_launch(18, &a, ss);  // serial fallback for pages whose segments did not decode alone
+    aw.sitems = B->d_sitems + 2 * (size_t)nwhole;
+    aw.nitems = ndict;
+    e |= pq_launch(0, &aw, ss);  // k_snappy: whole dictionary pages
     if (side) {
-      hipEventRecord(ctx->join[0], ss);
+      aw = a;
+      aw.list = B->d_lists + ns;
+      aw.nlist = nd;
+      e |= pq_launch(1, &aw, ss);  // k_dict_prepare (its pages are all decoded on this stream)
+    }
+    if (walk_side) {
+      a.nitems = nwhole;
+      e |= pq_launch(0, &a, sw);  // k_snappy: whole data pages
+    }
+    if (side) {
+      hipEventRecord(ctx->join[0], ctx->side[0]);
       hipStreamWaitEvent(s, ctx->join[0], 0);
     }
-    e |= pq_launch(18, &a, s);  // serial fallback for pages whose segments did not decode alone
   }
   // without BYTE_ARRAY dictionaries nothing k_prepare reads waits on k_copy
   // except data pages with deferred literals: k_prepare runs beside the copies
-  // in one launch and those pages after it
+  // in one launch and those pages after it (with string dictionaries, the
+  // string pages would all wait: measured slower)
   const bool fused = nd == 0 && B->max_jobs > 0 && !B->seg_times;
   if (fused) {
     a.list = B->d_lists + ns + nd;
@@ -1969,9 +2007,11 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   } else {
     e |= pq_launch(6, &a, s);  // k_copy: long literals, timed together with k_snappy
     mark(false);
-    a.list = B->d_lists + ns;
-    a.nlist = nd;
-    e |= pq_launch(1, &a, s);
+    if (B->seg_times) {  // phase timing: k_dict_prepare here (not on the side stream)
+      a.list = B->d_lists + ns;
+      a.nlist = nd;
+      e |= pq_launch(1, &a, s);
+    }
     mark(false);
     a.list = B->d_lists + ns + nd;
     a.nlist = ndata;
@@ -2413,7 +2453,7 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
 extern "C" int pqg_diag_reset(pqg_batch *B) {
   hipStreamSynchronize(B->ctx->stream);
   const size_t n1 = std::max(8 * 4 * (B->tiles.size() + 1), 4 * (B->pages.size() + 1));
-  const size_t n2 = 8 * (B->pages.size() + 1) + 256;
+  const size_t n2 = 16 * (B->pages.size() + 1) + 256;
   if (B->d_dbg) hipMemset(B->d_dbg, 0, 8 * n1);
   if (B->d_dbg2) hipMemset(B->d_dbg2, 0, 8 * n2);
   return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
@@ -2432,7 +2472,7 @@ extern "C" int pqg_diag_stamps(pqg_batch *B, uint64_t *out, size_t n) {
 }
 extern "C" int pqg_diag_stamps2(pqg_batch *B, uint64_t *out, size_t n) {
   hipStreamSynchronize(B->ctx->stream);
-  size_t cap = 8 * (B->pages.size() + 1) + 256;
+  size_t cap = 16 * (B->pages.size() + 1) + 256;
   if (n > cap) n = cap;
   return hipMemcpy(out, B->d_dbg2, n * 8, hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
 }

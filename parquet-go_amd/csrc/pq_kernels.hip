@@ -925,47 +925,93 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
 // that ends early), 2 = nothing to decode.
 //
 // The token chain is walked lane-parallel, WALK_CHUNK compressed bytes at a
-// time, staged in LDS by LDS-DMA.  Lane l owns region [64 l, 64 l + 64) and
+// time, staged in LDS by LDS-DMA.  Lane l owns region [R l, R l + R) (WALK_R) and
 // walks WALK_K chains from its first WALK_K bytes, which gives the exact exit
 // and output count for every entry a stream of short tokens can have (a
 // single speculative start phase-locks on periodic data such as a dictionary
-// of increasing integers).  The true chain then visits lanes 0 -> lane of
-// exit(0) -> ... (a scalar loop over <= 64 lanes, the entry offset picking the
-// chain); a lane entered further in (a literal spanning its region start)
-// walks again from its true entry, and if its exit differs from the guess the
-// path is retraced.  Output positions are an exclusive scan; a lane holding a
+// of increasing integers); pass 1 also marks every token its chains visit
+// (merge table).  The regions the true chain visits are found by pointer
+// jumping over states (region, entry offset 0 / 1 / later) — a scalar hop
+// loop cost ~400 cycles a hop; a lane entered further in (a literal spanning
+// its region start) walks from its true entry until it meets a marked token,
+// and if its exit differs from the guess the path is found again.  Output positions are an exclusive scan; a lane holding a
 // boundary walks its region once more to find the token that starts there.
 // ---------------------------------------------------------------------------
-constexpr int WALK_R = 256;                  // region bytes per lane (speculative chains converge well inside)
+// region bytes per lane (speculative chains converge well inside); 65 dwords,
+// not 64: the lanes' reads start in 32 different LDS banks (a 256-byte stride
+// put all 32 lanes of a group on one bank: 32-way conflicts on every read)
+constexpr int WALK_R = 260;
 constexpr int WALK_K = 2;                    // exact chains per region (entry offsets 0 .. WALK_K - 1)
+static_assert(WALK_K == 2 && 64 * WALK_R * 2 % 16 == 0, "merge table: one chain bit, uint4 fill");
 constexpr int WALK_CHUNK = 64 * WALK_R;      // compressed bytes per step
-constexpr int WALK_STAGE = WALK_CHUNK + 1024;  // staged by LDS-DMA in 1 KiB pieces (header lookahead, alignment)
+// staged by LDS-DMA in 1 KiB pieces: alignment skew, the chunk, token lookahead
+constexpr int WALK_STAGE = (WALK_CHUNK + 32 + 1023) / 1024 * 1024;
 
-// size in the stream and output length of the token at LDS byte b[r]
-__device__ __forceinline__ void walk_token(const uint8_t *b, int r, int32_t &adv, int32_t &len) {
-  const uint32_t tag = b[r];
-  const uint32_t c = snappy_tok_class(tag);  // size | output << 8, 0: long literal
-  if (c) {
-    adv = (int32_t)(c & 0xff);
-    len = (int32_t)(c >> 8);
-  } else {
-    const int extra = (int)(tag >> 2) - 59;
-    uint32_t v = 0;
-    for (int k = 0; k < extra; k++) v |= (uint32_t)b[r + 1 + k] << (8 * k);
-    // lengths past 2^30 do not fit a page (page sizes are int32): clamp, the
-    // walk then leaves the page and the segments report it
-    len = v >= 0x3fffffffu ? 0x3fffffff : (int32_t)v + 1;
-    adv = 1 + extra + len;
-  }
+// size in the stream and output length of the token at LDS byte p of the
+// (16-byte aligned) staging buffer w, branch-free: three dword reads and
+// selects, no exec-mask changes, so the walks of several chains interleave
+__device__ __forceinline__ void walk_token(const uint32_t *w, int p, int32_t &adv, int32_t &len) {
+  const int q = p >> 2, sb = p & 3;
+  const uint32_t d0 = w[q], d1 = w[q + 1], d2 = w[q + 2];
+  const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sb);  // bytes p .. p + 3
+  const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, sb);  // bytes p + 4 .. p + 7
+  const uint32_t tag = lo & 0xff, t = tag & 3, x = tag >> 2;
+  // short literal x + 1 bytes; copy-1 4 + (x & 7) from 2 bytes; copy-2 / -4: x + 1 from 3 / 5
+  int32_t l = (int32_t)(t == 1 ? 4 + (x & 7) : x + 1);
+  int32_t z = (int32_t)(t == 0 ? x + 2 : t == 1 ? 2 : t == 2 ? 3 : 5);
+  // long literal: 1 .. 4 little-endian length bytes follow the tag; lengths
+  // past 2^30 do not fit a page (page sizes are int32): clamp, the walk then
+  // leaves the page and the segments report it
+  const int extra = (int)x - 59;
+  const uint32_t lb = (lo >> 8) | (hi << 24);
+  const uint32_t v = extra >= 4 ? lb : lb & ((1u << (8 * (extra & 3))) - 1u);
+  const int32_t ll = v >= 0x3fffffffu ? 0x3fffffff : (int32_t)v + 1;
+  const bool lng = t == 0 && x >= 60;
+  len = lng ? ll : l;
+  adv = lng ? 1 + extra + ll : z;
 }
 
-__global__ __launch_bounds__(256) void k_snappy_walk(KArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t wbuf_all[4][WALK_STAGE];
+// the state after exit position x: region x / WALK_R entered at offset 0, 1
+// or later (2); 192 past the chunk
+__device__ __forceinline__ int walk_state(int32_t x, int cend) {
+  if (x >= cend) return 192;
+  const int n = x / WALK_R;
+  return 3 * n + min(x - WALK_R * n, 2);
+}
+
+__global__ __launch_bounds__(64) void k_snappy_walk(KArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t wbuf[WALK_STAGE];
+  // merge table, per region position: 0xffff, or the pass-1 chain k that
+  // visits the token starting there (bit 14) and its output before it
+  __shared__ __attribute__((aligned(16))) uint16_t wtab[64 * WALK_R];
+  __shared__ uint8_t pjt[2][256];  // pass 2: state graph levels (ping-pong)
+  __shared__ int32_t xtab[192];    // exit position per state
+  __shared__ int32_t etab[64];     // entry position per region (-1: not on the chain)
+  // a few serial waves sharing the GPU with k_snappy's whole pages (side
+  // stream): their segments wait on them, so they win issue arbitration
+  __builtin_amdgcn_s_setprio(3);
   const int lane = lane_id();
-  const int wv = (int)ufirst(threadIdx.x >> 6);
-  const int wi = blockIdx.x * 4 + wv;
+  const int wi = blockIdx.x;
   if (wi >= a.nwalk) return;
-  uint8_t *wbuf = wbuf_all[wv];
+#ifdef PQ_SNAP_STAMPS
+  // diagnostic build: per page, cycles of the whole walk, 100 MHz ticks, staging +
+  // pass 1, pass 3, boundaries, path rounds, pass-1 steps, path hops
+  uint64_t wst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t wt0 = __builtin_amdgcn_s_memtime(), wrt0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t wtp = wt0;
+#define WALK_T(i)                                     \
+  do {                                                \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    wst[i] += t_ - wtp;                               \
+    wtp = t_;                                         \
+  } while (0)
+#define WALK_N(i, v) (wst[i] += (v))
+#else
+#define WALK_T(i) \
+  do {            \
+  } while (0)
+#define WALK_N(i, v) ((void)0)
+#endif
   const int gi = ufirst(a.walk[wi]);
   const int page = ufirst(a.list[gi]);
   const PageDesc d = a.pages[page];
@@ -1044,7 +1090,8 @@ __global__ __launch_bounds__(256) void k_snappy_walk(KArgs a) {
                                                (__attribute__((address_space(3))) void *)(wbuf + off), 16, 0, 0);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           wave_lds_sync();
-          const uint8_t *b = wbuf + ((uintptr_t)(src + s) - A);
+          const uint32_t *wb = (const uint32_t *)wbuf;
+          const int boff = (int)((uintptr_t)(src + s) - A);  // LDS byte of stream position s
           // positions relative to s; the chunk holds regions of lanes below
           // nreg (its end is the page end when that comes first)
           const int64_t rest = slen - s;
@@ -1062,76 +1109,111 @@ __global__ __launch_bounds__(256) void k_snappy_walk(KArgs a) {
             yk[k] = r0 + k;
             ok[k] = 0;
           }
+          uint16_t *tab = wtab + WALK_R * lane - r0;  // tab[r], r0 <= r < r1
+          for (int i = lane; i < 64 * WALK_R * 2 / 16; i += 64) ((uint4 *)wtab)[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+          wave_lds_sync();
           if (r0 < cend) {
             for (;;) {
               bool more = false;
 #pragma unroll
               for (int k = 0; k < WALK_K; k++) {
-                if (yk[k] < r1) {
-                  int32_t adv, len;
-                  walk_token(b, yk[k], adv, len);
-                  yk[k] += adv;
-                  ok[k] += len;
-                  more |= yk[k] < r1;
-                }
+                // predicated, not branched: finished chains re-read their exit
+                const bool act = yk[k] < r1;
+                int32_t adv, len;
+                if (act) tab[yk[k]] = (uint16_t)((k << 14) | ok[k]);
+                walk_token(wb, boff + min(yk[k], cend), adv, len);
+                yk[k] = act ? yk[k] + adv : yk[k];
+                ok[k] += act ? len : 0;
+                more |= yk[k] < r1;
               }
+              WALK_N(6, 1);
               if (!ballot(more)) break;
             }
           }
+          WALK_T(2);
           // a later entry (inside a literal that spans the region start) uses
           // the last chain as a guess, checked below
-          int32_t y = yk[WALK_K - 1];
-          // passes 2 + 3 until the true path agrees with the exits used
+          int32_t xg = yk[WALK_K - 1];
           int32_t entry = -1, tx = 0, tout = 0;  // my true entry, exit, output bytes
-          int32_t last = 0, guard = 0;
+          int32_t guard = 0;
           for (;;) {
-            // the true chain's lanes: 0 -> lane(exit(0)) -> ... (exits >= region ends)
-            int cur = 0, ein = 0;
-            entry = -1;
-            bool exact = false;
-            while (true) {
-              const int e = ein - WALK_R * cur;
-              int32_t ex = __builtin_amdgcn_readlane(y, cur), eo = -1;  // a guess unless an exact chain starts there
+            // pass 2: the true chain's regions.  State 3 l + c = region l
+            // entered at offset c (0, 1: exact chains; 2: any later entry, the
+            // guess), 192 = past the chunk.  Pointer jumping over the state
+            // graph: lane m lands on the m-th state of the chain from state 0
+            // (levels 2^j applied for the bits of m, as computed; they commute)
+            xtab[3 * lane + 0] = yk[0];
+            xtab[3 * lane + 1] = yk[1];
+            xtab[3 * lane + 2] = xg;
+            pjt[0][3 * lane + 0] = walk_state(yk[0], cend);
+            pjt[0][3 * lane + 1] = walk_state(yk[1], cend);
+            pjt[0][3 * lane + 2] = walk_state(xg, cend);
+            pjt[0][192 + lane] = 192;
+            pjt[1][192 + lane] = 192;
+            etab[lane] = -1;
+            wave_lds_sync();
+            int sm = 0;
 #pragma unroll
-              for (int k = 0; k < WALK_K; k++)
-                if (e == k) {  // scalar: the entry offset picks the chain
-                  ex = __builtin_amdgcn_readlane(yk[k], cur);
-                  eo = __builtin_amdgcn_readlane(ok[k], cur);
-                }
-              if (lane == cur) {
-                entry = ein;
-                exact = eo >= 0;
-                if (exact) {
-                  tx = ex;
-                  tout = eo;
-                }
+            for (int j = 0; j < 6; j++) {
+              const uint8_t *P = pjt[j & 1];
+              if ((lane >> j) & 1) sm = P[sm];
+              if (j < 5) {
+                uint8_t *Q = pjt[(j + 1) & 1];
+                const int a0 = P[3 * lane], a1 = P[3 * lane + 1], a2 = P[3 * lane + 2];
+                Q[3 * lane] = P[a0];
+                Q[3 * lane + 1] = P[a1];
+                Q[3 * lane + 2] = P[a2];
               }
-              last = cur;
-              if (ex >= cend) break;
-              ein = ex;
-              cur = ex / WALK_R;
+              wave_lds_sync();
             }
+            // the entry of the m-th state is the exit of the (m - 1)-th: give
+            // it to the region's lane
+            const int sp = __shfl_up(sm, 1);
+            if (sm != 192) etab[sm / 3] = lane == 0 ? 0 : xtab[sp];
+            wave_lds_sync();
+            entry = etab[lane];
+            const int c = entry < 0 ? 0 : min(entry - r0, 2);
+            const bool exact = entry >= 0 && c < 2;
+            if (exact) {
+              tx = c ? yk[1] : yk[0];
+              tout = c ? ok[1] : ok[0];
+            }
+            WALK_T(7);
             // pass 3: path lanes with a guessed exit walk from their true entry
+            // until they meet a pass-1 chain (merge table)
             bool bad = false;
             if (entry >= 0 && !exact) {
               int32_t adv, len;
               tout = 0;
               tx = entry;
               while (tx < r1) {
-                walk_token(b, tx, adv, len);
+                const uint32_t m = tab[tx];
+                if (m != 0xffffu) {
+                  const bool k1 = (m >> 14) & 1;
+                  tout += (k1 ? ok[WALK_K - 1] : ok[0]) - (int32_t)(m & 0x3fff);
+                  tx = k1 ? yk[WALK_K - 1] : yk[0];
+                  break;
+                }
+                walk_token(wb, boff + tx, adv, len);
                 tx += adv;
                 tout += len;
               }
-              bad = tx != y;
+              bad = tx != xg;
             }
             const uint64_t badm = ballot(bad);
+            WALK_N(5, 1);
             if (!badm || ++guard > 64) {
               if (badm) fail = true;
               break;
             }
-            if (bad) y = tx;  // correct the exits and retrace the path
+            if (bad) xg = tx;  // correct the exits and retrace the path
+            wave_lds_sync();   // the tables are rewritten
           }
-          if (entry >= 0) y = tx;  // the path lanes' true exits
+          // the chain leaves the chunk from the one path lane whose exit is past it
+          const uint64_t lastm = ballot(entry >= 0 && tx >= cend);
+          const int last = lastm ? (int)__builtin_ctzll(lastm) : 0;
+          if (!lastm) fail = true;
+          WALK_T(3);
           if (fail) break;
           // output positions of the path lanes' first tokens
           int32_t ctot;
@@ -1145,7 +1227,7 @@ __global__ __launch_bounds__(256) void k_snappy_walk(KArgs a) {
             int64_t o = o0;
             int32_t r = entry, adv, len;
             while (r < r1 && bnext < o0 + tout) {
-              walk_token(b, r, adv, len);
+              walk_token(wb, boff + r, adv, len);
               if (o == bnext) {
                 const int64_t k = bnext / SNAP_SEG;
                 if (k < nseg) a.segs[sb + k] = s + r;
@@ -1158,6 +1240,7 @@ __global__ __launch_bounds__(256) void k_snappy_walk(KArgs a) {
               r += adv;
             }
           }
+          WALK_T(4);
           if (ballot(bfail)) {
             fail = true;
             break;
@@ -1167,7 +1250,7 @@ __global__ __launch_bounds__(256) void k_snappy_walk(KArgs a) {
             nb += SNAP_SEG;
             kb++;
           }
-          s += __builtin_amdgcn_readlane(y, last);
+          s += __builtin_amdgcn_readlane(tx, last);
           wave_lds_sync();
         }
         flag = (!fail && kb >= nseg) ? 0u : 1u;
@@ -1175,6 +1258,14 @@ __global__ __launch_bounds__(256) void k_snappy_walk(KArgs a) {
     }
   }
   if (lane == 0) a.seg_flag[gi] = flag;
+#ifdef PQ_SNAP_STAMPS
+  wst[0] = __builtin_amdgcn_s_memtime() - wt0;
+  wst[1] = __builtin_amdgcn_s_memrealtime() - wrt0;
+  if (a.dbg3 && lane == 0)  // after the 256 run-walk stamps
+    for (int i = 0; i < 8; i++) a.dbg3[256 + (size_t)page * 8 + i] = wst[i];
+#endif
+#undef WALK_T
+#undef WALK_N
 }
 
 // ===========================================================================
@@ -3657,7 +3748,7 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
   }
   if (which == 17 || which == 18) {  // k_snappy_walk / serial fallback over the segmented pages
     if (k.nwalk <= 0) return 0;
-    if (which == 17) hipLaunchKernelGGL(pq::k_snappy_walk, dim3((k.nwalk + 3) / 4), dim3(256), 0, s, k);
+    if (which == 17) hipLaunchKernelGGL(pq::k_snappy_walk, dim3(k.nwalk), dim3(64), 0, s, k);
     else hipLaunchKernelGGL(pq::k_snappy<pq::SNAP_FALLBACK>, dim3((k.nwalk + 3) / 4), dim3(256), 0, s, k);
     return hipGetLastError() == hipSuccess ? 0 : 17;
   }

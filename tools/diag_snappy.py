@@ -64,3 +64,18 @@ for ci in sorted(set((pc >> 8).tolist())):
         " ".join("%6.1f%%" % (100 * x / max(tot.sum(), 1)) for x in tot), tot.sum() / max(nb, 1)))
     print("%16s longest wave kcyc: median %.0f p90 %.0f max %.0f; batches/page max %d" % (
         "", np.median(life) / 1e3, np.percentile(life, 90) / 1e3, life.max() / 1e3, ph[m, 7].max()))
+
+# k_snappy_walk (pages longer than one segment): per page, cycles of the walk
+# and its parts, chunks, path rounds and pass-1 steps (after the k_snappy
+# stamps and 256 run-walk stamps in the same buffer)
+full = np.zeros(16 * (npg + 1) + 256, np.uint64)
+L.pqg_diag_stamps2(b._h, full.ctypes.data, full.size)
+w = full[8 * (npg + 1) + 256:][:8 * npg].reshape(npg, 8).astype(np.float64)
+walked = np.nonzero(w[:, 0] > 0)[0]
+print("\nk_snappy_walk: %d pages" % walked.size)
+print("%-16s %4s %7s %7s %6s | %7s %7s %7s %7s | %6s %7s" % ("column", "kind", "KB in", "kcyc", "GHz", "pass1", "pass3", "bound", "hops",
+                                                           "rounds", "p1steps"))
+for p in walked[np.argsort(-w[walked, 0])][:40]:
+    print("%-16s %4d %7.0f %7.0f %6.2f | %6.1f%% %6.1f%% %6.1f%% %6.1f%% | %6d %7d" % (
+        names[pc[p] >> 8][:16], pc[p] & 255, pg[p, 3] / 1e3 if pg[p, 3] else 0, w[p, 0] / 1e3, w[p, 0] / max(w[p, 1], 1) / 10,
+        100 * w[p, 2] / w[p, 0], 100 * w[p, 3] / w[p, 0], 100 * w[p, 4] / w[p, 0], 100 * w[p, 7] / w[p, 0], w[p, 5], w[p, 6]))

@@ -1,0 +1,37 @@
+"""Diagnostic: the kernel timeline of one decode step (rocprofv3 kernel trace
+of a short `bench.py --child` run): per launch, its stream queue, start and
+end relative to the step's k_reset, and duration.
+
+usage: python tools/timeline.py CONFIG [extra bench args]   (on the GPU box)
+"""
+import csv
+import glob
+import os
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c5"
+with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+    cmd = ["timeout", "-s", "KILL", "150", "rocprofv3", "--kernel-trace", "--output-format", "csv", "-d", td, "-o", "run",
+           "--", sys.executable, os.path.join(ROOT, "bench.py"), "--child", "--steps", "3", "--warmup", "1",
+           "--config", cfg] + sys.argv[2:]
+    subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, check=True, timeout=180)
+    rows = []
+    for f in glob.glob(os.path.join(td, "**", "*kernel_trace.csv"), recursive=True):
+        rows += list(csv.DictReader(open(f)))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+name = lambda r: r["Kernel_Name"].split("(")[0].replace("void ", "").replace("pq::", "").strip()
+resets = [i for i, r in enumerate(rows) if name(r) == "k_reset"]
+if len(resets) < 2:
+    sys.exit("fewer than two decode steps in the trace")
+step = rows[resets[-2]:resets[-1]]  # the last complete step
+t0 = int(step[0]["Start_Timestamp"])
+end = max(int(r["End_Timestamp"]) for r in step)
+print("%s: step %.3f ms (k_reset to last end), %d launches" % (cfg, (end - t0) / 1e6, len(step)))
+print("%-22s %6s %9s %9s %9s %7s" % ("kernel", "queue", "start us", "end us", "dur us", "grid"))
+for r in step:
+    s, e = int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0
+    print("%-22s %6s %9.1f %9.1f %9.1f %7s" % (name(r)[:22], r.get("Queue_Id", r.get("Stream_Id", "")), s / 1e3, e / 1e3,
+                                             (e - s) / 1e3, r.get("Grid_Size", r.get("Grid_Size_X", ""))))
