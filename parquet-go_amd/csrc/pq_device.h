@@ -182,7 +182,10 @@ __device__ __forceinline__ uint32_t read_uvarint(Win &W, const uint8_t *p, int64
 // ---------------------------------------------------------------------------
 // RLE / bit-packed hybrid stream (hybrid_decoder.go:30-166)
 // ---------------------------------------------------------------------------
-struct Hyb {
+// TABLE = false: the serial header walk only (no run table, and none of its
+// registers: k_decode, whose register budget is tight).
+template <bool TABLE>
+struct HybT {
   const uint8_t *p;
   int64_t len;     // < 0: stream not initialised ("reader is not initialized")
   int64_t pos;     // next header
@@ -195,6 +198,23 @@ struct Hyb {
   int32_t got;     // values the last next4 / next produced (before an error: the ones the
                    // reference read successfully, value by value, hybrid_decoder.go:82-114)
   Win W;
+  // Run table (streams of short runs): up to 64 whole runs parsed at once,
+  // lane m holding run m — its first value (relative to t_base), kind and
+  // RLE value or bit-packed data offset.  The header chain inside the
+  // 256-byte window is found by pointer jumping (every byte position parsed
+  // as a header, lane m lands on header m), so a stream of short runs costs
+  // one window step per 64 runs instead of a serial header walk per run.
+  // Anything unusual (a header or payload past the stream, an oversized
+  // varint, an empty run) ends the table before it: the serial path reads it
+  // with the reference's exact errors.
+  int64_t vdone;   // values produced since init
+  int64_t t_base;  // value index of table run 0
+  int64_t t_end;   // value index after the table (t_end == vdone: no table)
+  int32_t t_n;     // runs in the table
+  int32_t t_try;   // build a table at the next header (short runs lately)
+  int32_t tr_s;    // lane m < t_n: run m's first value - t_base
+  uint32_t tr_v;   // RLE value, or bit-packed data offset in the stream
+  int32_t tr_k;    // 1 RLE, 0 bit-packed
 
   __device__ __forceinline__ void init(const uint8_t *ptr, int64_t n, int bitw) {
     p = ptr;
@@ -208,6 +228,12 @@ struct Hyb {
     rle = 0;
     got = 0;
     W.reset();
+    vdone = t_base = t_end = 0;
+    t_n = 0;
+    t_try = 1;
+    tr_s = 0x7fffffff;
+    tr_v = 0;
+    tr_k = 0;
   }
 
   // readRunHeader :143-166 (+ readRLERunValue :116-131)
@@ -241,11 +267,167 @@ struct Hyb {
       rem = c;
       rle_val = v;
     }
+    // serial runs: a short one suggests more (try the table at the next header)
+    t_try = rem < 64;
     return E_OK;
   }
 
-  // Produce the next n (<= 256) values, four per lane: value j goes to lane
-  // j >> 2, element j & 3.
+  // one window position i (relative to W.ab, i < 248) parsed as a run header:
+  // returns the position after its run (relative to W.ab; 0x7fffffff:
+  // not a whole, well-formed run inside the stream), its value count, and
+  // its RLE value / bit-packed data offset (relative to W.ab)
+  __device__ __forceinline__ int32_t parse_at(int i, int32_t &cnt, uint32_t &val, int32_t &kind, int32_t &hdr_len) const {
+    const int q = i >> 2, sb = i & 3;
+    const uint32_t d0 = shfl32(W.w, q), d1 = shfl32(W.w, q + 1 < 64 ? q + 1 : 63), d2 = shfl32(W.w, q + 2 < 64 ? q + 2 : 63);
+    const uint32_t x0 = __builtin_amdgcn_alignbyte(d1, d0, sb), x1 = __builtin_amdgcn_alignbyte(d2, d1, sb);
+    const uint64_t B = ((uint64_t)x1 << 32) | x0;  // bytes i .. i + 7
+    const uint32_t b0 = x0 & 0xff, b1 = (x0 >> 8) & 0xff, b2 = (x0 >> 16) & 0xff, b3 = x0 >> 24, b4 = x1 & 0xff;
+    const int hl = b0 < 0x80 ? 1 : b1 < 0x80 ? 2 : b2 < 0x80 ? 3 : b3 < 0x80 ? 4 : 5;
+    const uint64_t h = (uint64_t)(b0 & 0x7f) | ((uint64_t)(b1 & 0x7f) << 7) * (hl > 1) |
+                       ((uint64_t)(b2 & 0x7f) << 14) * (hl > 2) | ((uint64_t)(b3 & 0x7f) << 21) * (hl > 3) |
+                       ((uint64_t)b4 << 28) * (hl > 4);
+    const int sz = (bw + 7) >> 3;
+    bool ok = !(hl == 5 && b4 >= 0x08) && h <= 0x7fffffffull && (h >> 1) != 0;
+    const bool bp = h & 1;
+    const int64_t g = (int64_t)(h >> 1);
+    int64_t nx;
+    uint32_t v = 0;
+    if (bp) {
+      nx = (int64_t)i + hl + g * bw;
+      cnt = g <= (1 << 22) ? (int32_t)(g * 8) : (1 << 25);
+      v = (uint32_t)(i + hl);
+    } else {
+      nx = (int64_t)i + hl + sz;
+      ok &= hl + sz <= 8;
+      const uint64_t rv = B >> (8 * hl);
+      v = sz == 0 ? 0u : (uint32_t)(rv & (sz >= 4 ? 0xffffffffull : ((1ull << (8 * sz)) - 1)));
+      ok &= bw >= 32 || (v >> bw) == 0;
+      cnt = g <= (1 << 25) ? (int32_t)g : (1 << 25);
+    }
+    // the whole run lies inside the stream
+    ok &= (int64_t)(W.ab - p) + nx <= len;
+    val = v;
+    kind = bp ? 0 : 1;
+    hdr_len = hl;
+    return ok ? (int32_t)nx : 0x7fffffff;
+  }
+
+  // build a table of the runs from header `pos` (0: none, serial path)
+  __device__ __forceinline__ int build_table() {
+    const int lane = lane_id();
+    if (pos >= len || len < 0) return 0;
+    if ((uint64_t)(p + pos - W.ab) > 8) {
+      W.ab = (const uint8_t *)((uintptr_t)(p + pos) & ~(uintptr_t)3);
+      W.w = ((const uint32_t *)W.ab)[lane];
+    }
+    const int h0 = (int)(p + pos - W.ab);
+    // J_0 over positions 4 lane + k: the next header, 256 = none
+    uint32_t j01 = 0, j23 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int i = 4 * lane + k;
+      int32_t c, kd, hl;
+      uint32_t v;
+      const int32_t nx0 = parse_at(i < 248 ? i : 0, c, v, kd, hl);
+      const int32_t nx = i < 248 ? nx0 : 0x7fffffff;
+      const uint32_t J = nx < 248 ? (uint32_t)nx : 256u;
+      if (k == 0) j01 = J;
+      if (k == 1) j01 |= J << 16;
+      if (k == 2) j23 = J;
+      if (k == 3) j23 |= J << 16;
+    }
+    auto gather = [&](uint32_t x) -> uint32_t {  // J_b(x), x <= 256
+      const int l = (int)(x >> 2) & 63;
+      const uint32_t a = shfl32(j01, l), b = shfl32(j23, l);
+      const uint32_t w = (x & 2) ? b : a;
+      const uint32_t r = (x & 1) ? (w >> 16) : (w & 0xffff);
+      return x >= 256 ? 256u : r;
+    };
+    uint32_t at = (uint32_t)h0;  // lane m: header m
+#pragma unroll
+    for (int b = 0; b < 6; b++) {
+      const uint32_t hop = gather(at);
+      if ((lane >> b) & 1) at = hop;
+      if (b < 5) {
+        const uint32_t n0 = gather(j01 & 0xffff), n1 = gather(j01 >> 16), n2 = gather(j23 & 0xffff), n3 = gather(j23 >> 16);
+        j01 = n0 | (n1 << 16);
+        j23 = n2 | (n3 << 16);
+      }
+    }
+    // my run (a header every hop before me is whole and well-formed)
+    int32_t c = 0, kd = 0, hl = 0;
+    uint32_t v = 0;
+    // (every lane parses: a masked lane's window dword would not reach the shuffles)
+    const int32_t nx = parse_at(at < 248 ? (int)at : 0, c, v, kd, hl);
+    const bool valid = at < 248 && nx != 0x7fffffff;
+    const uint64_t vm = ballot(valid);
+    int R = ~vm ? (int)__builtin_ctzll(~vm) : 64;  // leading runs
+    // a huge run ends the table (its count was clamped)
+    const uint64_t big = ballot(lane < R && c >= (1 << 25));
+    if (big) R = min(R, (int)__builtin_ctzll(big));
+    if (R == 0) return 0;
+    int32_t tot = 0;
+    const int32_t st = wave_excl_scan32(lane < R ? c : 0, &tot);
+    tr_s = lane < R ? st : 0x7fffffff;
+    tr_k = kd;
+    tr_v = kd ? v : (uint32_t)((int64_t)(W.ab - p) + (int64_t)v);
+    t_n = R;
+    t_base = vdone;
+    t_end = vdone + tot;
+    pos = (int64_t)(W.ab - p) + (int64_t)__builtin_amdgcn_readlane(nx, R - 1);
+    t_try = tot < 64 * R;  // keep building while the runs stay short
+    return R;
+  }
+
+  // value number rel (relative to t_base) of the table
+  __device__ __forceinline__ uint32_t table_value(int32_t rel) const {
+    int r = 0;
+#pragma unroll
+    for (int st = 32; st >= 1; st >>= 1) {
+      const int32_t s2 = (int32_t)shfl32((uint32_t)tr_s, r + st < 64 ? r + st : 63);
+      if (r + st < t_n && s2 <= rel) r += st;
+    }
+    const int32_t s0 = (int32_t)shfl32((uint32_t)tr_s, r);
+    const uint32_t v = shfl32(tr_v, r);
+    const int32_t k = (int32_t)shfl32((uint32_t)tr_k, r);
+    const int64_t bitpos = (int64_t)v * 8 + (int64_t)(rel - s0) * bw;
+    const uint64_t o = (uint64_t)(p + (bitpos >> 3) - W.ab);
+    const bool inwin = o + 8 <= 256;
+    // every lane takes part in the window's shuffles (a masked lane's
+    // register does not reach ds_bpermute); a position past the window (the
+    // last run's tail) is read from memory
+    const uint32_t wv = win_unpack(inwin ? bitpos : (int64_t)(W.ab - p) * 8);
+    if (k) return v;
+    return inwin ? wv : unpack_u32(p, len, bitpos, bw);
+  }
+
+  // Bit-packed values of the current run from the register window: the bytes
+  // [lo, hi) of the stream are made resident (one refill, a 256-byte load)
+  // when they fit; false when they do not (wide values: the caller reads
+  // memory).  One global load per window instead of one per run: level
+  // streams of short runs waited on a load per run.
+  __device__ __forceinline__ bool window_covers(int64_t lo, int64_t hi) {
+    if (hi - lo > 248) return false;
+    const uint64_t o0 = (uint64_t)(p + lo - W.ab), o1 = (uint64_t)(p + hi - W.ab);
+    if (o0 < 256 && o1 <= 256) return true;
+    W.ab = (const uint8_t *)((uintptr_t)(p + lo) & ~(uintptr_t)3);
+    W.w = ((const uint32_t *)W.ab)[lane_id()];
+    return true;
+  }
+  // value at stream bit `bitpos` (bw bits, LSB first) from the window; bytes
+  // at or beyond len read as zero (unpack_u32)
+  __device__ __forceinline__ uint32_t win_unpack(int64_t bitpos) const {
+    const int64_t byte = bitpos >> 3;
+    const uint32_t off = (uint32_t)(uint64_t)(p + byte - W.ab);  // <= 248
+    const int li = (int)(off >> 2) & 63;
+    const uint32_t d0 = shfl32(W.w, li), d1 = shfl32(W.w, li + 1 < 64 ? li + 1 : 63);
+    const uint64_t v = (((uint64_t)d1 << 32) | d0) >> ((off & 3) * 8 + (uint32_t)(bitpos & 7));
+    uint32_t val = (uint32_t)v & (bw == 32 ? 0xffffffffu : ((1u << bw) - 1));
+    const int64_t avail = (len - byte) * 8 - (bitpos & 7);
+    if (avail < bw) val = avail <= 0 ? 0u : (val & ((1u << avail) - 1));
+    return val;
+  }
+
   // Bit-packed values [vi, vi + take) of the current run that the reference can
   // read: every 8-value group must start inside the stream (a short last group
   // is zero-filled, readBitPackedRun :133-141).
@@ -256,81 +438,180 @@ struct Hyb {
     return (int)max<int64_t>(0, min<int64_t>((int64_t)take, groups * 8 - vi));
   }
 
-  __device__ uint32_t next4(int n, uint32_t (&out)[4]) {
+  // Produce the next n (<= 256) values, PER values a lane: value j goes to
+  // lane j / PER, element j % PER (next4: PER 4, n <= 256; next: PER 1, n <= 64).
+  template <int PER>
+  __device__ __forceinline__ uint32_t produce(int n, uint32_t (&out)[PER]) {
     const int lane = lane_id();
 #pragma unroll
-    for (int k = 0; k < 4; k++) out[k] = 0;
+    for (int k = 0; k < PER; k++) out[k] = 0;
     got = 0;
-    if (bw == 0) {
+    if (bw == 0) {  // hybrid_decoder.go:84-86
       got = n;
+      vdone += n;
       return E_OK;
     }
     while (got < n) {
       if (rem == 0) {
+        if (TABLE && t_end <= vdone && t_try) build_table();
+        if (TABLE && t_end > vdone) {  // from the table
+          const int take = (int)min<int64_t>(t_end - vdone, (int64_t)(n - got));
+          const int32_t rel0 = (int32_t)(vdone - t_base) - got;
+#pragma unroll
+          for (int k = 0; k < PER; k++) {
+            const int j = PER * lane + k;
+            const bool in = j >= got && j < got + take;
+            const uint32_t v = table_value(rel0 + (in ? j : got));
+            if (in) out[k] = v;
+          }
+          got += take;
+          vdone += take;
+          continue;
+        }
         uint32_t e = header();
         if (e) return e;
       }
       int take = (int)min<int64_t>(rem, (int64_t)(n - got));
       if (rle) {
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-          int j = 4 * lane + k;
+        for (int k = 0; k < PER; k++) {
+          int j = PER * lane + k;
           if (j >= got && j < got + take) out[k] = rle_val;
         }
       } else {
         const int ok = readable(take);
         const int64_t bit0 = data * 8 + (vi - got) * (int64_t)bw;
+        if (window_covers(data + ((vi * bw) >> 3), data + (((vi + take) * bw + 7) >> 3) + 8)) {
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-          int j = 4 * lane + k;
-          if (j >= got && j < got + ok) out[k] = unpack_u32(p, len, bit0 + (int64_t)j * bw, bw);
+          for (int k = 0; k < PER; k++) {
+            const int j = PER * lane + k;
+            const bool in = j >= got && j < got + ok;
+            const uint32_t v = win_unpack(bit0 + (int64_t)(in ? j : got) * bw);  // every lane shuffles
+            if (in) out[k] = v;
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < PER; k++) {
+            int j = PER * lane + k;
+            if (j >= got && j < got + ok) out[k] = unpack_u32(p, len, bit0 + (int64_t)j * bw, bw);
+          }
         }
         if (ok < take) {  // a group starting at the end of the stream: io.EOF
           got += ok;
+          vdone += ok;
           return E_EOF;
         }
         vi += take;
       }
       rem -= take;
       got += take;
+      vdone += take;
     }
     return E_OK;
   }
 
-  // Produce the next n (<= 64) values: lane l < n receives value l.
-  __device__ uint32_t next(int n, uint32_t &out) {
-    int lane = lane_id();
-    out = 0;
-    got = 0;
-    if (bw == 0) {  // hybrid_decoder.go:84-86
-      got = n;
+  // bit-packed values [lo, hi) of the run whose value 0 is at stream bit b0
+  // (lo, hi relative to the run), counted: == A into cA, >= B into cB
+  __device__ __forceinline__ void count_packed(int64_t b0, int64_t lo, int64_t hi, uint32_t A, uint32_t B, int64_t &cA,
+                                               int64_t &cB) {
+    const int lane = lane_id();
+    for (int64_t j0 = lo; j0 < hi; j0 += 64) {
+      const int64_t j = j0 + lane;
+      const bool in = j < hi;
+      const int64_t last = min<int64_t>(j0 + 64, hi) - 1;
+      uint32_t v;
+      const int64_t blo = (b0 + j0 * bw) >> 3, bhi = ((b0 + (last + 1) * bw + 7) >> 3) + 8;
+      if (window_covers(blo, bhi)) v = win_unpack(b0 + (in ? j : j0) * bw);
+      else v = in ? unpack_u32(p, len, b0 + j * bw, bw) : 0u;
+      cA += __popcll(ballot(in && v == A));
+      cB += __popcll(ballot(in && v >= B));
+    }
+  }
+
+  // Consume the next n values (any n), counting those == A (cA) and >= B
+  // (cB): the count path of k_prepare, no value leaves the run table (RLE
+  // runs count whole).  Errors as next4 would report reading them.
+  __device__ uint32_t count2(int64_t n, uint32_t A, uint32_t B, int64_t &cA, int64_t &cB) {
+    const int lane = lane_id();
+    if (n <= 0) return E_OK;
+    if (bw == 0) {  // all zeros
+      cA += A == 0 ? n : 0;
+      cB += B == 0 ? n : 0;
+      vdone += n;
       return E_OK;
     }
-    while (got < n) {
+    int64_t left = n;
+    while (left > 0) {
       if (rem == 0) {
-        uint32_t e = header();
-        if (e) return e;
+        if (TABLE && t_end <= vdone && t_try) build_table();
+        if (TABLE && t_end > vdone) {
+          const int64_t take = min<int64_t>(t_end - vdone, left);
+          const int32_t rel0 = (int32_t)(vdone - t_base), rel1 = rel0 + (int32_t)take;
+          const int32_t nxt = (int32_t)shfl32((uint32_t)tr_s, lane + 1 < 64 ? lane + 1 : 63);
+          const int32_t e = lane + 1 < t_n ? nxt : (int32_t)(t_end - t_base);
+          const bool mine = lane < t_n;
+          const int32_t lo = max(tr_s, rel0), hi = min(e, rel1);
+          const int64_t c = mine && hi > lo ? (int64_t)(hi - lo) : 0;
+          // RLE runs: whole counts, summed over the wave
+          int64_t ra = mine && tr_k && tr_v == A ? c : 0, rb = mine && tr_k && tr_v >= B ? c : 0;
+#pragma unroll
+          for (int d = 32; d >= 1; d >>= 1) {
+            ra += (int64_t)shfl64((uint64_t)ra, lane ^ d);
+            rb += (int64_t)shfl64((uint64_t)rb, lane ^ d);
+          }
+          cA += ufirst64(ra);
+          cB += ufirst64(rb);
+          // bit-packed runs: their values, 64 at a time
+          uint64_t bpm = ballot(mine && !tr_k && c > 0);
+          while (bpm) {
+            const int m = (int)__builtin_ctzll(bpm);
+            bpm &= bpm - 1;
+            const int32_t sm = __builtin_amdgcn_readlane(tr_s, m), lm = __builtin_amdgcn_readlane(lo, m),
+                          hm = __builtin_amdgcn_readlane(hi, m);
+            const uint32_t dm = __builtin_amdgcn_readlane(tr_v, m);
+            count_packed((int64_t)dm * 8, lm - sm, hm - sm, A, B, cA, cB);
+          }
+          vdone += take;
+          left -= take;
+          continue;
+        }
+        uint32_t er = header();
+        if (er) return er;
       }
-      int take = (int)min<int64_t>(rem, (int64_t)(n - got));
-      bool mine = lane >= got && lane < got + take;
+      const int64_t take = min<int64_t>(rem, left);
       if (rle) {
-        if (mine) out = rle_val;
+        cA += rle_val == A ? take : 0;
+        cB += rle_val >= B ? take : 0;
       } else {
-        // every bit-packed group needed must start inside the stream (:133-141)
-        const int ok = readable(take);
-        if (lane >= got && lane < got + ok) out = unpack_u32(p, len, data * 8 + (vi + (lane - got)) * (int64_t)bw, bw);
+        const int ok = readable((int)min<int64_t>(take, 1 << 30));
+        count_packed(data * 8, vi, vi + ok, A, B, cA, cB);
         if (ok < take) {
-          got += ok;
+          vdone += ok;
           return E_EOF;
         }
         vi += take;
       }
       rem -= take;
-      got += take;
+      left -= take;
+      vdone += take;
     }
     return E_OK;
   }
+
+  // Produce the next n (<= 256) values, four per lane: value j goes to lane
+  // j >> 2, element j & 3.
+  __device__ __forceinline__ uint32_t next4(int n, uint32_t (&out)[4]) { return produce<4>(n, out); }
+
+  // Produce the next n (<= 64) values: lane l < n receives value l.
+  __device__ __forceinline__ uint32_t next(int n, uint32_t &out) {
+    uint32_t o[1];
+    const uint32_t e = produce<1>(n, o);
+    out = o[0];
+    return e;
+  }
 };
+using Hyb = HybT<true>;     // run tables (k_prepare's count path, k_level_check)
+using HybS = HybT<false>;   // serial (k_decode)
 
 // ---------------------------------------------------------------------------
 // DELTA_BINARY_PACKED (deltabp_decoder.go:14-334); lanes receive delta+minDelta

@@ -578,6 +578,7 @@ struct pqg_batch {
   pqg_file *file = nullptr;
   int rg_begin = 0, rg_end = 0, flags = 0;
   std::vector<ColumnPlan> cols;
+  std::vector<int64_t> page_foff;  // per page: payload offset in the file (host)
   std::vector<PageDesc> pages;
   std::vector<uint32_t> status0;  // host-side initial status per page
   std::vector<int32_t> snappy_list, dict_list, data_list;
@@ -1087,6 +1088,41 @@ struct HostBuf {  // the device input buffer's layout: byte ranges of the (mappe
 constexpr size_t kPad = 4096;  // readable slack after every device buffer (1 KiB register windows)
 }  // namespace
 
+// Snappy stream whose first 256 KiB of output (or 4096 tokens) are at least
+// 3/4 long literals (>= 1 KiB): an incompressible body, which one k_snappy
+// wave hands to k_copy a token at a time — nothing serial to cut into
+// segments.  A peek at the host copy; anything malformed answers false.
+static bool snappy_long_literals(const uint8_t *p, int64_t n) {
+  int64_t i = 0;
+  for (int k = 0; k < 10 && i < n; k++)  // preamble
+    if (p[i++] < 0x80) break;
+  int64_t out = 0, lit = 0;
+  for (int t = 0; t < 4096 && i < n && out < (256 << 10); t++) {
+    const uint32_t tag = p[i], x = tag >> 2;
+    int64_t len, adv;
+    if ((tag & 3) == 0) {
+      if (x < 60) {
+        len = x + 1;
+        adv = 1 + len;
+      } else {
+        const int extra = (int)x - 59;
+        if (i + 1 + extra > n) return false;
+        uint32_t v = 0;
+        for (int q = 0; q < extra; q++) v |= (uint32_t)p[i + 1 + q] << (8 * q);
+        len = (int64_t)v + 1;
+        adv = 1 + extra + len;
+      }
+      if (len >= 1024) lit += len;
+    } else {
+      len = (tag & 3) == 1 ? 4 + (x & 7) : x + 1;
+      adv = (tag & 3) == 1 ? 2 : (tag & 3) == 2 ? 3 : 5;
+    }
+    out += len;
+    i += adv;
+  }
+  return out > 0 && lit * 4 >= out * 3;
+}
+
 static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t, std::vector<uint8_t>>> &host_bodies,
                       int64_t &stage_off, int ci, int rg) {
   pqg_file *f = B->file;
@@ -1186,6 +1222,7 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
     d.ord = w.ord;
     d.dict = dict_idx;
     d.src = base + (uint64_t)(w.payload - chunk_lo);
+    B->page_foff.push_back(w.payload);  // host copy of the payload (segment planning peeks at it)
     uint32_t st = STATUS_OK;
     auto fail = [&](uint32_t stage, int code) {
       if (st == STATUS_OK) st = make_status(stage, (uint32_t)code);
@@ -1569,11 +1606,23 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     std::vector<It> items;
     B->seg_base.assign(B->snappy_list.size() + 1, 0);
     for (size_t q = 0; q < B->snappy_list.size(); q++) {
-      const int64_t body = B->pages[(size_t)B->snappy_list[q]].body_len;
+      const int32_t pq = B->snappy_list[q];
+      const PageDesc &pd = B->pages[(size_t)pq];
+      const int64_t body = pd.body_len;
       // long pages only: their serial token chains set k_snappy's critical
       // path, while the walk that finds segment starts costs a pass over the
-      // compressed bytes (PQG_SNAPPY_SEG_MIN: the threshold, bytes)
-      const int32_t nseg = use_seg && body >= seg_min ? (int32_t)((body + kSnapSeg - 1) / kSnapSeg) : 1;
+      // compressed bytes (PQG_SNAPPY_SEG_MIN: the threshold, bytes).  Not a
+      // page of long literals that k_copy takes (it parallelises them
+      // already; BYTE_ARRAY dictionaries copy their own)
+      bool cut = use_seg && body >= seg_min;
+      const bool defers = !(pd.kind == PAGE_DICT && B->cols[(size_t)pd.col].info.physical_type == T_BYTE_ARRAY);
+      if (cut && defers) {
+        const int64_t lsize = pd.kind == PAGE_V2 ? (int64_t)pd.v2_rep_len + pd.v2_def_len : 0;
+        const int64_t fo = B->page_foff[(size_t)pq] + lsize;
+        if (fo >= 0 && fo + (int64_t)pd.comp_len <= (int64_t)B->file->len)
+          cut = !snappy_long_literals(B->file->data + fo, pd.comp_len);
+      }
+      const int32_t nseg = cut ? (int32_t)((body + kSnapSeg - 1) / kSnapSeg) : 1;
       B->seg_base[q + 1] = B->seg_base[q] + nseg;
       if (nseg > 1) B->walk_list.push_back((int32_t)q);
       for (int32_t k = 0; k < nseg; k++)
@@ -1651,10 +1700,12 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   std::vector<int32_t> job_base(B->snappy_list.size() + 1), job_owner;
   for (size_t q = 0; q < B->snappy_list.size(); q++) {
     job_base[q] = (int32_t)job_owner.size();
-    // dictionary pages copy their long literals themselves: k_dict_prepare
-    // runs beside the data pages' Snappy decode, before k_copy
+    // BYTE_ARRAY dictionary pages copy their long literals themselves:
+    // k_dict_prepare reads them beside the data pages' Snappy decode, before
+    // k_copy (fixed-width dictionaries are read after it)
     const PageDesc &sp = B->pages[(size_t)B->snappy_list[q]];
-    int32_t cap = sp.kind == PAGE_DICT ? 0 : std::min(64, sp.body_len / (16 * 1024));
+    const bool ba_dict = sp.kind == PAGE_DICT && B->cols[(size_t)sp.col].info.physical_type == T_BYTE_ARRAY;
+    int32_t cap = ba_dict ? 0 : std::min(64, sp.body_len / (16 * 1024));
     for (int32_t k = 0; k < cap; k++) job_owner.push_back((int32_t)q);
   }
   B->max_jobs = (uint32_t)job_owner.size();

@@ -1079,6 +1079,31 @@ __global__ __launch_bounds__(64) void k_snappy_walk(KArgs a) {
             nb += SNAP_SEG;
             continue;
           }
+          {
+            // a long literal at s: stepped over from its header, no staging
+            // (an incompressible block is one literal); one that spans a
+            // boundary means no segments
+            const uint32_t tag = W.byte_at(src + s);
+            if ((tag & 3) == 0 && (tag >> 2) >= 60) {
+              const int extra = (int)(tag >> 2) - 59;
+              if (s + 1 + extra > slen) {
+                fail = true;
+                break;
+              }
+              uint32_t v = 0;
+              for (int k = 0; k < extra; k++) v |= W.byte_at(src + s + 1 + k) << (8 * k);
+              const int64_t len = (int64_t)v + 1;
+              if (len >= 1024) {
+                if (out + len > nb || s + 1 + extra + len > slen) {
+                  fail = true;
+                  break;
+                }
+                out += len;
+                s += 1 + extra + len;
+                continue;
+              }
+            }
+          }
           // stage [s, s + WALK_CHUNK + lookahead) by LDS-DMA, 1 KiB a piece (lane
           // l's 16 bytes at +16 l); readable slack follows every chunk (kPad)
           const uintptr_t A = (uintptr_t)(src + s) & ~(uintptr_t)15;
@@ -1912,6 +1937,9 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
 // ===========================================================================
 // Page gi of the list.  mode -1: every page; 0: pages whose body does not
 // wait on k_copy (run beside it, k_prepare_copy); 1: only the pages that do.
+// TABLE: level counts through run tables (k_prepare); k_prepare_copy, whose
+// registers also hold the copy loop, counts with the serial walk
+template <bool TABLE>
 __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lbytes, uint16_t *lnx, int mode) {
   if (gi >= a.nlist) return;
   const int lane = lane_id();
@@ -2042,40 +2070,38 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
 
   // counts for lists / strings: decode the level streams (phase 2 stages)
   const int n = d.num_values;
-  Hyb rep, def;
+  using Lv = HybT<TABLE>;
+  // diagnostic build: count-path stamps (1 levels start, 2 rep done, 6 def
+  // done, 7 strings done; 3 values, 4 = 100 + encoding)
+  PSTAMP(page, 1, __builtin_amdgcn_s_memrealtime());
+  PSTAMP(page, 3, (uint64_t)n);
+  PSTAMP(page, 4, (uint64_t)(100 + d.enc));
+  Lv rep, def;
   rep.init(ps.lvl + ps.rep_off, ps.rep_len, bits_len(c.max_rep));
   def.init(ps.lvl + ps.def_off, ps.def_len, bits_len(c.max_def));
   int64_t rows = 0, slots = 0, nn = 0;
-  // 256 entries a round, four per lane (entry 4 * lane + k in element k)
-  for (int e0 = 0; e0 < n && c.max_rep > 0; e0 += 256) {
-    const int cnt = min(256, n - e0);
-    uint32_t r[4];
-    e = rep.next4(cnt, r);
+  // whole runs counted from the run table (Hyb::count2): rows = rep levels
+  // 0; non-null = def levels max_def; slots = def levels >= rep_def
+  if (c.max_rep > 0) {
+    int64_t unused = 0;
+    e = rep.count2(n, 0u, 0xffffffffu, rows, unused);
     if (e) {
       set_status(a.status, page, ST_REP, e);
       return;
     }
-#pragma unroll
-    for (int k = 0; k < 4; k++) rows += __popcll(ballot(4 * lane + k < cnt && r[k] == 0));
   }
-  for (int e0 = 0; e0 < n; e0 += 256) {
-    const int cnt = min(256, n - e0);
-    uint32_t dl[4] = {0, 0, 0, 0};
-    if (c.max_def > 0) {
-      e = def.next4(cnt, dl);
-      if (e) {
-        set_status(a.status, page, ST_DEF, e);
-        return;
-      }
+  PSTAMP(page, 2, __builtin_amdgcn_s_memrealtime());
+  if (c.max_def > 0) {
+    e = def.count2(n, (uint32_t)c.max_def, c.max_rep > 0 ? (uint32_t)c.rep_def : 0u, nn, slots);
+    if (e) {
+      set_status(a.status, page, ST_DEF, e);
+      return;
     }
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const bool act = 4 * lane + k < cnt;
-      nn += __popcll(ballot(act && (int)dl[k] == c.max_def));
-      slots += __popcll(ballot(act && (c.max_rep == 0 || (int)dl[k] >= c.rep_def)));
-    }
+  } else {
+    nn = slots = n;  // no def levels: every value is defined
   }
   if (c.max_rep == 0) rows = n;
+  PSTAMP(page, 6, __builtin_amdgcn_s_memrealtime());
   // string bytes of the non-null values
   int64_t sbytes = 0;
   if (c.ptype == T_BYTE_ARRAY && nn > 0) {
@@ -2102,7 +2128,7 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
     } else if (d.enc == ENC_RLE_DICT) {
       if (d.dict < 0) {
         // dictDecoder with no dictionary: the first key is out of range
-        Hyb keys;
+        Lv keys;
         keys.init(ps.body + ps.val_off + 1, ps.val_len - 1, idx_bw);
         uint32_t k;
         e = keys.next(1, k);
@@ -2111,7 +2137,7 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
       }
       const PageDesc dd = a.pages[d.dict];
       const int64_t dn = dd.num_values;
-      Hyb keys;
+      Lv keys;
       keys.init(ps.body + ps.val_off + 1, ps.val_len - 1, idx_bw);
       int64_t acc = 0;
       for (int64_t k0 = 0; k0 < nn; k0 += 64) {
@@ -2180,6 +2206,7 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
       return;
     }
   }
+  PSTAMP(page, 7, __builtin_amdgcn_s_memrealtime());
   if (lane == 0) {
     pi->rows = rows;
     pi->slots = slots;
@@ -2189,11 +2216,11 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
 }
 
 template <int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_prepare(KArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_prepare(KArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t wl_bytes[4][1024];  // run walk: window bytes
   __shared__ __attribute__((aligned(16))) uint16_t wl_nx[4][2048];    // run walk: chain table (BYTE_ARRAY walk: two)
   const int wv = (int)ufirst(threadIdx.x >> 6);
-  prepare_page(a, (int)blockIdx.x * 4 + wv, wl_bytes[wv], wl_nx[wv], MODE);
+  prepare_page<true>(a, (int)blockIdx.x * 4 + wv, wl_bytes[wv], wl_nx[wv], MODE);
 }
 
 // k_prepare beside k_copy in one launch (batches without BYTE_ARRAY
@@ -2207,7 +2234,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
   const uint32_t pb = ((uint32_t)a.nlist + 3) / 4;
   if (blockIdx.x < pb) {
     const int wv = (int)ufirst(threadIdx.x >> 6);
-    prepare_page(a, (int)blockIdx.x * 4 + wv, wl_bytes[wv], wl_nx[wv], 0);
+    prepare_page<false>(a, (int)blockIdx.x * 4 + wv, wl_bytes[wv], wl_nx[wv], 0);
     return;
   }
   copy_items(a, blockIdx.x - pb, gridDim.x - pb);
@@ -2404,11 +2431,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   const bool is_bool = KIND == 0 && c.ptype == T_BOOLEAN;
   const bool emit_lv = KIND == 0 && (c.flags & COL_EMIT_LEVELS);
 
-  Hyb rep, def;
+  HybS rep, def;
   rep.init(lvl + pi.rep_off, pi.rep_len, bits_len(c.max_rep));
   def.init(lvl + pi.def_off, pi.def_len, bits_len(c.max_def));
 
-  Hyb keys;
+  HybS keys;
   Delta dz;
   const PageDesc *dp = d.dict >= 0 ? &a.pages[d.dict] : nullptr;
   const uint8_t *dict_vals = nullptr;
