@@ -71,6 +71,9 @@ struct PageDesc {
                          // suffix / prefix lengths; PLAIN (offset, length) per value from k_prepare's walk
   int32_t sidx;          // index in the Snappy page list (-1: not decoded by k_snappy)
   int32_t pad2;
+  int64_t lvl_base;      // page with levels on k_prepare's count path: byte offset of its decoded
+                         // levels in the level scratch (rep bytes if max_rep > 0, then def bytes,
+                         // num_values each); -1: k_decode reads the level streams itself
 };
 
 // Tiled flat decode (k_prepare's run walk + k_expand).  The run walk records,

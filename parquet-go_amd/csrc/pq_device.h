@@ -511,9 +511,10 @@ struct HybT {
   }
 
   // bit-packed values [lo, hi) of the run whose value 0 is at stream bit b0
-  // (lo, hi relative to the run), counted: == A into cA, >= B into cB
+  // (lo, hi relative to the run), counted: == A into cA, >= B into cB; with
+  // dst (the run's value 0), each stored as a byte
   __device__ __forceinline__ void count_packed(int64_t b0, int64_t lo, int64_t hi, uint32_t A, uint32_t B, int64_t &cA,
-                                               int64_t &cB) {
+                                               int64_t &cB, uint8_t *dst) {
     const int lane = lane_id();
     for (int64_t j0 = lo; j0 < hi; j0 += 64) {
       const int64_t j = j0 + lane;
@@ -525,18 +526,25 @@ struct HybT {
       else v = in ? unpack_u32(p, len, b0 + j * bw, bw) : 0u;
       cA += __popcll(ballot(in && v == A));
       cB += __popcll(ballot(in && v >= B));
+      if (dst && in) dst[j] = (uint8_t)v;
     }
+  }
+  // RLE value v for values [lo, hi) of dst
+  __device__ __forceinline__ static void fill_run(uint8_t *dst, int64_t lo, int64_t hi, uint32_t v) {
+    for (int64_t j = lo + lane_id(); j < hi; j += 64) dst[j] = (uint8_t)v;
   }
 
   // Consume the next n values (any n), counting those == A (cA) and >= B
   // (cB): the count path of k_prepare, no value leaves the run table (RLE
-  // runs count whole).  Errors as next4 would report reading them.
-  __device__ uint32_t count2(int64_t n, uint32_t A, uint32_t B, int64_t &cA, int64_t &cB) {
+  // runs count whole).  Errors as next4 would report reading them.  With
+  // dst, value i (since init) is also stored at dst[i] (one byte).
+  __device__ uint32_t count2(int64_t n, uint32_t A, uint32_t B, int64_t &cA, int64_t &cB, uint8_t *dst = nullptr) {
     const int lane = lane_id();
     if (n <= 0) return E_OK;
     if (bw == 0) {  // all zeros
       cA += A == 0 ? n : 0;
       cB += B == 0 ? n : 0;
+      if (dst) fill_run(dst, vdone, vdone + n, 0u);
       vdone += n;
       return E_OK;
     }
@@ -561,6 +569,15 @@ struct HybT {
           }
           cA += ufirst64(ra);
           cB += ufirst64(rb);
+          if (dst) {  // RLE runs' bytes, a run at a time
+            uint64_t rm = ballot(mine && tr_k && c > 0);
+            while (rm) {
+              const int m = (int)__builtin_ctzll(rm);
+              rm &= rm - 1;
+              const int32_t lm = __builtin_amdgcn_readlane(lo, m), hm = __builtin_amdgcn_readlane(hi, m);
+              fill_run(dst, t_base + lm, t_base + hm, __builtin_amdgcn_readlane(tr_v, m));
+            }
+          }
           // bit-packed runs: their values, 64 at a time
           uint64_t bpm = ballot(mine && !tr_k && c > 0);
           while (bpm) {
@@ -569,7 +586,7 @@ struct HybT {
             const int32_t sm = __builtin_amdgcn_readlane(tr_s, m), lm = __builtin_amdgcn_readlane(lo, m),
                           hm = __builtin_amdgcn_readlane(hi, m);
             const uint32_t dm = __builtin_amdgcn_readlane(tr_v, m);
-            count_packed((int64_t)dm * 8, lm - sm, hm - sm, A, B, cA, cB);
+            count_packed((int64_t)dm * 8, lm - sm, hm - sm, A, B, cA, cB, dst ? dst + t_base + sm : nullptr);
           }
           vdone += take;
           left -= take;
@@ -582,9 +599,10 @@ struct HybT {
       if (rle) {
         cA += rle_val == A ? take : 0;
         cB += rle_val >= B ? take : 0;
+        if (dst) fill_run(dst, vdone, vdone + take, rle_val);
       } else {
         const int ok = readable((int)min<int64_t>(take, 1 << 30));
-        count_packed(data * 8, vi, vi + ok, A, B, cA, cB);
+        count_packed(data * 8, vi, vi + ok, A, B, cA, cB, dst ? dst + vdone - vi : nullptr);
         if (ok < take) {
           vdone += ok;
           return E_EOF;

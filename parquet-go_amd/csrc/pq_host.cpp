@@ -55,6 +55,7 @@ struct pq_launch_args {
   uint32_t *copy_cnt;
   int32_t *copy_idx;
   int32_t *lens;
+  uint8_t *lvl;
   void *runs;
   void *tile_info;
   const void *tiles;
@@ -625,6 +626,8 @@ struct pqg_batch {
   int32_t *d_copy_idx = nullptr;   // their job slots, compact
   int32_t *d_lens = nullptr;       // DELTA string pages: length scratch
   int64_t lens_entries = 0;
+  int64_t lvl_bytes = 0;     // decoded-level scratch (PageDesc::lvl_base)
+  uint8_t *d_lvl = nullptr;
   uint64_t *d_dbg = nullptr;     // diagnostic stamps (PQ_STAMPS builds only)
   uint64_t *d_dbg2 = nullptr;
   void *d_runs = nullptr;        // run tables (k_prepare's run walk -> k_expand)
@@ -1216,6 +1219,7 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
     memset(&d, 0, sizeof(d));
     d.job_base = -1;  // not a tiled page
     d.lens_base = -1;
+    d.lvl_base = -1;
     d.sidx = -1;
     d.col = ci;
     d.rg = rg;
@@ -1328,6 +1332,12 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
     } else {
       B->data_list.push_back(my_index);
       level_base += d.num_values;
+      // pages with levels: k_levels leaves them decoded (a byte each) with the
+      // counts k_prepare needs, for k_prepare and k_decode
+      if (L.max_def > 0 && L.max_def < 256 && d.num_values > 0) {
+        B->pages.back().lvl_base = B->lvl_bytes;
+        B->lvl_bytes += (((int64_t)(L.max_rep > 0 ? 2 : 1) * d.num_values) + 15) & ~(int64_t)15;
+      }
       if (L.physical_type == T_BYTE_ARRAY && (d.enc == ENC_DELTA_LBA || d.enc == ENC_DELTA_BA)) {
         B->pages.back().lens_base = B->lens_entries;  // suffix lengths, then prefix lengths
         B->lens_entries += 2 * (int64_t)std::max(d.num_values, 0);
@@ -1716,6 +1726,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   rc |= alloc_dev((void **)&B->d_copy_cnt, 16);
   rc |= alloc_dev((void **)&B->d_copy_idx, 4 * (job_owner.size() + 1));
   rc |= alloc_dev((void **)&B->d_lens, 4 * (size_t)(B->lens_entries + 1));
+  rc |= alloc_dev((void **)&B->d_lvl, (size_t)B->lvl_bytes + 16);
   rc |= alloc_dev((void **)&B->d_sitems, 4 * (B->snap_items.size() + 2));
   rc |= alloc_dev((void **)&B->d_seg_base, 4 * B->seg_base.size());
   rc |= alloc_dev((void **)&B->d_walk, 4 * (B->walk_list.size() + 1));
@@ -1954,6 +1965,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.copy_cnt = B->d_copy_cnt;
   a.copy_idx = B->d_copy_idx;
   a.lens = B->d_lens;
+  a.lvl = B->d_lvl;
   a.status0 = B->d_status0;
   a.zr = B->d_zr;
   a.nzr = upto_scan ? 0 : B->nzr;  // the bitmaps are written by the decode kernels only
@@ -2053,8 +2065,12 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   if (fused) {
     a.list = B->d_lists + ns + nd;
     a.nlist = ndata;
+    if (B->lvl_bytes) e |= pq_launch(20, &a, s);  // k_levels: pages that do not wait on k_copy
     e |= pq_launch(12, &a, s);  // k_prepare_copy (+ the run walk of tiled RLE_DICTIONARY pages)
-    if (B->data_may_defer) e |= pq_launch(11, &a, s);  // pages that waited on k_copy
+    if (B->data_may_defer) {    // pages that waited on k_copy
+      if (B->lvl_bytes) e |= pq_launch(21, &a, s);
+      e |= pq_launch(11, &a, s);
+    }
   } else {
     e |= pq_launch(6, &a, s);  // k_copy: long literals, timed together with k_snappy
     mark(false);
@@ -2066,6 +2082,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     mark(false);
     a.list = B->d_lists + ns + nd;
     a.nlist = ndata;
+    if (B->lvl_bytes) e |= pq_launch(19, &a, s);  // k_levels
     e |= pq_launch(2, &a, s);  // (+ the run walk of tiled RLE_DICTIONARY pages)
   }
   mark(false);
@@ -2334,6 +2351,7 @@ void pqg_batch_destroy(pqg_batch *B) {
   hipFree(B->d_zr);
   hipFree(B->d_copy_idx);
   hipFree(B->d_lens);
+  hipFree(B->d_lvl);
   hipFree(B->d_dbg);
   hipFree(B->d_dbg2);
   hipFree(B->d_runs);

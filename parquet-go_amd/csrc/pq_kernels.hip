@@ -75,6 +75,7 @@ struct KArgs {
   uint32_t *copy_cnt;     // deferred literals registered this decode: [epoch & 1] (the other is reset)
   int32_t *copy_idx;      // their job slots, compact (k_snappy -> k_copy)
   int32_t *lens;          // DELTA string pages: suffix lengths [0, nv), prefix lengths [nv, 2 nv)
+  uint8_t *lvl;           // decoded levels of count-path pages (PageDesc::lvl_base), k_prepare -> k_decode
   const uint32_t *status0;  // k_reset: every page's initial status (host planning errors)
   const ZeroRange *zr;      // k_reset: buffers zeroed per decode (validity bitmaps)
   int32_t nzr, npages;
@@ -1937,9 +1938,6 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
 // ===========================================================================
 // Page gi of the list.  mode -1: every page; 0: pages whose body does not
 // wait on k_copy (run beside it, k_prepare_copy); 1: only the pages that do.
-// TABLE: level counts through run tables (k_prepare); k_prepare_copy, whose
-// registers also hold the copy loop, counts with the serial walk
-template <bool TABLE>
 __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lbytes, uint16_t *lnx, int mode) {
   if (gi >= a.nlist) return;
   const int lane = lane_id();
@@ -2070,35 +2068,41 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
 
   // counts for lists / strings: decode the level streams (phase 2 stages)
   const int n = d.num_values;
-  using Lv = HybT<TABLE>;
+  using Lv = HybS;
   // diagnostic build: count-path stamps (1 levels start, 2 rep done, 6 def
   // done, 7 strings done; 3 values, 4 = 100 + encoding)
   PSTAMP(page, 1, __builtin_amdgcn_s_memrealtime());
   PSTAMP(page, 3, (uint64_t)n);
   PSTAMP(page, 4, (uint64_t)(100 + d.enc));
-  Lv rep, def;
-  rep.init(ps.lvl + ps.rep_off, ps.rep_len, bits_len(c.max_rep));
-  def.init(ps.lvl + ps.def_off, ps.def_len, bits_len(c.max_def));
   int64_t rows = 0, slots = 0, nn = 0;
-  // whole runs counted from the run table (Hyb::count2): rows = rep levels
-  // 0; non-null = def levels max_def; slots = def levels >= rep_def
-  if (c.max_rep > 0) {
-    int64_t unused = 0;
-    e = rep.count2(n, 0u, 0xffffffffu, rows, unused);
-    if (e) {
-      set_status(a.status, page, ST_REP, e);
-      return;
-    }
-  }
-  PSTAMP(page, 2, __builtin_amdgcn_s_memrealtime());
-  if (c.max_def > 0) {
-    e = def.count2(n, (uint32_t)c.max_def, c.max_rep > 0 ? (uint32_t)c.rep_def : 0u, nn, slots);
-    if (e) {
-      set_status(a.status, page, ST_DEF, e);
-      return;
-    }
+  if (d.lvl_base >= 0) {
+    // k_levels decoded the level streams (and checked them) in the previous
+    // launch: its counts, read at device scope
+    rows = __hip_atomic_load(&pi->rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    slots = __hip_atomic_load(&pi->slots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    nn = __hip_atomic_load(&pi->non_null, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
-    nn = slots = n;  // no def levels: every value is defined
+    // rows = rep levels 0; non-null = def levels max_def; slots = def levels >= rep_def
+    HybS rep, def;
+    rep.init(ps.lvl + ps.rep_off, ps.rep_len, bits_len(c.max_rep));
+    def.init(ps.lvl + ps.def_off, ps.def_len, bits_len(c.max_def));
+    if (c.max_rep > 0) {
+      int64_t unused = 0;
+      e = rep.count2(n, 0u, 0xffffffffu, rows, unused);
+      if (e) {
+        set_status(a.status, page, ST_REP, e);
+        return;
+      }
+    }
+    if (c.max_def > 0) {
+      e = def.count2(n, (uint32_t)c.max_def, c.max_rep > 0 ? (uint32_t)c.rep_def : 0u, nn, slots);
+      if (e) {
+        set_status(a.status, page, ST_DEF, e);
+        return;
+      }
+    } else {
+      nn = slots = n;  // no def levels: every value is defined
+    }
   }
   if (c.max_rep == 0) rows = n;
   PSTAMP(page, 6, __builtin_amdgcn_s_memrealtime());
@@ -2216,11 +2220,68 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
 }
 
 template <int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_prepare(KArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_prepare(KArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t wl_bytes[4][1024];  // run walk: window bytes
   __shared__ __attribute__((aligned(16))) uint16_t wl_nx[4][2048];    // run walk: chain table (BYTE_ARRAY walk: two)
   const int wv = (int)ufirst(threadIdx.x >> 6);
-  prepare_page<true>(a, (int)blockIdx.x * 4 + wv, wl_bytes[wv], wl_nx[wv], MODE);
+  prepare_page(a, (int)blockIdx.x * 4 + wv, wl_bytes[wv], wl_nx[wv], MODE);
+}
+
+// k_levels: the level streams of every page with a level scratch
+// (PageDesc::lvl_base), one wave a page: run tables (HybT<true>) decoded into
+// a byte a level, with the counts k_prepare needs (rows: rep levels 0,
+// non-null: def levels max_def, slots: def levels >= rep_def).  Errors in the
+// streams are the page's (ST_REP / ST_DEF, the reference's readLevels order);
+// k_prepare and k_decode then read the counts and levels instead of the
+// streams.  MODE as k_prepare (-1 every page, 0 / 1 pages that do not / do
+// wait on k_copy).
+template <int MODE>
+__global__ __launch_bounds__(256) void k_levels(KArgs a) {
+  const int gi = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
+  if (gi >= a.nlist) return;
+  const int lane = lane_id();
+  const int page = ufirst(a.list[gi]);
+  const PageDesc d = a.pages[page];
+  if (d.lvl_base < 0) return;
+  if (MODE >= 0) {
+    const bool waits = d.sidx >= 0 && a.njobs[d.sidx] > 0;
+    if (waits != (MODE == 1)) return;
+  }
+  if (page_status(a.status, page) != STATUS_OK) return;
+  if (d.dict >= 0 && page_status(a.status, d.dict) != STATUS_OK) return;
+  const ColDesc c = a.cols[d.col];
+  PageStreams ps;
+  uint32_t stage = ST_REP_INIT;
+  uint32_t e = layout(a, d, page, c, ps, stage);
+  if (e) {
+    set_status(a.status, page, stage, e);
+    return;
+  }
+  const int n = d.num_values;
+  Hyb rep, def;
+  rep.init(ps.lvl + ps.rep_off, ps.rep_len, bits_len(c.max_rep));
+  def.init(ps.lvl + ps.def_off, ps.def_len, bits_len(c.max_def));
+  uint8_t *lv = a.lvl + d.lvl_base;
+  int64_t rows = 0, slots = 0, nn = 0, unused = 0;
+  if (c.max_rep > 0) {
+    e = rep.count2(n, 0u, 0xffffffffu, rows, unused, lv);
+    if (e) {
+      set_status(a.status, page, ST_REP, e);
+      return;
+    }
+    lv += n;
+  }
+  e = def.count2(n, (uint32_t)c.max_def, c.max_rep > 0 ? (uint32_t)c.rep_def : 0u, nn, slots, lv);
+  if (e) {
+    set_status(a.status, page, ST_DEF, e);
+    return;
+  }
+  if (c.max_rep == 0) rows = n;
+  if (lane == 0) {
+    a.info[page].rows = rows;
+    a.info[page].slots = slots;
+    a.info[page].non_null = nn;
+  }
 }
 
 // k_prepare beside k_copy in one launch (batches without BYTE_ARRAY
@@ -2234,7 +2295,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
   const uint32_t pb = ((uint32_t)a.nlist + 3) / 4;
   if (blockIdx.x < pb) {
     const int wv = (int)ufirst(threadIdx.x >> 6);
-    prepare_page<false>(a, (int)blockIdx.x * 4 + wv, wl_bytes[wv], wl_nx[wv], 0);
+    prepare_page(a, (int)blockIdx.x * 4 + wv, wl_bytes[wv], wl_nx[wv], 0);
     return;
   }
   copy_items(a, blockIdx.x - pb, gridDim.x - pb);
@@ -2475,18 +2536,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   while (e0 < n) {
     const int cnt = (int)min<int64_t>(n - e0, flat ? 256 - ((slot_base + e0) & 255) : 256);
     uint32_t r[4] = {0, 0, 0, 0}, dl[4] = {0, 0, 0, 0};
-    if (!flat) {
-      err = rep.next4(cnt, r);
-      if (err) {
-        err_stage = ST_REP;
-        break;
+    if (d.lvl_base >= 0) {  // decoded (and checked) by k_prepare's level walk
+      const uint8_t *lr = a.lvl + d.lvl_base + e0, *ld = lr + (c.max_rep > 0 ? (int64_t)n : 0);
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int j = 4 * lane + k;
+        if (j < cnt) {
+          if (!flat) r[k] = lr[j];
+          dl[k] = ld[j];
+        }
       }
-    }
-    if (c.max_def > 0) {
-      err = def.next4(cnt, dl);
-      if (err) {
-        err_stage = ST_DEF;
-        break;
+    } else {
+      if (!flat) {
+        err = rep.next4(cnt, r);
+        if (err) {
+          err_stage = ST_REP;
+          break;
+        }
+      }
+      if (c.max_def > 0) {
+        err = def.next4(cnt, dl);
+        if (err) {
+          err_stage = ST_DEF;
+          break;
+        }
       }
     }
     bool act[4], valid[4], slot[4];
@@ -3658,6 +3731,7 @@ struct pq_launch_args {
   uint32_t *copy_cnt;
   int32_t *copy_idx;
   int32_t *lens;
+  uint8_t *lvl;
   void *runs;
   void *tile_info;
   const void *tiles;
@@ -3708,6 +3782,7 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   k.copy_cnt = p->copy_cnt;
   k.copy_idx = p->copy_idx;
   k.lens = p->lens;
+  k.lvl = p->lvl;
   k.status0 = p->status0;
   k.zr = (const pq::ZeroRange *)p->zr;
   k.nzr = p->nzr;
@@ -3785,6 +3860,9 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     case 1: hipLaunchKernelGGL(pq::k_dict_prepare, grid, block, 0, s, k); break;
     case 2: hipLaunchKernelGGL(pq::k_prepare<-1>, grid, block, 0, s, k); break;
     case 11: hipLaunchKernelGGL(pq::k_prepare<1>, grid, block, 0, s, k); break;
+    case 19: hipLaunchKernelGGL(pq::k_levels<-1>, grid, block, 0, s, k); break;
+    case 20: hipLaunchKernelGGL(pq::k_levels<0>, grid, block, 0, s, k); break;
+    case 21: hipLaunchKernelGGL(pq::k_levels<1>, grid, block, 0, s, k); break;
     case 3: hipLaunchKernelGGL(pq::k_decode<0>, grid, block, 0, s, k); break;
     case 14: hipLaunchKernelGGL(pq::k_decode<1>, grid, block, 0, s, k); break;
     case 15: hipLaunchKernelGGL(pq::k_decode<2>, grid, block, 0, s, k); break;
