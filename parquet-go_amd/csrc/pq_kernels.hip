@@ -1411,10 +1411,16 @@ __device__ __forceinline__ uint32_t ba_walk(const uint8_t *vp, int64_t vlen, int
     const int64_t avail = vlen - P;
     const uintptr_t ab = (uintptr_t)(vp + P) & ~(uintptr_t)3;
     const int sh = (int)((uintptr_t)(vp + P) & 3);
-    const uint32_t *ga = (const uint32_t *)ab;
+    // global (not generic) loads, all issued before the LDS stores: generic
+    // loads may alias LDS, and were each waited for before their store
+    const __attribute__((address_space(1))) uint32_t *ga = (const __attribute__((address_space(1))) uint32_t *)ab;
+    constexpr int NQ = (WINB / 4 + 8 + 63) / 64;
+    uint32_t gq[NQ];
 #pragma unroll
-    for (int q = 0; q * 64 < WINB / 4 + 8; q++)
-      if (lane + 64 * q < WINB / 4 + 8) win[lane + 64 * q] = ga[lane + 64 * q];
+    for (int q = 0; q < NQ; q++) gq[q] = lane + 64 * q < WINB / 4 + 8 ? ga[lane + 64 * q] : 0u;
+#pragma unroll
+    for (int q = 0; q < NQ; q++)
+      if (lane + 64 * q < WINB / 4 + 8) win[lane + 64 * q] = gq[q];
     wave_lds_sync();
     uint16_t *ja = ja0, *jb = jb0;
 #pragma unroll
@@ -1492,12 +1498,12 @@ __global__ __launch_bounds__(256) void k_dict_prepare(KArgs a) {
     return;
   }
   // length-prefix walk (type_bytearray.go:24-45): entry table (offset << 32 | length)
-  __shared__ BaLdsT<BA_WIN_DICT> ba_all[4];
+  __shared__ __attribute__((aligned(16))) BaLdsT<BA_WIN_DICT> ba_all[4];
   BaLdsT<BA_WIN_DICT> &bl = ba_all[threadIdx.x >> 6];
-  const uint32_t e = ba_walk<BA_WIN_DICT>(body, len, n, bl.win, bl.jt[0], bl.jt[1],
-                             [&](int64_t first, int ln, int64_t voff, int32_t l, int cnt) {
-                               if (ln < cnt) a.dict_ent[d.dict_base + first + ln] = ((uint64_t)voff << 32) | (uint32_t)l;
-                             });
+  auto put = [&](int64_t first, int ln, int64_t voff, int32_t l, int cnt) {
+    if (ln < cnt) a.dict_ent[d.dict_base + first + ln] = ((uint64_t)voff << 32) | (uint32_t)l;
+  };
+  const uint32_t e = ba_walk<BA_WIN_DICT>(body, len, n, bl.win, bl.jt[0], bl.jt[1], put);
   if (e) set_status(a.status, page, ST_DICT_VALUES, e);
 }
 
@@ -2115,15 +2121,15 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
       int64_t acc = 0;
       int32_t *SO = d.lens_base >= 0 ? a.lens + d.lens_base : nullptr;
       const int32_t nvp = max(d.num_values, 0);
-      const uint32_t e2 = ba_walk<960>(ps.body + ps.val_off, ps.val_len, nn, (uint32_t *)lbytes, lnx, lnx + 968,
-                                       [&](int64_t first, int ln, int64_t voff, int32_t l, int cnt) {
-                                         const int64_t t = wave_incl_scan64(ln < cnt ? (int64_t)l : 0);
-                                         acc += (int64_t)ufirst64((int64_t)shfl64((uint64_t)t, 63));
-                                         if (SO && ln < cnt && first + ln < nvp) {
-                                           SO[first + ln] = (int32_t)voff;
-                                           SO[nvp + first + ln] = l;
-                                         }
-                                       });
+      auto put = [&](int64_t first, int ln, int64_t voff, int32_t l, int cnt) {
+        const int64_t t = wave_incl_scan64(ln < cnt ? (int64_t)l : 0);
+        acc += (int64_t)ufirst64((int64_t)shfl64((uint64_t)t, 63));
+        if (SO && ln < cnt && first + ln < nvp) {
+          SO[first + ln] = (int32_t)voff;
+          SO[nvp + first + ln] = l;
+        }
+      };
+      const uint32_t e2 = ba_walk<960>(ps.body + ps.val_off, ps.val_len, nn, (uint32_t *)lbytes, lnx, lnx + 968, put);
       if (e2) {
         set_status(a.status, page, ST_VALUES, e2);
         return;
