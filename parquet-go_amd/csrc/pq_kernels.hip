@@ -346,7 +346,7 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
                                              uint32_t &err, const uint8_t *pend_src, int64_t pend_dpos,
                                              int64_t &pend_len, int ndefer, int64_t def_dst, int64_t def_len,
                                              uint64_t def_src, int lane, const uint8_t *in_end, int64_t &pf_s,
-                                             uint32_t &pg0, uint32_t &pg1, uint32_t &pg2) {
+                                             int64_t &pf_F, uint32_t &pg0, uint32_t &pg1, uint32_t &pg2) {
   SNAP_T(-1);
   // 1. stage the window (aligned base; `sh` = position of byte s); the
   // previous batch prefetched it into pg0..pg2 when it ended at s
@@ -355,10 +355,15 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
   const uint32_t *ga = (const uint32_t *)abase;
   PQ_CHK(in_end && abase + 528 > (uintptr_t)in_end, 10, abase, in_end, err = E_SNAPPY; return false);
   uint32_t g0, g1, g2;
+  // staged output known written: loads and stores retire in order (one
+  // vmcnt), so waiting for the window's loads retired every store issued
+  // before them — the flushes up to pf_F for the prefetch, F for a fresh load
+  int64_t F_safe = F;
   if (pf_s == s) {
     g0 = pg0;
     g1 = pg1;
     g2 = pg2;
+    F_safe = pf_F;
   } else {
     g0 = ga[lane];
     g1 = ga[lane + 64];
@@ -484,7 +489,9 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
     bool pre = false;
     if (ballot(act && !lit && S < near_lo)) {
       // this wave's earlier staging stores must be visible to the loads below
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      // (unless every source lies in output known written)
+      if (ballot(act && !lit && S < near_lo && S + (int64_t)len > F_safe))
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
       pre = act && !lit && x >= len && S + (int64_t)len <= near_lo;
       uintptr_t fsrc = pre ? (uintptr_t)(dst + S) : 0;
       bool in_payload = false;
@@ -532,6 +539,7 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
         pg1 = gn[lane + 64];
         pg2 = lane < 4 ? gn[lane + 128] : 0u;
         pf_s = sn;
+        pf_F = F;
       }
     }
     SNAP_T(3);
@@ -778,6 +786,7 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
   int64_t def_dst = 0, def_len = 0;
   uint64_t def_src = 0;
   int64_t pf_s = -1;  // stream position of the window prefetched into pg0..pg2
+  int64_t pf_F = 0;   // staged output flushed when that prefetch was issued
   uint32_t pg0 = 0, pg1 = 0, pg2 = 0;
   while (s < slen && (!seg || dpos < dl)) {
     const uint32_t tag = pf_s == s ? (__builtin_amdgcn_readlane(pg0, 0) >> (8 * ((uintptr_t)(src + s) & 3))) & 0xffu
@@ -786,7 +795,7 @@ __global__ __launch_bounds__(256) void k_snappy(KArgs a) {
       // ---- short tokens (copies, literals <= 60 bytes): one batch of up to
       // SB_TOK tokens / SB_OUT output bytes per pass (snappy_batch)
       if (!snappy_batch(L, ring, src, slen, dst, dl, seg_lo, write, s, dpos, F, err, pend_src, pend_dpos, pend_len, ndefer,
-                        def_dst, def_len, def_src, lane, a.in_end, pf_s, pg0, pg1, pg2))
+                        def_dst, def_len, def_src, lane, a.in_end, pf_s, pf_F, pg0, pg1, pg2))
         break;
       continue;
     }
