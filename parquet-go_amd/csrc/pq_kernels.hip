@@ -670,7 +670,7 @@ constexpr int64_t SNAP_SEG = 65536;
 enum { SNAP_ITEMS = 0, SNAP_FALLBACK = 1 };
 
 template <int MODE>
-__global__ __launch_bounds__(256) void k_snappy(KArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_snappy(KArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t ring_all[SNAPPY_WAVES][RING];
   __shared__ SnapLds sl_all[SNAPPY_WAVES];
   const int lane = lane_id();
