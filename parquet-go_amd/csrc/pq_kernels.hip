@@ -399,13 +399,17 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
   int pos = sh;
 #pragma unroll
   for (int b = 0; b < 6; b++) {
-    if ((lane >> b) & 1) pos = ja[pos];
+    // every read of a round issued before its writes (the tables are both
+    // LDS: the compiler cannot reorder a read past a write that may alias
+    // it, and each read-modify-write pair cost an LDS round trip)
+    const int hop = ja[pos];
     if (b < 5) {
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const int i = 4 * lane + j;
-        jb[i] = ja[ja[i]];
-      }
+      const uint2 q = *(const uint2 *)(ja + 4 * lane);  // J_b(4 lane .. 4 lane + 3)
+      const uint32_t n0 = ja[q.x & 0xffff], n1 = ja[q.x >> 16], n2 = ja[q.y & 0xffff], n3 = ja[q.y >> 16];
+      *(uint2 *)(jb + 4 * lane) = make_uint2(n0 | (n1 << 16), n2 | (n3 << 16));
+    }
+    if ((lane >> b) & 1) pos = hop;
+    if (b < 5) {
       wave_lds_sync();
       uint16_t *t = ja;
       ja = jb;
@@ -1432,15 +1436,29 @@ __device__ __forceinline__ uint32_t ba_walk(const uint8_t *vp, int64_t vlen, int
       if (lane + 64 * q < WINB / 4 + 8) win[lane + 64 * q] = gq[q];
     wave_lds_sync();
     uint16_t *ja = ja0, *jb = jb0;
+    // reads of a group of positions issued before its writes (window and
+    // tables are all LDS: a read cannot pass a write that may alias it, and
+    // each read / write pair cost an LDS round trip)
+    constexpr int NP = WINB / 64;
+    constexpr int G = NP % 8 == 0 ? 8 : NP % 5 == 0 ? 5 : NP % 4 == 0 ? 4 : NP % 3 == 0 ? 3 : 1;
 #pragma unroll
-    for (int q = 0; q < WINB / 64; q++) {
-      const int i = lane + 64 * q;
-      const int b = sh + i;
-      const uint64_t w2 = (uint64_t)win[b >> 2] | ((uint64_t)win[(b >> 2) + 1] << 32);
-      const int32_t l = (int32_t)(uint32_t)(w2 >> ((b & 3) * 8));
-      const bool ok = (int64_t)i + 4 <= avail && l >= 0 && (int64_t)i + 4 + l <= avail;
-      const int64_t nx = (int64_t)i + 4 + (int64_t)l;
-      ja[i] = (uint16_t)((ok && nx < WINB) ? nx : WINB);
+    for (int g0 = 0; g0 < NP; g0 += G) {
+      uint32_t wl[G], wh[G];
+#pragma unroll
+      for (int q = 0; q < G; q++) {
+        const int b = sh + lane + 64 * (g0 + q);
+        wl[q] = win[b >> 2];
+        wh[q] = win[(b >> 2) + 1];
+      }
+#pragma unroll
+      for (int q = 0; q < G; q++) {
+        const int i = lane + 64 * (g0 + q);
+        const int b = sh + i;
+        const int32_t l = (int32_t)__builtin_amdgcn_alignbyte(wh[q], wl[q], b & 3);
+        const bool ok = (int64_t)i + 4 <= avail && l >= 0 && (int64_t)i + 4 + l <= avail;
+        const int64_t nx = (int64_t)i + 4 + (int64_t)l;
+        ja[i] = (uint16_t)((ok && nx < WINB) ? nx : WINB);
+      }
     }
     if (lane == 0) {
       ja[WINB] = WINB;
@@ -1450,13 +1468,21 @@ __device__ __forceinline__ uint32_t ba_walk(const uint8_t *vp, int64_t vlen, int
     int pos = 0;
 #pragma unroll
     for (int bt = 0; bt < 6; bt++) {
-      if ((lane >> bt) & 1) pos = ja[pos];
+      const int hop = ja[pos];
       if (bt < 5) {
 #pragma unroll
-        for (int q = 0; q < WINB / 64; q++) {
-          const int i = lane + 64 * q;
-          jb[i] = ja[ja[i]];
+        for (int g0 = 0; g0 < NP; g0 += G) {
+          uint32_t t1[G], t2[G];
+#pragma unroll
+          for (int q = 0; q < G; q++) t1[q] = ja[lane + 64 * (g0 + q)];
+#pragma unroll
+          for (int q = 0; q < G; q++) t2[q] = ja[t1[q]];
+#pragma unroll
+          for (int q = 0; q < G; q++) jb[lane + 64 * (g0 + q)] = (uint16_t)t2[q];
         }
+      }
+      if ((lane >> bt) & 1) pos = hop;
+      if (bt < 5) {
         wave_lds_sync();
         uint16_t *t = ja;
         ja = jb;
