@@ -259,6 +259,49 @@ def segment_times(reader, rg0, rg1, decodes=6):
         b.close()
 
 
+def e2e_rates(reader, rg0, rg1, stats, slices=12):
+    """PCIe-inclusive rates (never `value`): the whole shard read through
+    pqg_stream — the host worker plans and uploads slice k + 1 (pinned ring,
+    PQG_UPLOAD_THREADS gather threads) while the GPU decodes slice k — timed
+    from opening the stream to the last slice's sync; beside it the bare PCIe
+    rate, one hipMemcpy of the shard's input bytes from pinned host memory."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    n = int(stats["h2d_bytes"] or stats["input_bytes"])
+    hbuf, dbuf = ctypes.c_void_p(), ctypes.c_void_p()
+    pcie = None
+    if hip.hipHostMalloc(ctypes.byref(hbuf), ctypes.c_size_t(n), 0) == 0:
+        if hip.hipMalloc(ctypes.byref(dbuf), ctypes.c_size_t(n)) == 0:
+            ctypes.memset(hbuf, 1, n)
+            best = None
+            for _ in range(3):
+                t = time.perf_counter()
+                hip.hipMemcpy(dbuf, hbuf, ctypes.c_size_t(n), 1)  # hipMemcpyHostToDevice
+                t = time.perf_counter() - t
+                best = t if best is None else min(best, t)
+            pcie = best
+            hip.hipFree(dbuf)
+        hip.hipHostFree(hbuf)
+    per = max(1, (rg1 - rg0 + slices - 1) // slices)
+    best = None
+    for _ in range(2):  # the first pass also maps the file pages
+        t = time.perf_counter()
+        with reader.stream(rg0, rg1, per) as st:
+            for b in st:
+                b.sync()
+        t = time.perf_counter() - t
+        best = t if best is None else min(best, t)
+    out = {"stream_ms": round(best * 1e3, 2), "stream_rgs_per_slice": per,
+           "GBps_stream_incl_plan_and_h2d": round(stats["output_bytes"] / best / 1e9, 1),
+           "h2d_bytes": n}
+    if pcie:
+        out["pcie_only_ms"] = round(pcie * 1e3, 2)
+        out["pcie_only_GBps_in"] = round(n / pcie / 1e9, 1)
+        # the decoded-bytes rate a pure upload of the shard's input would allow
+        out["GBps_pcie_only_decoded_equiv"] = round(stats["output_bytes"] / pcie / 1e9, 1)
+        out["stream_vs_pcie_only"] = round(pcie / best, 3)
+    return out
+
+
 def parity_check(reader, rg):
     """Row group `rg` of the bench file decoded again on the GPU (outside the
     timed region) and compared bit-exactly, buffer by buffer, with the oracle."""
@@ -448,6 +491,7 @@ def main():
                     line["roofline"]["traffic"] = round(sum(pmc[k]["fetch"] + pmc[k]["write"] for k in ks) / 1e6, 1)
                     line["roofline"]["traffic_unit"] = "MB per launch of the phase's kernels (FETCH_SIZE x 2 + WRITE_SIZE)"
         line["config"]["parity"] = parity_check(reader, rg0)
+        line["config"]["e2e"].update(e2e_rates(reader, rg0, rg1, stats))
     if "roofline" not in line:
         # N > 1: the decode phase, HIP events over the timed steps (per rank)
         dms = sum(decode_ms.values())

@@ -193,6 +193,24 @@ int pqg_batch_kernel_times(pqg_batch *b, const char **names, float *ms, int cap)
 int pqg_batch_set_timing(pqg_batch *b, int every);
 void pqg_batch_destroy(pqg_batch *b);
 
+/* ---- stream: row groups [rg_begin, rg_end) in slices of rgs_per_slice row
+ *      groups, pipelined.  Replaces the reader's row-group iteration
+ *      (file_reader.go:101-116 NextRow / SkipRowGroup / PreLoad ->
+ *      readRowGroup, chunk_reader.go:206-283): a host worker thread plans slice
+ *      k + 1 and queues its H2D upload (the context's upload stream, pinned ring
+ *      filled by PQG_UPLOAD_THREADS host threads) while the GPU decodes slice k.
+ *      `depth` slices are built ahead (>= 1). ---------------------------------- */
+typedef struct pqg_stream pqg_stream;
+int pqg_stream_open(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const int *leaves, int nleaves, int flags,
+                    int rgs_per_slice, int depth, pqg_stream **out);
+/* The next slice: its decode is launched (asynchronous; pqg_batch_sync waits
+ * and reports its first error) and *out is its batch, owned by the stream and
+ * valid until the next pqg_stream_next / pqg_stream_close.  *out = NULL and
+ * PQG_OK after the last slice; a slice whose planning failed returns that
+ * error (the stream ends there). *rg_first: the slice's first row group. */
+int pqg_stream_next(pqg_stream *s, pqg_batch **out, int *rg_first);
+void pqg_stream_close(pqg_stream *s);
+
 #ifdef __cplusplus
 }
 #endif

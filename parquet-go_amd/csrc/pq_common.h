@@ -92,6 +92,11 @@ struct ZeroRange {
 constexpr int LD_WAVES_H = 4;             // waves of a k_expand_mix workgroup
 constexpr int LD_LDS_MAX = 160 * 1024;    // LDS of one CU (gfx950)
 constexpr int LD_MIX_MAX = 32 * 1024;     // k_expand_mix LDS per workgroup with a dictionary (default)
+// k_expand_big: dictionaries past LD_MIX_MAX that still fit one CU's LDS beside
+// BIG_WAVES waves' staged keys; one workgroup of BIG_WAVES waves per group,
+// its own launch (the dynamic LDS size is per launch)
+constexpr int BIG_WAVES = 8;
+constexpr int BIG_JOBS = 16;              // jobs per group (default; PQG_BIG_JOBS)
 struct LdsGroup {
   int32_t job0, njobs;   // jobs [job0, job0 + njobs) of the launch order
   int32_t dpage;         // the chunk's dictionary page; -1: one job per wave, L1/L2 gathers

@@ -21,10 +21,13 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <shared_mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/pqgpu.h"
@@ -477,27 +480,101 @@ bool codec_builtin(int codec, bool *registered) {
 // ===========================================================================
 // objects
 // ===========================================================================
+// Host threads that fill the pinned upload ring: each ring buffer's gather
+// (memcpy from the file mapping) is split into parts run by the pool and the
+// calling thread together, so the copy into pinned memory keeps up with the
+// PCIe DMA (one thread copies at about half the DMA rate).
+struct GatherPool {
+  std::vector<std::thread> th;
+  std::mutex mu;
+  std::condition_variable go, done_cv;
+  std::function<void(int)> job;
+  int nparts = 0, next = 0, done = 0;
+  uint64_t gen = 0;
+  bool stop = false;
+  void start(int n) {
+    for (int i = 0; i < n; i++)
+      th.emplace_back([this] {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+          go.wait(lk, [&] { return stop || gen != seen; });
+          if (stop) return;
+          seen = gen;
+          while (next < nparts) {
+            const int p = next++;
+            lk.unlock();
+            job(p);
+            lk.lock();
+            if (++done == nparts) done_cv.notify_all();
+          }
+        }
+      });
+  }
+  // runs f(0 .. parts-1) on the pool and the calling thread; returns when all are done
+  void run(int parts, const std::function<void(int)> &f) {
+    std::unique_lock<std::mutex> lk(mu);
+    job = f;
+    nparts = parts;
+    next = done = 0;
+    gen++;
+    go.notify_all();
+    while (next < nparts) {
+      const int p = next++;
+      lk.unlock();
+      f(p);
+      lk.lock();
+      if (++done == nparts) done_cv.notify_all();
+    }
+    done_cv.wait(lk, [&] { return done == nparts; });
+    nparts = 0;
+  }
+  ~GatherPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      stop = true;
+    }
+    go.notify_all();
+    for (auto &t : th) t.join();
+  }
+};
+
 struct pqg_ctx {
   int device = 0;
   int cus = 256;  // compute units (k_snappy's segmentation threshold)
   hipStream_t stream = nullptr;
   hipStream_t side[3] = {nullptr, nullptr, nullptr};  // concurrent size-class decode launches
   hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr};
+  // batch set-up stream: the H2D copies of chunk bytes run here, and a batch's
+  // decodes wait on its `ready` event, so a pqg_stream worker can upload the
+  // next slice while the context stream decodes the current one
+  hipStream_t upload = nullptr;
+  // launch sequences (which share the fork/join events) from several host
+  // threads — a pqg_stream's worker runs counting passes beside the caller's decodes
+  std::mutex launch_mu;
   // pinned upload ring (allocated on first use): chunk bytes are copied into
   // one buffer while the DMA of the previous one runs
   static constexpr int kRingBufs = 4;
   static constexpr size_t kRingBytes = 16u << 20;
   void *pin[kRingBufs] = {};
   hipEvent_t pin_ev[kRingBufs] = {};
+  bool pin_busy[kRingBufs] = {};  // pin_ev recorded after a DMA that may still read the buffer
+  int pin_next = 0;
+  std::mutex upload_mu;  // one ring_upload at a time per context
+  GatherPool pool;       // PQG_UPLOAD_THREADS - 1 helper threads (started on first upload)
+  bool pool_started = false;
   std::string err;
 };
 
 // host -> device upload of the input layout straight from the file's pages
-// through the context's pinned ring (each buffer filled while the DMA of the
-// previous one runs); alignment gaps are zeroed
+// through the context's pinned ring (each buffer filled — by the gather pool —
+// while the DMA of the previous one runs); alignment gaps are zeroed.  The
+// DMAs are queued on `s` and the call returns without waiting for the last
+// ones (a later upload waits for a buffer's event before refilling it).
 template <class Layout>
 static int ring_upload(pqg_ctx *c, uint8_t *dst, const Layout &in, hipStream_t s) {
   const size_t n = in.n;
+  std::lock_guard<std::mutex> lk(c->upload_mu);
   if (!c->pin[0]) {
     for (int i = 0; i < pqg_ctx::kRingBufs; i++) {
       if (hipHostMalloc(&c->pin[i], pqg_ctx::kRingBytes, hipHostMallocDefault) != hipSuccess ||
@@ -509,36 +586,53 @@ static int ring_upload(pqg_ctx *c, uint8_t *dst, const Layout &in, hipStream_t s
       }
     }
   }
-  size_t off = 0, ri = 0;
-  int k = 0;
-  bool used[pqg_ctx::kRingBufs] = {};
+  if (!c->pool_started) {
+    const char *e = getenv("PQG_UPLOAD_THREADS");
+    const int nt = std::max(1, std::min(e ? atoi(e) : 4, 32));
+    c->pool.start(nt - 1);
+    c->pool_started = true;
+  }
+  const int nthreads = (int)c->pool.th.size() + 1;
+  size_t off = 0;
   while (off < n) {
+    const int k = c->pin_next;
     const size_t m = std::min(pqg_ctx::kRingBytes, n - off);
-    if (used[k] && hipEventSynchronize(c->pin_ev[k]) != hipSuccess) return 1;
-    // gather [off, off + m) of the layout into the pinned buffer
+    if (c->pin_busy[k] && hipEventSynchronize(c->pin_ev[k]) != hipSuccess) return 1;
+    c->pin_busy[k] = false;
+    // gather [off, off + m) of the layout into the pinned buffer, in parts of >= 1 MiB
     uint8_t *pb = (uint8_t *)c->pin[k];
-    size_t at = off;
-    while (at < off + m) {
-      while (ri < in.ranges.size() && in.ranges[ri].off + in.ranges[ri].len <= at) ri++;
-      const size_t next = ri < in.ranges.size() ? in.ranges[ri].off : n;
-      if (at < next) {  // alignment gap
-        const size_t z = std::min(next, off + m) - at;
-        memset(pb + (at - off), 0, z);
+    const int parts = (int)std::max<size_t>(1, std::min<size_t>((size_t)nthreads, m >> 20));
+    auto part = [&](int p) {
+      const size_t lo = off + m * (size_t)p / (size_t)parts, hi = off + m * (size_t)(p + 1) / (size_t)parts;
+      // first range ending after lo
+      size_t ri = (size_t)(std::upper_bound(in.ranges.begin(), in.ranges.end(), lo,
+                                            [](size_t v, const decltype(in.ranges[0]) &r) { return v < r.off + r.len; }) -
+                           in.ranges.begin());
+      size_t at = lo;
+      while (at < hi) {
+        while (ri < in.ranges.size() && in.ranges[ri].off + in.ranges[ri].len <= at) ri++;
+        const size_t next = ri < in.ranges.size() ? in.ranges[ri].off : n;
+        if (at < next) {  // alignment gap
+          const size_t z = std::min(next, hi) - at;
+          memset(pb + (at - off), 0, z);
+          at += z;
+          continue;
+        }
+        const auto &r = in.ranges[ri];
+        const size_t z = std::min(r.off + r.len, hi) - at;
+        memcpy(pb + (at - off), r.src + (at - r.off), z);
         at += z;
-        continue;
       }
-      const auto &r = in.ranges[ri];
-      const size_t z = std::min(r.off + r.len, off + m) - at;
-      memcpy(pb + (at - off), r.src + (at - r.off), z);
-      at += z;
-    }
+    };
+    if (parts > 1) c->pool.run(parts, part);
+    else part(0);
     if (hipMemcpyAsync(dst + off, c->pin[k], m, hipMemcpyHostToDevice, s) != hipSuccess) return 1;
     hipEventRecord(c->pin_ev[k], s);
-    used[k] = true;
+    c->pin_busy[k] = true;
     off += m;
-    k = (k + 1) % pqg_ctx::kRingBufs;
+    c->pin_next = (k + 1) % pqg_ctx::kRingBufs;
   }
-  return hipStreamSynchronize(s) == hipSuccess ? 0 : 1;
+  return 0;
 }
 
 struct pqg_file {
@@ -640,8 +734,8 @@ struct pqg_batch {
   TileJob *d_tiles = nullptr;
   std::vector<LdsGroup> lgroups;     // k_expand_ld groups, 4-byte columns first
   LdsGroup *d_lgroups = nullptr;
-  int32_t ldn[6] = {}, ldl[6] = {};  // groups and LDS bytes per (width 4, 8) x LDS class
-  uint32_t *h_status = nullptr;  // pinned mirror
+  int32_t ldn[6] = {}, ldl[6] = {};  // groups and LDS bytes: [0], [1] k_expand_mix (width 4, 8),
+                                     // [2], [3] k_expand_big (width 4, 8)
   std::vector<ColDesc> hcols;
   // timing: a ring of event sets, one per decode, harvested by pqg_batch_kernel_times
   static constexpr int kRing = 64;
@@ -655,6 +749,7 @@ struct pqg_batch {
   int kms_n = 0;
   int err_rg = -1, err_leaf = -1, err_page = -1;
   bool decoded = false;
+  hipEvent_t ready = nullptr;  // recorded on the context's upload stream after the chunk bytes' H2D
 };
 
 // timed segments: with PQG_SEGMENT_TIMES every phase, otherwise the decode phase only
@@ -716,6 +811,10 @@ int pqg_ctx_create(int device, pqg_ctx **out) {
     }
   }
   hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
+  if (hipStreamCreateWithFlags(&c->upload, hipStreamNonBlocking) != hipSuccess) {
+    set_err("hipStreamCreate failed");
+    return PQG_ERR_DEVICE;
+  }
   *out = c;
   return PQG_OK;
 }
@@ -729,6 +828,10 @@ void pqg_ctx_destroy(pqg_ctx *ctx) {
     if (ctx->join[i]) hipEventDestroy(ctx->join[i]);
   }
   if (ctx->fork) hipEventDestroy(ctx->fork);
+  if (ctx->upload) {
+    hipStreamSynchronize(ctx->upload);
+    hipStreamDestroy(ctx->upload);
+  }
   for (int i = 0; i < pqg_ctx::kRingBufs; i++) {
     if (ctx->pin[i]) hipHostFree(ctx->pin[i]);
     if (ctx->pin_ev[i]) hipEventDestroy(ctx->pin_ev[i]);
@@ -1359,13 +1462,91 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
   return 0;
 }
 
+// Device memory cache.  Batches come and go (a pqg_stream makes one per
+// slice) and hipMalloc / hipFree cost tens of µs each — hipFree also waits for
+// the whole device — so released buffers are kept per device in size classes
+// (2^k, 1.25, 1.5, 1.75 x 2^k) and handed out again.  A buffer is released
+// only after its batch's work has finished (pqg_batch_destroy synchronises).
+// Held bytes are capped (PQG_DEV_CACHE_MB, default 32 GiB); a failed
+// hipMalloc releases the device's cache and retries.
+namespace {
+struct DevCache {
+  std::mutex mu;
+  std::multimap<std::pair<int, size_t>, void *> idle;  // (device, class bytes) -> buffer
+  std::map<void *, std::pair<int, size_t>> live;
+  size_t idle_bytes = 0;
+};
+DevCache &dev_cache() {
+  static DevCache *c = new DevCache();  // never destroyed: buffers outlive static destructors
+  return *c;
+}
+size_t size_class(size_t n) {
+  if (n <= 4096) return 4096;
+  size_t p = 4096;
+  while (p * 2 < n) p *= 2;  // p < n <= 2p
+  for (int q = 5; q <= 8; q++)
+    if (n <= p * (size_t)q / 4) return p * (size_t)q / 4;
+  return 2 * p;
+}
+void release_idle(DevCache &c, int dev) {  // caller holds c.mu
+  for (auto it = c.idle.begin(); it != c.idle.end();) {
+    if (dev >= 0 && it->first.first != dev) {
+      ++it;
+      continue;
+    }
+    hipFree(it->second);
+    c.idle_bytes -= it->first.second;
+    it = c.idle.erase(it);
+  }
+}
+}  // namespace
+
 static int alloc_dev(void **p, size_t n) {
-  hipError_t e = hipMalloc(p, n + kPad);
+  int dev = 0;
+  hipGetDevice(&dev);
+  const size_t cls = size_class(n + kPad);
+  DevCache &c = dev_cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  auto it = c.idle.find({dev, cls});
+  if (it != c.idle.end()) {
+    *p = it->second;
+    c.idle.erase(it);
+    c.idle_bytes -= cls;
+    c.live[*p] = {dev, cls};
+    return 0;
+  }
+  hipError_t e = hipMalloc(p, cls);
+  if (e != hipSuccess && !c.idle.empty()) {
+    release_idle(c, dev);
+    e = hipMalloc(p, cls);
+  }
   if (e != hipSuccess) {
+    *p = nullptr;
     set_err("hipMalloc(%zu) failed: %s", n, hipGetErrorString(e));
     return PQG_ERR_DEVICE;
   }
+  c.live[*p] = {dev, cls};
   return 0;
+}
+
+static void free_dev(void *p) {
+  if (!p) return;
+  DevCache &c = dev_cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  auto it = c.live.find(p);
+  if (it == c.live.end()) {
+    hipFree(p);
+    return;
+  }
+  static const size_t cap = (getenv("PQG_DEV_CACHE_MB") ? (size_t)atoll(getenv("PQG_DEV_CACHE_MB")) : 32768) << 20;
+  const auto key = it->second;
+  c.live.erase(it);
+  if (c.idle_bytes + key.second > cap) {
+    hipFree(p);
+    return;
+  }
+  c.idle.insert({key, p});
+  c.idle_bytes += key.second;
 }
 
 static int launch_all(pqg_batch *B, bool upto_scan, bool timed);
@@ -1492,8 +1673,11 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   // the machine for the whole launch.
   B->ex_lds = (B->ex_lds + 255) & ~255;  // LDS-DMA pieces of 16 bytes per lane, the last one partial
   const bool ld_off = getenv("PQG_NO_LDS_DICT") != nullptr;
-  std::vector<TileJob> slot_tiles, ld_tiles;
+  std::vector<TileJob> slot_tiles, ld_tiles, big_tiles;
+  std::vector<LdsGroup> big_groups[2];
   const int64_t ld_max = getenv("PQG_LD_MAX_KB") ? 1024 * (int64_t)atoi(getenv("PQG_LD_MAX_KB")) : LD_MIX_MAX;
+  const bool big_off = getenv("PQG_NO_BIG") != nullptr || getenv("PQG_BIG") == nullptr;  // analysis: opt-in until measured
+  const int64_t big_jobs = getenv("PQG_BIG_JOBS") ? std::max(1, atoi(getenv("PQG_BIG_JOBS"))) : BIG_JOBS;
   for (int ws = 0; ws < 2; ws++) {
     const int32_t W = ws == 0 ? 4 : 8;
     struct LdG {
@@ -1522,6 +1706,24 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
           for (int64_t q = 0; q < ng; q++) ldg.push_back({&ct, q * J / ng, (q + 1) * J / ng, (int32_t)dbytes, ks});
           ld = true;
           B->pages[(size_t)ct[0].dict].alias_any = 1;  // copied into LDS with a funnel shift anyway
+        } else if (!big_off && dbytes > 0 && ks > 0 && dbytes + (int64_t)BIG_WAVES * ks <= LD_LDS_MAX &&
+                   dbytes * 4 <= J * EX_WAVE_VALUES * W) {
+          // a dictionary past the mixed launch's LDS that one CU holds beside
+          // BIG_WAVES waves' keys: groups of big_jobs jobs in k_expand_big
+          const int64_t ng = (J + big_jobs - 1) / big_jobs;
+          for (int64_t q = 0; q < ng; q++) {
+            LdsGroup g = {};
+            g.job0 = -1 - (int32_t)big_tiles.size();  // rebased below
+            for (int64_t j = q * J / ng; j < (q + 1) * J / ng; j++) big_tiles.push_back(ct[(size_t)j]);
+            g.njobs = (int32_t)((q + 1) * J / ng - q * J / ng);
+            g.dpage = ct[0].dict;
+            g.dict_bytes = (int32_t)dbytes;
+            g.kspan = ks;
+            big_groups[ws].push_back(g);
+            B->ldl[2 + ws] = std::max(B->ldl[2 + ws], (int32_t)(dbytes + (int64_t)BIG_WAVES * ks));
+          }
+          ld = true;
+          B->pages[(size_t)ct[0].dict].alias_any = 1;
         }
       }
       if (!ld) {
@@ -1586,8 +1788,19 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     if (g.job0 < 0) g.job0 = (int32_t)slot_tiles.size() + (-1 - g.job0);
     if (b >= (size_t)B->ldn[0]) g.job0 -= B->ldn[0] * LD_WAVES_H;
   }
+  // k_expand_big groups after the mixed ones, with absolute job indices (their
+  // launches start at the first slot)
+  const size_t big_base = slot_tiles.size() + ld_tiles.size();
+  for (int ws = 0; ws < 2; ws++) {
+    for (LdsGroup g : big_groups[ws]) {
+      g.job0 = (int32_t)big_base + (-1 - g.job0);
+      B->lgroups.push_back(g);
+    }
+    B->ldn[2 + ws] = (int32_t)big_groups[ws].size();
+  }
   B->tiles = std::move(slot_tiles);
   B->tiles.insert(B->tiles.end(), ld_tiles.begin(), ld_tiles.end());
+  B->tiles.insert(B->tiles.end(), big_tiles.begin(), big_tiles.end());
 
   // k_snappy takes pages in list order, one wave each: the longest bodies
   // first (longest-processing-time order), so that the long serial token
@@ -1750,20 +1963,22 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   rc |= alloc_dev((void **)&B->d_dbg2, sizeof(uint64_t) * (16 * (npages + 1) + 256));  // + k_snappy_walk stamps
 #endif
   if (rc) return PQG_ERR_DEVICE;
-  if (hipHostMalloc((void **)&B->h_status, sizeof(uint32_t) * (npages + 1), hipHostMallocDefault) != hipSuccess) {
-    set_err("hipHostMalloc failed");
-    return PQG_ERR_DEVICE;
-  }
   phase("alloc");
   hipStream_t s = ctx->stream;
-  // one upload of all chunk bytes through the context's pinned ring
+  // one upload of all chunk bytes through the context's pinned ring, queued on
+  // the upload stream (decodes wait on `ready`; the host goes on planning)
   {
-    if (in_bytes && ring_upload(ctx, B->d_in, in, s)) {
+    if (in_bytes && ring_upload(ctx, B->d_in, in, ctx->upload)) {
       set_err("input upload failed");
       return PQG_ERR_DEVICE;
     }
-    hipMemsetAsync(B->d_in + in_bytes, 0, kPad, s);
+    hipMemsetAsync(B->d_in + in_bytes, 0, kPad, ctx->upload);
     B->h2d_bytes += (int64_t)in_bytes;
+    if (hipEventCreateWithFlags(&B->ready, hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(B->ready, ctx->upload) != hipSuccess) {
+      set_err("hipEventRecord failed");
+      return PQG_ERR_DEVICE;
+    }
   }
   for (auto &hb : host_bodies) {
     HIPCHK(hipMemcpy(B->d_stage + hb.first, hb.second.data(), hb.second.size(), hipMemcpyHostToDevice));
@@ -1790,7 +2005,6 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     lists.insert(lists.end(), B->dba_list.begin(), B->dba_list.end());
     if (!lists.empty()) HIPCHK(hipMemcpy(B->d_lists, lists.data(), sizeof(int32_t) * lists.size(), hipMemcpyHostToDevice));
   }
-  memcpy(B->h_status, B->status0.data(), sizeof(uint32_t) * npages);
   if (npages) HIPCHK(hipMemcpy(B->d_status0, B->status0.data(), sizeof(uint32_t) * npages, hipMemcpyHostToDevice));
   phase("upload");
 
@@ -1816,8 +2030,9 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   if (!B->cols.empty())
     HIPCHK(hipMemcpy(B->d_cols, B->hcols.data(), sizeof(ColDesc) * B->cols.size(), hipMemcpyHostToDevice));
   // the set-up copies and memsets above ran on the null stream, which the
-  // non-blocking context stream does not wait for
-  HIPCHK(hipDeviceSynchronize());
+  // non-blocking context stream does not wait for (only the null stream is
+  // waited for: another thread may be decoding on this device meanwhile)
+  HIPCHK(hipStreamSynchronize(nullptr));
   if (any_count) {
     // counting pass: snappy + prepare + scan once to size list/string outputs
     rc = launch_all(B, true, false);
@@ -1898,8 +2113,6 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   }
   if (!B->tiles.empty())
     HIPCHK(hipMemcpy(B->d_tiles, B->tiles.data(), sizeof(TileJob) * B->tiles.size(), hipMemcpyHostToDevice));
-  for (int k = 0; k < pqg_batch::kRing; k++)
-    for (int i = 0; i < 8; i++) hipEventCreate(&B->ev[k][i]);
   {  // the validity bitmaps k_reset zeroes in every decode
     std::vector<ZeroRange> zr;
     for (auto &cp : B->cols) {
@@ -1915,7 +2128,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
       HIPCHK(hipMemcpy(B->d_zr, zr.data(), sizeof(ZeroRange) * zr.size(), hipMemcpyHostToDevice));
     }
   }
-  HIPCHK(hipDeviceSynchronize());  // null-stream set-up done before the first decode on the context stream
+  HIPCHK(hipStreamSynchronize(nullptr));  // null-stream set-up done before the first decode on the context stream
   phase("outputs+tables");
   return PQG_OK;
 }
@@ -1946,6 +2159,11 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
 static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   hipStream_t s = B->ctx->stream;
   const size_t npages = B->pages.size();
+  // one launch sequence at a time per context (shared fork/join events)
+  std::lock_guard<std::mutex> launch_lock(B->ctx->launch_mu);
+  if (B->ready) hipStreamWaitEvent(s, B->ready, 0);  // the chunk bytes are on the device
+  if (timed && !B->ev[B->ring_head][0])  // timing events of this ring slot, made on first use
+    for (int i = 0; i < 8; i++) hipEventCreate(&B->ev[B->ring_head][i]);
   pq_launch_args a = {};
   a.in = B->d_in;
   a.stage = B->d_stage;
@@ -2126,7 +2344,20 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
       e |= pq_launch(10, &a, s);
     }
     a.nlist = (int32_t)B->tiles.size();
+    // k_expand_big (dictionaries that need a CU's LDS): after the mixed
+    // launch, before it (PQG_BIG_ORDER=1) or beside it on a side stream (=2)
+    static const int big_order = getenv("PQG_BIG_ORDER") ? atoi(getenv("PQG_BIG_ORDER")) : 0;
+    const bool big = B->ldn[2] + B->ldn[3] > 0;
+    if (big && big_order == 2) {
+      hipEventRecord(ctx->fork, s);
+      hipStreamWaitEvent(ctx->side[1], ctx->fork, 0);
+      e |= pq_launch(22, &a, ctx->side[1]);
+      hipEventRecord(ctx->join[1], ctx->side[1]);
+    }
+    if (big && big_order == 1) e |= pq_launch(22, &a, s);
     e |= pq_launch(9, &a, s);  // k_expand_mix (tiled pages)
+    if (big && big_order == 0) e |= pq_launch(22, &a, s);
+    if (big && big_order == 2) hipStreamWaitEvent(s, ctx->join[1], 0);
     if (B->ngen_flat > 0) hipStreamWaitEvent(s, ctx->join[0], 0);
     if (B->ngen_nest > 0) hipStreamWaitEvent(s, ctx->join[2], 0);
     mark(true);
@@ -2324,52 +2555,168 @@ int pqg_batch_kernel_times(pqg_batch *B, const char **names, float *ms, int cap)
 void pqg_batch_destroy(pqg_batch *B) {
   if (!B) return;
   hipSetDevice(B->ctx->device);
+  if (B->ready) hipEventSynchronize(B->ready);  // an upload never decoded may still be in flight
   hipStreamSynchronize(B->ctx->stream);
   for (auto &cp : B->cols) {
-    hipFree(cp.values);
-    hipFree(cp.validity);
-    hipFree(cp.list_offsets);
-    hipFree(cp.list_validity);
-    hipFree(cp.str_offsets);
-    hipFree(cp.def_out);
-    hipFree(cp.rep_out);
+    free_dev(cp.values);
+    free_dev(cp.validity);
+    free_dev(cp.list_offsets);
+    free_dev(cp.list_validity);
+    free_dev(cp.str_offsets);
+    free_dev(cp.def_out);
+    free_dev(cp.rep_out);
   }
-  hipFree(B->d_in_alloc);
-  hipFree(B->d_stage);
-  hipFree(B->d_pages);
-  hipFree(B->d_info);
-  hipFree(B->d_status);
-  hipFree(B->d_cols);
-  hipFree(B->d_dict);
-  hipFree(B->d_lists);
-  hipFree(B->d_jobs);
-  hipFree(B->d_njobs);
-  hipFree(B->d_job_base);
-  hipFree(B->d_job_owner);
-  hipFree(B->d_copy_cnt);
-  hipFree(B->d_status0);
-  hipFree(B->d_zr);
-  hipFree(B->d_copy_idx);
-  hipFree(B->d_lens);
-  hipFree(B->d_lvl);
-  hipFree(B->d_dbg);
-  hipFree(B->d_dbg2);
-  hipFree(B->d_runs);
-  hipFree(B->d_tile_info);
-  hipFree(B->d_tiles);
-  hipFree(B->d_recs);
-  hipFree(B->d_page_jobs);
-  hipFree(B->d_lgroups);
-  hipFree(B->d_sitems);
-  hipFree(B->d_seg_base);
-  hipFree(B->d_walk);
-  hipFree(B->d_segs);
-  hipFree(B->d_seg_flag);
-  if (B->h_status) hipHostFree(B->h_status);
+  free_dev(B->d_in_alloc);
+  free_dev(B->d_stage);
+  free_dev(B->d_pages);
+  free_dev(B->d_info);
+  free_dev(B->d_status);
+  free_dev(B->d_cols);
+  free_dev(B->d_dict);
+  free_dev(B->d_lists);
+  free_dev(B->d_jobs);
+  free_dev(B->d_njobs);
+  free_dev(B->d_job_base);
+  free_dev(B->d_job_owner);
+  free_dev(B->d_copy_cnt);
+  free_dev(B->d_status0);
+  free_dev(B->d_zr);
+  free_dev(B->d_copy_idx);
+  free_dev(B->d_lens);
+  free_dev(B->d_lvl);
+  free_dev(B->d_dbg);
+  free_dev(B->d_dbg2);
+  free_dev(B->d_runs);
+  free_dev(B->d_tile_info);
+  free_dev(B->d_tiles);
+  free_dev(B->d_recs);
+  free_dev(B->d_page_jobs);
+  free_dev(B->d_lgroups);
+  free_dev(B->d_sitems);
+  free_dev(B->d_seg_base);
+  free_dev(B->d_walk);
+  free_dev(B->d_segs);
+  free_dev(B->d_seg_flag);
+  if (B->ready) hipEventDestroy(B->ready);
   for (int k = 0; k < pqg_batch::kRing; k++)
     for (int i = 0; i < 8; i++)
       if (B->ev[k][i]) hipEventDestroy(B->ev[k][i]);
   delete B;
+}
+
+// ---------------------------------------------------------------------------
+// pipelined row-group slices (pqg_stream)
+// ---------------------------------------------------------------------------
+struct pqg_stream {
+  pqg_ctx *ctx = nullptr;
+  pqg_file *f = nullptr;
+  std::vector<int> leaves;
+  int flags = 0, depth = 2;
+  std::vector<std::pair<int, int>> slices;
+  std::vector<pqg_batch *> built;  // per slice, set by the worker
+  std::vector<int> rcs;
+  std::vector<std::string> errs;
+  size_t nbuilt = 0, ntaken = 0;
+  bool stop = false;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::thread worker;
+  pqg_batch *cur = nullptr;  // the slice last handed out
+};
+
+static void stream_worker(pqg_stream *S) {
+  hipSetDevice(S->ctx->device);
+  for (size_t k = 0; k < S->slices.size(); k++) {
+    {
+      std::unique_lock<std::mutex> lk(S->mu);
+      // at most `depth` slices built ahead of the one the caller holds
+      S->cv.wait(lk, [&] { return S->stop || k < S->ntaken + (size_t)S->depth; });
+      if (S->stop) return;
+    }
+    pqg_batch *B = nullptr;
+    const int rc = pqg_batch_create(S->ctx, S->f, S->slices[k].first, S->slices[k].second,
+                                    S->leaves.empty() ? nullptr : S->leaves.data(), (int)S->leaves.size(), S->flags, &B);
+    std::lock_guard<std::mutex> lk(S->mu);
+    S->built[k] = B;
+    S->rcs[k] = rc;
+    if (rc) S->errs[k] = g_err;  // the worker's thread-local message
+    S->nbuilt = k + 1;
+    S->cv.notify_all();
+    if (rc) return;  // the stream ends at a slice that failed to plan
+  }
+}
+
+int pqg_stream_open(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const int *leaves, int nleaves, int flags,
+                    int rgs_per_slice, int depth, pqg_stream **out) {
+  *out = nullptr;
+  if (!ctx || !f || rg_begin < 0 || rg_end > (int)f->rgs.size() || rg_begin > rg_end || nleaves < 0 ||
+      rgs_per_slice < 1 || depth < 1) {
+    set_err("bad stream arguments");
+    return PQG_ERR_ARG;
+  }
+  for (int i = 0; i < nleaves; i++)
+    if (!leaves || leaves[i] < 0 || leaves[i] >= (int)f->leaves.size()) {
+      set_err("leaf out of range");
+      return PQG_ERR_ARG;
+    }
+  pqg_stream *S = new pqg_stream();
+  S->ctx = ctx;
+  S->f = f;
+  if (nleaves > 0) S->leaves.assign(leaves, leaves + nleaves);
+  S->flags = flags;
+  S->depth = depth;
+  for (int r = rg_begin; r < rg_end; r += rgs_per_slice) S->slices.push_back({r, std::min(rg_end, r + rgs_per_slice)});
+  S->built.assign(S->slices.size(), nullptr);
+  S->rcs.assign(S->slices.size(), 0);
+  S->errs.assign(S->slices.size(), std::string());
+  S->worker = std::thread(stream_worker, S);
+  *out = S;
+  return PQG_OK;
+}
+
+int pqg_stream_next(pqg_stream *S, pqg_batch **out, int *rg_first) {
+  *out = nullptr;
+  if (!S) return PQG_ERR_ARG;
+  if (S->cur) {  // the caller is done with the previous slice
+    pqg_batch_destroy(S->cur);
+    S->cur = nullptr;
+  }
+  size_t k;
+  {
+    std::unique_lock<std::mutex> lk(S->mu);
+    k = S->ntaken;
+    if (k >= S->slices.size()) return PQG_OK;
+    S->cv.wait(lk, [&] { return S->nbuilt > k; });
+    S->ntaken = k + 1;
+    S->cv.notify_all();
+    if (S->rcs[k]) {
+      set_err("%s", S->errs[k].c_str());
+      S->ntaken = S->slices.size();  // nothing after a failed slice
+      return S->rcs[k];
+    }
+  }
+  pqg_batch *B = S->built[k];
+  S->built[k] = nullptr;
+  const int rc = pqg_batch_decode(B);
+  S->cur = B;
+  if (rc) return rc;
+  *out = B;
+  if (rg_first) *rg_first = S->slices[k].first;
+  return PQG_OK;
+}
+
+void pqg_stream_close(pqg_stream *S) {
+  if (!S) return;
+  {
+    std::lock_guard<std::mutex> lk(S->mu);
+    S->stop = true;
+    S->cv.notify_all();
+  }
+  if (S->worker.joinable()) S->worker.join();
+  if (S->cur) pqg_batch_destroy(S->cur);
+  for (pqg_batch *B : S->built)
+    if (B) pqg_batch_destroy(B);
+  delete S;
 }
 
 }  // extern "C"
@@ -2483,7 +2830,7 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
     hipMemcpyAsync(&hi, d_info, sizeof(hi), hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
     if (hi.alias1 && expect) hipMemcpyAsync(d_out, d_in + (hi.alias1 - 1), expect, hipMemcpyDeviceToDevice, s);
-    hipFree(d_info);
+    free_dev(d_info);
     hipStreamSynchronize(s);
     hipMemcpyAsync(&st, d_st, 4, hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
@@ -2493,22 +2840,22 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
       hipStreamSynchronize(s);
     }
   }
-  hipFree(d_in);
-  hipFree(d_out);
-  hipFree(d_page);
-  hipFree(d_st);
-  hipFree(d_list);
-  hipFree(d_jobs);
-  hipFree(d_njobs);
-  hipFree(d_cc);
-  hipFree(d_ci);
-  hipFree(d_jb);
-  hipFree(d_jo);
-  hipFree(d_sitems);
-  hipFree(d_sbase);
-  hipFree(d_walk);
-  hipFree(d_segs);
-  hipFree(d_sflag);
+  free_dev(d_in);
+  free_dev(d_out);
+  free_dev(d_page);
+  free_dev(d_st);
+  free_dev(d_list);
+  free_dev(d_jobs);
+  free_dev(d_njobs);
+  free_dev(d_cc);
+  free_dev(d_ci);
+  free_dev(d_jb);
+  free_dev(d_jo);
+  free_dev(d_sitems);
+  free_dev(d_sbase);
+  free_dev(d_walk);
+  free_dev(d_segs);
+  free_dev(d_sflag);
   if (rc) {
     if (g_err.empty()) set_err("device snappy failed");
     return PQG_ERR_DEVICE;

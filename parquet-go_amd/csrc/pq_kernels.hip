@@ -1521,7 +1521,6 @@ __device__ __forceinline__ uint32_t ba_walk(const uint8_t *vp, int64_t vlen, int
 __global__ __launch_bounds__(256) void k_dict_prepare(KArgs a) {
   const int gi = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
   if (gi >= a.nlist) return;
-  const int lane = lane_id();
   const int page = ufirst(a.list[gi]);
   const PageDesc d = a.pages[page];
   if (page_status(a.status, page) != STATUS_OK) return;
@@ -3563,7 +3562,7 @@ __device__ __forceinline__ void mix_global(const KArgs &a, const LdsGroup &g, ui
   expand_job<WIDTH, false>(a, tj, rc, lds_dyn + wv * (g.kspan / 4), g.kspan, nullptr);
 }
 
-template <int WIDTH>
+template <int WIDTH, int NW = LD_WAVES>
 __device__ __forceinline__ void mix_lds(const KArgs &a, const LdsGroup &g, uint32_t *lds_dyn) {
   const int wv = (int)ufirst(threadIdx.x >> 6);
   const int jend = g.job0 + g.njobs;
@@ -3594,7 +3593,7 @@ __device__ __forceinline__ void mix_lds(const KArgs &a, const LdsGroup &g, uint3
       (void *)((uintptr_t)dict & ~(uintptr_t)3), (short)0, (int)((nbytes + dsh + 3) & ~3u), 0x00020000);
   const uint32_t n16 = (nbytes + 15) / 16;
   // the copy: four 16-byte pieces per thread in flight at a time
-  constexpr uint32_t T = LD_WAVES * 64;
+  constexpr uint32_t T = NW * 64;
   for (uint32_t i0 = threadIdx.x; i0 < n16; i0 += 4 * T) {
     u32x4 x[4];
     uint32_t y[4];
@@ -3615,7 +3614,7 @@ __device__ __forceinline__ void mix_lds(const KArgs &a, const LdsGroup &g, uint3
   }
   __syncthreads();
   uint32_t *kspan = lds_dyn + g.dict_bytes / 4 + wv * (g.kspan / 4);
-  for (; j < jend; j += LD_WAVES) {
+  for (; j < jend; j += NW) {
     if (j != g.job0 + wv) {
       tj = sload(a.tiles + j);
       rc = sload(a.recs + j);
@@ -3638,6 +3637,20 @@ __global__ __launch_bounds__(LD_WAVES_H * 64) void k_expand_mix(KArgs a) {
     a.dbg[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + 7] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
+}
+
+// k_expand_big: one workgroup of BIG_WAVES waves per group of jobs whose
+// dictionary is too large for the mixed launch's LDS budget but fits a CU's
+// (host: dictionary + BIG_WAVES staged-key spans <= 160 KiB).  The dictionary
+// is copied once and shared by twice as many waves as in k_expand_mix, so one
+// resident workgroup per CU still keeps two waves per SIMD gathering from LDS
+// (measured on single-width files: bit widths 13-15 gather from L1/L2 at
+// 270-490 Gvalues/s, from LDS at 340-660 even with one 4-wave group per CU).
+template <int WIDTH>
+__global__ __launch_bounds__(BIG_WAVES * 64) void k_expand_big(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
+  const LdsGroup g = sload(a.lgroups + blockIdx.x);
+  mix_lds<WIDTH, BIG_WAVES>(a, g, lds_dyn);
 }
 
 // ===========================================================================
@@ -3867,12 +3880,28 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     hipLaunchKernelGGL(pq::k_copy, dim3(items < 4096 ? items : 4096), dim3(256), 0, s, k);
     return hipGetLastError() == hipSuccess ? 0 : 17;
   }
-  if (which == 9) {  // k_expand_mix: one 512-thread workgroup per LdsGroup (absolute job indices)
+  if (which == 9 || which == 22) {  // k_expand_mix (9) / k_expand_big (22): one workgroup per LdsGroup
     static bool attr = false;
     if (!attr) {
       hipFuncSetAttribute((const void *)pq::k_expand_mix<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       hipFuncSetAttribute((const void *)pq::k_expand_mix<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      hipFuncSetAttribute((const void *)pq::k_expand_big<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      hipFuncSetAttribute((const void *)pq::k_expand_big<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr = true;
+    }
+    if (which == 22) {
+      // k_expand_big: big-dictionary groups after the mixed ones, absolute job indices
+      const pq::LdsGroup *bg = (const pq::LdsGroup *)p->lgroups + p->ldn[0] + p->ldn[1];
+      for (int w = 0; w < 2; w++) {
+      if (p->ldn[2 + w] <= 0) continue;
+      pq::KArgs kb = k;
+      kb.lgroups = bg + (w ? p->ldn[2] : 0);
+      if (w == 0)
+        hipLaunchKernelGGL(pq::k_expand_big<4>, dim3(p->ldn[2]), dim3(pq::BIG_WAVES * 64), (size_t)p->ldl[2], s, kb);
+      else
+        hipLaunchKernelGGL(pq::k_expand_big<8>, dim3(p->ldn[3]), dim3(pq::BIG_WAVES * 64), (size_t)p->ldl[3], s, kb);
+      }
+      return hipGetLastError() == hipSuccess ? 0 : 17;
     }
     const dim3 blk(pq::LD_WAVES_H * 64);
     if (p->ldn[0] > 0) hipLaunchKernelGGL(pq::k_expand_mix<4>, dim3(p->ldn[0]), blk, (size_t)p->ldl[0], s, k);

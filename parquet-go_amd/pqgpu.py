@@ -56,6 +56,7 @@ EXPORTS = [
     "pqg_file_last_error", "pqg_batch_create", "pqg_batch_decode", "pqg_batch_sync",
     "pqg_batch_error_location", "pqg_batch_column", "pqg_batch_copy", "pqg_batch_stats_get",
     "pqg_batch_kernel_times", "pqg_batch_set_timing", "pqg_batch_destroy",
+    "pqg_stream_open", "pqg_stream_next", "pqg_stream_close",
 ]
 
 
@@ -131,6 +132,9 @@ def lib():
                 "pqg_batch_kernel_times": (i32, [vp, P(ctypes.c_char_p), P(ctypes.c_float), i32]),
                 "pqg_batch_set_timing": (i32, [vp, i32]),
                 "pqg_batch_destroy": (None, [vp]),
+                "pqg_stream_open": (i32, [vp, vp, i32, i32, P(ctypes.c_int), i32, i32, i32, i32, P(vp)]),
+                "pqg_stream_next": (i32, [vp, P(vp), P(ctypes.c_int)]),
+                "pqg_stream_close": (None, [vp]),
             }
             for name, (res, args) in sig.items():
                 fn = getattr(L, name)
@@ -314,6 +318,64 @@ class Batch:
             pass
 
 
+class _SliceBatch(Batch):
+    """A slice handed out by a Stream: the stream owns (and frees) its handle."""
+
+    def __init__(self, reader, handle, rg0, leaves, ctx):
+        self.reader, self.ctx, self.leaves, self.rg0 = reader, ctx, list(leaves), rg0
+        self._h = ctypes.c_void_p(handle)
+
+    def close(self):
+        self._h = ctypes.c_void_p()
+
+
+class Stream:
+    """Row groups [rg0, rg1) in slices of `rgs_per_slice`, pipelined: the next
+    slice is planned and uploaded by a host worker while the current one
+    decodes (pqg_stream_*; file_reader.go:101-116 row-group iteration).
+    Iterating yields each slice's batch with its decode launched; a yielded
+    batch is valid until the next one is requested."""
+
+    def __init__(self, reader, rg0, rg1, leaves, rgs_per_slice=1, depth=2, flags=0, ctx=None):
+        self.reader = reader
+        self.ctx = ctx or reader.ctx
+        self.leaves = list(leaves)
+        self._h = ctypes.c_void_p()
+        arr = (ctypes.c_int * max(len(self.leaves), 1))(*self.leaves)
+        _check(lib().pqg_stream_open(self.ctx.handle, reader.handle, rg0, rg1, arr, len(self.leaves), flags,
+                                     rgs_per_slice, depth, ctypes.byref(self._h)), "pqg_stream_open")
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        if not self._h:
+            raise StopIteration
+        b, rg = ctypes.c_void_p(), ctypes.c_int()
+        _check(lib().pqg_stream_next(self._h, ctypes.byref(b), ctypes.byref(rg)), "pqg_stream_next")
+        if not b.value:
+            self.close()
+            raise StopIteration
+        return _SliceBatch(self.reader, b.value, rg.value, self.leaves, self.ctx)
+
+    def close(self):
+        if self._h:
+            lib().pqg_stream_close(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class FileReader:
     """NewFileReader(r, columns...) (file_reader.go:27) backed by the GPU decoder."""
 
@@ -383,6 +445,11 @@ class FileReader:
     def batch(self, rg0=0, rg1=None, leaves=None, flags=0):
         rg1 = self.RowGroupCount() if rg1 is None else rg1
         return Batch(self, rg0, rg1, self.selected if leaves is None else leaves, flags)
+
+    def stream(self, rg0=0, rg1=None, rgs_per_slice=1, leaves=None, depth=2, flags=0):
+        """Pipelined decode of row groups [rg0, rg1) slice by slice (Stream)."""
+        rg1 = self.RowGroupCount() if rg1 is None else rg1
+        return Stream(self, rg0, rg1, self.selected if leaves is None else leaves, rgs_per_slice, depth, flags)
 
     def read_row_groups(self, rg0=0, rg1=None, leaves=None, levels=False):
         """Decode row groups [rg0, rg1) on the GPU; returns {flat_name: buffers}."""

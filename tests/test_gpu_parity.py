@@ -352,6 +352,55 @@ def test_c5_lineitem_large_string_dictionary(tmp_path):
     check_file(_c5_bytes(tmp_path, 80000, 40000), "c5 default dict")
 
 
+@pytest.mark.parametrize("per,depth", [(1, 2), (2, 1), (3, 3)])
+def test_stream_slices_match_oracle(tmp_path, per, depth):
+    """pqg_stream: row-group slices planned and uploaded by the host worker
+    while the previous slice decodes; every slice bit-exact against the oracle's
+    decode of the same row-group range (C5 shape: 16 leaves, strings, fallback
+    to PLAIN; C4 golden: lists and nullable strings)."""
+    pytest.importorskip("pyarrow")
+    for data, ctx in ((_c5_bytes(tmp_path, 70000, 10000, dictionary_pagesize_limit=64 << 10), "c5"),
+                      (golden_bytes("c4_list_str.parquet"), "c4")):
+        o = oracle.File(data)
+        r = pqgpu.FileReader(data)
+        leaves = list(range(len(r.Columns())))
+        seen = []
+        with r.stream(0, None, per, leaves, depth) as st:
+            for b in st:
+                rc = b.sync(raise_on_error=False)
+                assert rc == 0, (ctx, b.rg0, pqgpu.last_error())
+                rg1 = min(b.rg0 + per, o.num_row_groups)
+                for i, leaf in enumerate(leaves):
+                    info = o.leaves()[leaf]
+                    assert_same(b.column(i), o.decode(leaf, b.rg0, rg1), info["max_def"], info["max_rep"],
+                                "%s stream slice %d leaf %d" % (ctx, b.rg0, leaf))
+                seen.append(b.rg0)
+        assert seen == list(range(0, o.num_row_groups, per)), (ctx, seen)
+
+
+def test_stream_reports_slice_errors():
+    """A slice whose pages fail to decode reports the batch's first error; a
+    stream over a file with an unsupported slice stops there."""
+    data = golden_bytes("err_delta_1.parquet")
+    o = oracle.File(data)
+    r = pqgpu.FileReader(data)
+    leaves = list(range(len(r.Columns())))
+    codes = []
+    with r.stream(0, None, 1, leaves) as st:
+        try:
+            for b in st:
+                codes.append(b.sync(raise_on_error=False))
+        except pqgpu.PqgError as e:  # an error found while planning a slice
+            codes.append(e.code)
+    want = None
+    for leaf in leaves:
+        try:
+            o.decode(leaf)
+        except oracle.OracleError as e:
+            want = e.code if want is None else want
+    assert want is not None and want in codes, (codes, want)
+
+
 def test_tiled_rle_heavy_keys():
     """Bit width 1 and 2 key streams that alternate RLE and short bit-packed
     runs (the run walk's chain mode; k_expand's general rows)."""
