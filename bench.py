@@ -259,7 +259,7 @@ def segment_times(reader, rg0, rg1, decodes=6):
         b.close()
 
 
-def e2e_rates(reader, rg0, rg1, stats, slices=12):
+def e2e_rates(reader, rg0, rg1, stats, slices=24, depth=4):
     """PCIe-inclusive rates (never `value`): the whole shard read through
     pqg_stream — the host worker plans and uploads slice k + 1 (pinned ring,
     PQG_UPLOAD_THREADS gather threads) while the GPU decodes slice k — timed
@@ -285,12 +285,12 @@ def e2e_rates(reader, rg0, rg1, stats, slices=12):
     best = None
     for _ in range(2):  # the first pass also maps the file pages
         t = time.perf_counter()
-        with reader.stream(rg0, rg1, per) as st:
+        with reader.stream(rg0, rg1, per, None, depth) as st:
             for b in st:
                 b.sync()
         t = time.perf_counter() - t
         best = t if best is None else min(best, t)
-    out = {"stream_ms": round(best * 1e3, 2), "stream_rgs_per_slice": per,
+    out = {"stream_ms": round(best * 1e3, 2), "stream_rgs_per_slice": per, "stream_depth": depth,
            "GBps_stream_incl_plan_and_h2d": round(stats["output_bytes"] / best / 1e9, 1),
            "h2d_bytes": n}
     if pcie:

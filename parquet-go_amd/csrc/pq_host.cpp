@@ -588,16 +588,22 @@ static int ring_upload(pqg_ctx *c, uint8_t *dst, const Layout &in, hipStream_t s
   }
   if (!c->pool_started) {
     const char *e = getenv("PQG_UPLOAD_THREADS");
-    const int nt = std::max(1, std::min(e ? atoi(e) : 4, 32));
+    const int nt = std::max(1, std::min(e ? atoi(e) : 6, 32));
     c->pool.start(nt - 1);
     c->pool_started = true;
   }
   const int nthreads = (int)c->pool.th.size() + 1;
+  static const bool trace = getenv("PQG_TRACE_CREATE") != nullptr;
+  double t_wait = 0, t_gather = 0;
+  auto now = [] { return std::chrono::steady_clock::now(); };
   size_t off = 0;
   while (off < n) {
     const int k = c->pin_next;
     const size_t m = std::min(pqg_ctx::kRingBytes, n - off);
+    auto t0 = now();
     if (c->pin_busy[k] && hipEventSynchronize(c->pin_ev[k]) != hipSuccess) return 1;
+    auto t1 = now();
+    t_wait += std::chrono::duration<double, std::milli>(t1 - t0).count();
     c->pin_busy[k] = false;
     // gather [off, off + m) of the layout into the pinned buffer, in parts of >= 1 MiB
     uint8_t *pb = (uint8_t *)c->pin[k];
@@ -626,12 +632,16 @@ static int ring_upload(pqg_ctx *c, uint8_t *dst, const Layout &in, hipStream_t s
     };
     if (parts > 1) c->pool.run(parts, part);
     else part(0);
+    t_gather += std::chrono::duration<double, std::milli>(now() - t1).count();
     if (hipMemcpyAsync(dst + off, c->pin[k], m, hipMemcpyHostToDevice, s) != hipSuccess) return 1;
     hipEventRecord(c->pin_ev[k], s);
     c->pin_busy[k] = true;
     off += m;
     c->pin_next = (k + 1) % pqg_ctx::kRingBufs;
   }
+  if (trace)
+    fprintf(stderr, "ring_upload %.1f MB: gather %.2f ms (%.1f GB/s, %d threads), ring wait %.2f ms\n", n / 1e6, t_gather,
+            t_gather > 0 ? n / t_gather / 1e6 : 0.0, nthreads, t_wait);
   return 0;
 }
 
@@ -750,6 +760,10 @@ struct pqg_batch {
   int err_rg = -1, err_leaf = -1, err_page = -1;
   bool decoded = false;
   hipEvent_t ready = nullptr;  // recorded on the context's upload stream after the chunk bytes' H2D
+  std::vector<uint8_t> tab_host;  // the small tables (d_pages, d_info, d_lists, ...): host image, uploaded at
+                                  // the end of d_in
+  std::vector<ColDesc> hcols0;    // column descriptors as first uploaded (before the counting pass)
+  std::vector<ZeroRange> zr_host;
 };
 
 // timed segments: with PQG_SEGMENT_TIMES every phase, otherwise the decode phase only
@@ -1469,6 +1483,7 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
 // only after its batch's work has finished (pqg_batch_destroy synchronises).
 // Held bytes are capped (PQG_DEV_CACHE_MB, default 32 GiB); a failed
 // hipMalloc releases the device's cache and retries.
+}  // extern "C" (the cache is C++)
 namespace {
 struct DevCache {
   std::mutex mu;
@@ -1500,6 +1515,7 @@ void release_idle(DevCache &c, int dev) {  // caller holds c.mu
   }
 }
 }  // namespace
+extern "C" {
 
 static int alloc_dev(void **p, size_t n) {
   int dev = 0;
@@ -1676,8 +1692,39 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   std::vector<TileJob> slot_tiles, ld_tiles, big_tiles;
   std::vector<LdsGroup> big_groups[2];
   const int64_t ld_max = getenv("PQG_LD_MAX_KB") ? 1024 * (int64_t)atoi(getenv("PQG_LD_MAX_KB")) : LD_MIX_MAX;
-  const bool big_off = getenv("PQG_NO_BIG") != nullptr || getenv("PQG_BIG") == nullptr;  // analysis: opt-in until measured
   const int64_t big_jobs = getenv("PQG_BIG_JOBS") ? std::max(1, atoi(getenv("PQG_BIG_JOBS"))) : BIG_JOBS;
+  // which chunks fit the mixed launch's LDS groups, or only k_expand_big's
+  auto ld_class = [&](const std::vector<TileJob> &ct, int32_t W, int64_t &dbytes, int32_t &ks) {
+    dbytes = 0;
+    ks = 0;
+    if (ld_off || ct.empty() || ct[0].dict < 0) return 0;
+    dbytes = ((int64_t)std::max(B->pages[(size_t)ct[0].dict].num_values, 0) * W + 15) & ~15;
+    for (const TileJob &tj : ct) ks = std::max(ks, page_need[(size_t)tj.page]);
+    ks = (ks + 255) & ~255;
+    const int64_t J = (int64_t)ct.size();
+    if (dbytes <= 0 || ks <= 0 || dbytes * 4 > J * EX_WAVE_VALUES * W) return 0;
+    if (dbytes + (int64_t)LD_WAVES_H * ks <= ld_max) return 1;
+    if (dbytes + (int64_t)BIG_WAVES * ks <= LD_LDS_MAX) return 2;
+    return 0;
+  };
+  // k_expand_big is its own launch: it pays when its chunks are a good part
+  // of the tiled jobs (measured: single-width files at bit widths 13-15 gain
+  // 45-70 %; in C2, where they are 15 % of the jobs beside L2-bound blocks of
+  // wider dictionaries that hide them, the extra launch costs 13 %).
+  // PQG_BIG=1 / PQG_NO_BIG=1 force it on / off.
+  bool big_off;
+  {
+    int64_t nbig = 0, nall = 0;
+    for (const auto &ct : chunk_tiles) {
+      if (ct.empty()) continue;
+      const int32_t W = B->cols[(size_t)B->pages[(size_t)ct[0].page].col].info.value_width;
+      int64_t db;
+      int32_t ks;
+      nall += (int64_t)ct.size();
+      if (ld_class(ct, W, db, ks) == 2) nbig += (int64_t)ct.size();
+    }
+    big_off = getenv("PQG_NO_BIG") != nullptr || (getenv("PQG_BIG") == nullptr && nbig * 3 < nall);
+  }
   for (int ws = 0; ws < 2; ws++) {
     const int32_t W = ws == 0 ? 4 : 8;
     struct LdG {
@@ -1690,14 +1737,12 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     for (const auto &ct : chunk_tiles) {
       if (ct.empty() || B->cols[(size_t)B->pages[(size_t)ct[0].page].col].info.value_width != W) continue;
       bool ld = false;
-      if (!ld_off && ct[0].dict >= 0) {
-        const int64_t dbytes = ((int64_t)std::max(B->pages[(size_t)ct[0].dict].num_values, 0) * W + 15) & ~15;
-        int32_t ks = 0;
-        for (const TileJob &tj : ct) ks = std::max(ks, page_need[(size_t)tj.page]);
-        ks = (ks + 255) & ~255;
+      int64_t dbytes;
+      int32_t ks;
+      const int cls = ld_class(ct, W, dbytes, ks);
+      if (cls) {
         const int64_t J = (int64_t)ct.size();
-        if (dbytes > 0 && ks > 0 && dbytes + (int64_t)LD_WAVES_H * ks <= ld_max &&
-            dbytes * 4 <= J * EX_WAVE_VALUES * W) {
+        if (cls == 1) {
           const int64_t amort = getenv("PQG_LD_AMORT") ? atoi(getenv("PQG_LD_AMORT")) : 2;
           int64_t G = (dbytes * amort + (int64_t)EX_WAVE_VALUES * W - 1) / ((int64_t)EX_WAVE_VALUES * W);
           const int64_t gmin = getenv("PQG_LD_GMIN") ? atoi(getenv("PQG_LD_GMIN")) : LD_WAVES_H;
@@ -1706,8 +1751,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
           for (int64_t q = 0; q < ng; q++) ldg.push_back({&ct, q * J / ng, (q + 1) * J / ng, (int32_t)dbytes, ks});
           ld = true;
           B->pages[(size_t)ct[0].dict].alias_any = 1;  // copied into LDS with a funnel shift anyway
-        } else if (!big_off && dbytes > 0 && ks > 0 && dbytes + (int64_t)BIG_WAVES * ks <= LD_LDS_MAX &&
-                   dbytes * 4 <= J * EX_WAVE_VALUES * W) {
+        } else if (!big_off) {
           // a dictionary past the mixed launch's LDS that one CU holds beside
           // BIG_WAVES waves' keys: groups of big_jobs jobs in k_expand_big
           const int64_t ng = (J + big_jobs - 1) / big_jobs;
@@ -1871,6 +1915,76 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     }
   }
   phase("plan");
+  // tables
+  std::vector<std::pair<void **, size_t>> tab_fix;
+  size_t tab_off = 0;
+  // positions of every page's jobs in the launch order; records start stale (epoch 0)
+  std::vector<int32_t> pj((size_t)B->page_job_entries + 1, 0);
+  for (size_t p = 0; p < B->tiles.size(); p++) {
+    const TileJob &tj = B->tiles[p];
+    if (tj.page < 0) continue;
+    pj[(size_t)B->pages[(size_t)tj.page].job_base + (size_t)(tj.v0 / EX_WAVE_VALUES)] = (int32_t)p;
+  }
+  // per Snappy page a region of job slots: at most body_len / 16 KB literals are long enough to defer
+  std::vector<int32_t> job_base(B->snappy_list.size() + 1), job_owner;
+  for (size_t q = 0; q < B->snappy_list.size(); q++) {
+    job_base[q] = (int32_t)job_owner.size();
+    // BYTE_ARRAY dictionary pages copy their long literals themselves:
+    // k_dict_prepare reads them beside the data pages' Snappy decode, before
+    // k_copy (fixed-width dictionaries are read after it)
+    const PageDesc &sp = B->pages[(size_t)B->snappy_list[q]];
+    const bool ba_dict = sp.kind == PAGE_DICT && B->cols[(size_t)sp.col].info.physical_type == T_BYTE_ARRAY;
+    int32_t cap = ba_dict ? 0 : std::min(64, sp.body_len / (16 * 1024));
+    for (int32_t k = 0; k < cap; k++) job_owner.push_back((int32_t)q);
+  }
+  B->max_jobs = (uint32_t)job_owner.size();
+  B->ngen_flat = (int32_t)B->general_flat.size();
+  B->general_list.insert(B->general_list.end(), B->general_flat.begin(), B->general_flat.end());
+  B->general_flat.clear();
+  B->ngen_str = (int32_t)B->general_str.size();
+  B->general_list.insert(B->general_list.end(), B->general_str.begin(), B->general_str.end());
+  B->general_str.clear();
+  B->ngen_nest = (int32_t)B->general_nest.size();
+  B->general_list.insert(B->general_list.end(), B->general_nest.begin(), B->general_nest.end());
+  B->general_nest.clear();
+  {
+    std::vector<int32_t> lists;
+    lists.insert(lists.end(), B->snappy_list.begin(), B->snappy_list.end());
+    lists.insert(lists.end(), B->dict_list.begin(), B->dict_list.end());
+    lists.insert(lists.end(), B->data_list.begin(), B->data_list.end());
+    lists.insert(lists.end(), B->general_list.begin(), B->general_list.end());
+    lists.insert(lists.end(), B->dba_list.begin(), B->dba_list.end());
+    // the small tables: one host image (256-byte aligned entries; the
+    // zero-initialised ones are zeros in it) and one copy instead of a
+    // synchronous copy or memset each (tens of µs apiece)
+    struct {
+      std::vector<uint8_t> h;
+      std::vector<std::pair<void **, size_t>> fix;
+      void put(void **dst, const void *src, size_t n) {
+        const size_t off = (h.size() + 255) & ~(size_t)255;
+        h.resize(off + std::max<size_t>(n, 64), 0);
+        if (src && n) memcpy(h.data() + off, src, n);
+        fix.push_back({dst, off});
+      }
+    } tab;
+    tab.put((void **)&B->d_pages, B->pages.data(), sizeof(PageDesc) * npages);
+    tab.put((void **)&B->d_status0, B->status0.data(), sizeof(uint32_t) * npages);
+    tab.put((void **)&B->d_lists, lists.data(), sizeof(int32_t) * lists.size());
+    tab.put((void **)&B->d_lgroups, B->lgroups.data(), sizeof(LdsGroup) * (B->lgroups.size() + 1));
+    tab.put((void **)&B->d_page_jobs, pj.data(), sizeof(int32_t) * pj.size());
+    tab.put((void **)&B->d_sitems, B->snap_items.data(), 4 * B->snap_items.size());
+    tab.put((void **)&B->d_seg_base, B->seg_base.data(), 4 * B->seg_base.size());
+    tab.put((void **)&B->d_walk, B->walk_list.data(), 4 * B->walk_list.size());
+    tab.put((void **)&B->d_seg_flag, nullptr, 4 * (B->snappy_list.size() + 1));
+    tab.put((void **)&B->d_copy_cnt, nullptr, 16);
+    tab.put((void **)&B->d_job_base, job_base.data(), 4 * job_base.size());
+    tab.put((void **)&B->d_job_owner, job_owner.data(), 4 * job_owner.size());
+    // the image travels with the chunk bytes (the end of the input layout):
+    // one pinned-ring upload, no separate copy
+    B->tab_host = std::move(tab.h);
+    tab_off = in.append(B->tab_host.data(), B->tab_host.size(), 256);
+    tab_fix = std::move(tab.fix);
+  }
   // device buffers
   int rc = 0;
   size_t in_bytes = in.n;
@@ -1892,72 +2006,22 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   rc |= alloc_dev((void **)&B->d_stage, (size_t)stage_off);
   B->in_alloc = in_bytes + kPad;
   B->stage_alloc = (size_t)stage_off + kPad;
-  rc |= alloc_dev((void **)&B->d_pages, sizeof(PageDesc) * npages);
-  rc |= alloc_dev((void **)&B->d_info, sizeof(PageInfo) * npages);
   rc |= alloc_dev((void **)&B->d_status, sizeof(uint32_t) * npages);
-  rc |= alloc_dev((void **)&B->d_status0, sizeof(uint32_t) * npages);
+  // zero-initialised on the upload stream (not shipped as zeros): page infos
+  // (failed pages count zero in the scans) and job records (stale: epoch 0)
+  rc |= alloc_dev((void **)&B->d_info, sizeof(PageInfo) * npages);
+  rc |= alloc_dev(&B->d_recs, sizeof(ExRec) * (B->tiles.size() + 1));
   rc |= alloc_dev((void **)&B->d_cols, sizeof(ColDesc) * B->cols.size());
   rc |= alloc_dev((void **)&B->d_dict, sizeof(uint64_t) * (size_t)B->dict_entries);
-  size_t nl = B->snappy_list.size() + B->dict_list.size() + 3 * B->data_list.size() + 16;
-  rc |= alloc_dev((void **)&B->d_lists, sizeof(int32_t) * nl);
   rc |= alloc_dev(&B->d_runs, 8 * (size_t)(B->run_entries + 64));
   rc |= alloc_dev(&B->d_tile_info, 8 * (size_t)(B->tile_entries + EX_WAVE_VALUES / RUN_TILE + 1));
   rc |= alloc_dev((void **)&B->d_tiles, sizeof(TileJob) * (B->tiles.size() + 1));
-  rc |= alloc_dev(&B->d_recs, sizeof(ExRec) * (B->tiles.size() + 1));
-  rc |= alloc_dev((void **)&B->d_page_jobs, sizeof(int32_t) * (size_t)(B->page_job_entries + 1));
-  rc |= alloc_dev((void **)&B->d_lgroups, sizeof(LdsGroup) * (B->lgroups.size() + 1));
-  if (!rc && !B->lgroups.empty())
-    hipMemcpy(B->d_lgroups, B->lgroups.data(), sizeof(LdsGroup) * B->lgroups.size(), hipMemcpyHostToDevice);
-  if (!rc) {
-    // positions of every page's jobs in the launch order; records start stale (epoch 0)
-    std::vector<int32_t> pj((size_t)B->page_job_entries + 1, 0);
-    for (size_t p = 0; p < B->tiles.size(); p++) {
-      const TileJob &tj = B->tiles[p];
-      if (tj.page < 0) continue;
-      pj[(size_t)B->pages[(size_t)tj.page].job_base + (size_t)(tj.v0 / EX_WAVE_VALUES)] = (int32_t)p;
-    }
-    hipMemcpy(B->d_page_jobs, pj.data(), sizeof(int32_t) * pj.size(), hipMemcpyHostToDevice);
-    hipMemset(B->d_recs, 0, sizeof(ExRec) * (B->tiles.size() + 1));
-  }
-  // per Snappy page a region of job slots: at most body_len / 16 KB literals are long enough to defer
-  std::vector<int32_t> job_base(B->snappy_list.size() + 1), job_owner;
-  for (size_t q = 0; q < B->snappy_list.size(); q++) {
-    job_base[q] = (int32_t)job_owner.size();
-    // BYTE_ARRAY dictionary pages copy their long literals themselves:
-    // k_dict_prepare reads them beside the data pages' Snappy decode, before
-    // k_copy (fixed-width dictionaries are read after it)
-    const PageDesc &sp = B->pages[(size_t)B->snappy_list[q]];
-    const bool ba_dict = sp.kind == PAGE_DICT && B->cols[(size_t)sp.col].info.physical_type == T_BYTE_ARRAY;
-    int32_t cap = ba_dict ? 0 : std::min(64, sp.body_len / (16 * 1024));
-    for (int32_t k = 0; k < cap; k++) job_owner.push_back((int32_t)q);
-  }
-  B->max_jobs = (uint32_t)job_owner.size();
   rc |= alloc_dev(&B->d_jobs, 32 * (size_t)B->max_jobs);
   rc |= alloc_dev((void **)&B->d_njobs, 4 * (B->snappy_list.size() + 1));
-  rc |= alloc_dev((void **)&B->d_job_base, 4 * job_base.size());
-  rc |= alloc_dev((void **)&B->d_job_owner, 4 * (job_owner.size() + 1));
-  rc |= alloc_dev((void **)&B->d_copy_cnt, 16);
   rc |= alloc_dev((void **)&B->d_copy_idx, 4 * (job_owner.size() + 1));
   rc |= alloc_dev((void **)&B->d_lens, 4 * (size_t)(B->lens_entries + 1));
   rc |= alloc_dev((void **)&B->d_lvl, (size_t)B->lvl_bytes + 16);
-  rc |= alloc_dev((void **)&B->d_sitems, 4 * (B->snap_items.size() + 2));
-  rc |= alloc_dev((void **)&B->d_seg_base, 4 * B->seg_base.size());
-  rc |= alloc_dev((void **)&B->d_walk, 4 * (B->walk_list.size() + 1));
   rc |= alloc_dev((void **)&B->d_segs, 8 * (size_t)(B->seg_base.back() + 1));
-  rc |= alloc_dev((void **)&B->d_seg_flag, 4 * (B->snappy_list.size() + 1));
-  if (!rc) {
-    if (!B->snap_items.empty())
-      hipMemcpy(B->d_sitems, B->snap_items.data(), 4 * B->snap_items.size(), hipMemcpyHostToDevice);
-    hipMemcpy(B->d_seg_base, B->seg_base.data(), 4 * B->seg_base.size(), hipMemcpyHostToDevice);
-    if (!B->walk_list.empty())
-      hipMemcpy(B->d_walk, B->walk_list.data(), 4 * B->walk_list.size(), hipMemcpyHostToDevice);
-    hipMemset(B->d_seg_flag, 0, 4 * (B->snappy_list.size() + 1));
-  }
-  if (!rc) {
-    hipMemset(B->d_copy_cnt, 0, 16);
-    hipMemcpy(B->d_job_base, job_base.data(), 4 * job_base.size(), hipMemcpyHostToDevice);
-    if (!job_owner.empty()) hipMemcpy(B->d_job_owner, job_owner.data(), 4 * job_owner.size(), hipMemcpyHostToDevice);
-  }
 #ifdef PQ_STAMPS
   rc |= alloc_dev((void **)&B->d_dbg, sizeof(uint64_t) * std::max(8 * 4 * (B->tiles.size() + 1), 4 * (npages + 1)));
   rc |= alloc_dev((void **)&B->d_dbg2, sizeof(uint64_t) * (16 * (npages + 1) + 256));  // + k_snappy_walk stamps
@@ -1974,9 +2038,11 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     }
     hipMemsetAsync(B->d_in + in_bytes, 0, kPad, ctx->upload);
     B->h2d_bytes += (int64_t)in_bytes;
-    if (hipEventCreateWithFlags(&B->ready, hipEventDisableTiming) != hipSuccess ||
-        hipEventRecord(B->ready, ctx->upload) != hipSuccess) {
-      set_err("hipEventRecord failed");
+    for (auto &f : tab_fix) *f.first = B->d_in + tab_off + f.second;
+    hipMemsetAsync(B->d_info, 0, sizeof(PageInfo) * npages, ctx->upload);
+    hipMemsetAsync(B->d_recs, 0, sizeof(ExRec) * (B->tiles.size() + 1), ctx->upload);
+    if (hipEventCreateWithFlags(&B->ready, hipEventDisableTiming) != hipSuccess) {
+      set_err("hipEventCreate failed");
       return PQG_ERR_DEVICE;
     }
   }
@@ -1984,28 +2050,6 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     HIPCHK(hipMemcpy(B->d_stage + hb.first, hb.second.data(), hb.second.size(), hipMemcpyHostToDevice));
     B->h2d_bytes += (int64_t)hb.second.size();
   }
-  if (npages) HIPCHK(hipMemcpy(B->d_pages, B->pages.data(), sizeof(PageDesc) * npages, hipMemcpyHostToDevice));
-  // pages that fail before k_prepare contribute zero counts to the scans
-  if (npages) HIPCHK(hipMemset(B->d_info, 0, sizeof(PageInfo) * npages));
-  B->ngen_flat = (int32_t)B->general_flat.size();
-  B->general_list.insert(B->general_list.end(), B->general_flat.begin(), B->general_flat.end());
-  B->general_flat.clear();
-  B->ngen_str = (int32_t)B->general_str.size();
-  B->general_list.insert(B->general_list.end(), B->general_str.begin(), B->general_str.end());
-  B->general_str.clear();
-  B->ngen_nest = (int32_t)B->general_nest.size();
-  B->general_list.insert(B->general_list.end(), B->general_nest.begin(), B->general_nest.end());
-  B->general_nest.clear();
-  {
-    std::vector<int32_t> lists;
-    lists.insert(lists.end(), B->snappy_list.begin(), B->snappy_list.end());
-    lists.insert(lists.end(), B->dict_list.begin(), B->dict_list.end());
-    lists.insert(lists.end(), B->data_list.begin(), B->data_list.end());
-    lists.insert(lists.end(), B->general_list.begin(), B->general_list.end());
-    lists.insert(lists.end(), B->dba_list.begin(), B->dba_list.end());
-    if (!lists.empty()) HIPCHK(hipMemcpy(B->d_lists, lists.data(), sizeof(int32_t) * lists.size(), hipMemcpyHostToDevice));
-  }
-  if (npages) HIPCHK(hipMemcpy(B->d_status0, B->status0.data(), sizeof(uint32_t) * npages, hipMemcpyHostToDevice));
   phase("upload");
 
   // column descriptors (outputs allocated after the counting pass)
@@ -2027,12 +2071,14 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     c.total_levels = cp.levels;
   }
   const bool any_count = B->any_count;
+  // every set-up copy is queued on the upload stream behind the chunk bytes
+  // (from host memory the batch keeps): batch creation never waits for the
+  // DMA engine, and each decode waits on `ready`
+  B->hcols0 = B->hcols;  // hcols changes after the counting pass
   if (!B->cols.empty())
-    HIPCHK(hipMemcpy(B->d_cols, B->hcols.data(), sizeof(ColDesc) * B->cols.size(), hipMemcpyHostToDevice));
-  // the set-up copies and memsets above ran on the null stream, which the
-  // non-blocking context stream does not wait for (only the null stream is
-  // waited for: another thread may be decoding on this device meanwhile)
-  HIPCHK(hipStreamSynchronize(nullptr));
+    HIPCHK(hipMemcpyAsync(B->d_cols, B->hcols0.data(), sizeof(ColDesc) * B->cols.size(), hipMemcpyHostToDevice,
+                          ctx->upload));
+  HIPCHK(hipEventRecord(B->ready, ctx->upload));
   if (any_count) {
     // counting pass: snappy + prepare + scan once to size list/string outputs
     rc = launch_all(B, true, false);
@@ -2102,7 +2148,8 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   }
   if (rc) return PQG_ERR_DEVICE;
   if (!B->cols.empty())
-    HIPCHK(hipMemcpy(B->d_cols, B->hcols.data(), sizeof(ColDesc) * B->cols.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpyAsync(B->d_cols, B->hcols.data(), sizeof(ColDesc) * B->cols.size(), hipMemcpyHostToDevice,
+                          ctx->upload));
   // k_expand jobs: output pointers now that the outputs exist
   for (TileJob &tj : B->tiles) {
     if (tj.page < 0) continue;  // an unused slot
@@ -2112,9 +2159,10 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     tj.out = c.values + d.level_base * (int64_t)c.width;
   }
   if (!B->tiles.empty())
-    HIPCHK(hipMemcpy(B->d_tiles, B->tiles.data(), sizeof(TileJob) * B->tiles.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpyAsync(B->d_tiles, B->tiles.data(), sizeof(TileJob) * B->tiles.size(), hipMemcpyHostToDevice,
+                          ctx->upload));
   {  // the validity bitmaps k_reset zeroes in every decode
-    std::vector<ZeroRange> zr;
+    std::vector<ZeroRange> &zr = B->zr_host;
     for (auto &cp : B->cols) {
       if (cp.validity) zr.push_back({(uint32_t *)cp.validity, cp.validity_bytes / 4});
       if (cp.list_validity) zr.push_back({(uint32_t *)cp.list_validity, cp.list_val_bytes / 4});
@@ -2125,10 +2173,10 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
         set_err("device allocation failed");
         return PQG_ERR_DEVICE;
       }
-      HIPCHK(hipMemcpy(B->d_zr, zr.data(), sizeof(ZeroRange) * zr.size(), hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpyAsync(B->d_zr, zr.data(), sizeof(ZeroRange) * zr.size(), hipMemcpyHostToDevice, ctx->upload));
     }
   }
-  HIPCHK(hipStreamSynchronize(nullptr));  // null-stream set-up done before the first decode on the context stream
+  HIPCHK(hipEventRecord(B->ready, ctx->upload));  // decodes wait for every set-up copy
   phase("outputs+tables");
   return PQG_OK;
 }
@@ -2567,19 +2615,14 @@ void pqg_batch_destroy(pqg_batch *B) {
     free_dev(cp.rep_out);
   }
   free_dev(B->d_in_alloc);
-  free_dev(B->d_stage);
-  free_dev(B->d_pages);
   free_dev(B->d_info);
+  free_dev(B->d_recs);
+  free_dev(B->d_stage);
   free_dev(B->d_status);
   free_dev(B->d_cols);
   free_dev(B->d_dict);
-  free_dev(B->d_lists);
   free_dev(B->d_jobs);
   free_dev(B->d_njobs);
-  free_dev(B->d_job_base);
-  free_dev(B->d_job_owner);
-  free_dev(B->d_copy_cnt);
-  free_dev(B->d_status0);
   free_dev(B->d_zr);
   free_dev(B->d_copy_idx);
   free_dev(B->d_lens);
@@ -2589,14 +2632,7 @@ void pqg_batch_destroy(pqg_batch *B) {
   free_dev(B->d_runs);
   free_dev(B->d_tile_info);
   free_dev(B->d_tiles);
-  free_dev(B->d_recs);
-  free_dev(B->d_page_jobs);
-  free_dev(B->d_lgroups);
-  free_dev(B->d_sitems);
-  free_dev(B->d_seg_base);
-  free_dev(B->d_walk);
   free_dev(B->d_segs);
-  free_dev(B->d_seg_flag);
   if (B->ready) hipEventDestroy(B->ready);
   for (int k = 0; k < pqg_batch::kRing; k++)
     for (int i = 0; i < 8; i++)
@@ -2616,22 +2652,31 @@ struct pqg_stream {
   std::vector<pqg_batch *> built;  // per slice, set by the worker
   std::vector<int> rcs;
   std::vector<std::string> errs;
-  size_t nbuilt = 0, ntaken = 0;
-  bool stop = false;
+  std::vector<char> done;     // per slice: built (or failed)
+  size_t next_build = 0;      // next slice a worker takes
+  size_t ntaken = 0;
+  bool stop = false, failed = false;
   std::mutex mu;
   std::condition_variable cv;
-  std::thread worker;
+  std::vector<std::thread> workers;
   pqg_batch *cur = nullptr;  // the slice last handed out
 };
 
+// Several workers build slices concurrently (host planning, allocation and
+// table set-up of different slices overlap; the pinned-ring uploads take
+// turns on the context's upload stream), each taking the next slice index
+// while at most `depth` slices are built ahead of the one the caller holds.
 static void stream_worker(pqg_stream *S) {
   hipSetDevice(S->ctx->device);
-  for (size_t k = 0; k < S->slices.size(); k++) {
+  for (;;) {
+    size_t k;
     {
       std::unique_lock<std::mutex> lk(S->mu);
-      // at most `depth` slices built ahead of the one the caller holds
-      S->cv.wait(lk, [&] { return S->stop || k < S->ntaken + (size_t)S->depth; });
-      if (S->stop) return;
+      S->cv.wait(lk, [&] {
+        return S->stop || S->failed || S->next_build >= S->slices.size() || S->next_build < S->ntaken + (size_t)S->depth;
+      });
+      if (S->stop || S->failed || S->next_build >= S->slices.size()) return;
+      k = S->next_build++;
     }
     pqg_batch *B = nullptr;
     const int rc = pqg_batch_create(S->ctx, S->f, S->slices[k].first, S->slices[k].second,
@@ -2639,10 +2684,12 @@ static void stream_worker(pqg_stream *S) {
     std::lock_guard<std::mutex> lk(S->mu);
     S->built[k] = B;
     S->rcs[k] = rc;
-    if (rc) S->errs[k] = g_err;  // the worker's thread-local message
-    S->nbuilt = k + 1;
+    if (rc) {
+      S->errs[k] = g_err;  // the worker's thread-local message
+      S->failed = true;    // no slice after a failed one is started
+    }
+    S->done[k] = 1;
     S->cv.notify_all();
-    if (rc) return;  // the stream ends at a slice that failed to plan
   }
 }
 
@@ -2669,7 +2716,10 @@ int pqg_stream_open(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const i
   S->built.assign(S->slices.size(), nullptr);
   S->rcs.assign(S->slices.size(), 0);
   S->errs.assign(S->slices.size(), std::string());
-  S->worker = std::thread(stream_worker, S);
+  S->done.assign(S->slices.size(), 0);
+  const char *w = getenv("PQG_STREAM_WORKERS");
+  const int nw = std::max(1, std::min({w ? atoi(w) : 3, depth, (int)std::max<size_t>(1, S->slices.size())}));
+  for (int i = 0; i < nw; i++) S->workers.emplace_back(stream_worker, S);
   *out = S;
   return PQG_OK;
 }
@@ -2686,7 +2736,12 @@ int pqg_stream_next(pqg_stream *S, pqg_batch **out, int *rg_first) {
     std::unique_lock<std::mutex> lk(S->mu);
     k = S->ntaken;
     if (k >= S->slices.size()) return PQG_OK;
-    S->cv.wait(lk, [&] { return S->nbuilt > k; });
+    // a slice never started after an earlier one failed: the stream ends
+    S->cv.wait(lk, [&] { return S->done[k] || (S->failed && k >= S->next_build); });
+    if (!S->done[k]) {
+      S->ntaken = S->slices.size();
+      return PQG_OK;
+    }
     S->ntaken = k + 1;
     S->cv.notify_all();
     if (S->rcs[k]) {
@@ -2712,7 +2767,8 @@ void pqg_stream_close(pqg_stream *S) {
     S->stop = true;
     S->cv.notify_all();
   }
-  if (S->worker.joinable()) S->worker.join();
+  for (auto &t : S->workers)
+    if (t.joinable()) t.join();
   if (S->cur) pqg_batch_destroy(S->cur);
   for (pqg_batch *B : S->built)
     if (B) pqg_batch_destroy(B);

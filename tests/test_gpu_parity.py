@@ -244,6 +244,26 @@ def test_generated_dictionary_widths(bw):
                "dict bw%d" % bw)
 
 
+@pytest.mark.parametrize("bw", [13, 14, 15])
+def test_tiled_big_dictionary_groups(bw):
+    """k_expand_big: dictionaries of 2^13..2^15 entries copied once per
+    8-wave workgroup into LDS (PQG_BIG=1), INT32 and INT64 columns side by
+    side, against the oracle; and with the L1/L2 path (PQG_NO_BIG=1)."""
+    rng = np.random.default_rng(200 + bw)
+    K = 1 << bw
+    rows = 600000
+    d32 = rng.permutation(K).astype(np.int32) * 5 - 11
+    d64 = rng.permutation(K >> 1).astype(np.int64) * 0x1234567 - (1 << 35)
+    t = _req_table({"a": d32[rng.integers(0, K, rows)], "b": d64[rng.integers(0, K >> 1, rows)]})
+    data = _pq_bytes(t, compression="snappy", dictionary_pagesize_limit=1 << 30, row_group_size=300000)
+    for env in ("PQG_BIG", "PQG_NO_BIG"):
+        os.environ[env] = "1"
+        try:
+            check_file(data, "big dict bw%d %s" % (bw, env))
+        finally:
+            del os.environ[env]
+
+
 def test_generated_nullable_mix():
     pa = pytest.importorskip("pyarrow")
     rng = np.random.default_rng(11)
