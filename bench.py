@@ -259,7 +259,7 @@ def segment_times(reader, rg0, rg1, decodes=6):
         b.close()
 
 
-def e2e_rates(reader, rg0, rg1, stats, slices=24, depth=4):
+def e2e_rates(reader, rg0, rg1, stats, slice_counts=(4, 8, 24), depth=4):
     """PCIe-inclusive rates (never `value`): the whole shard read through
     pqg_stream — the host worker plans and uploads slice k + 1 (pinned ring,
     PQG_UPLOAD_THREADS gather threads) while the GPU decodes slice k — timed
@@ -281,16 +281,27 @@ def e2e_rates(reader, rg0, rg1, stats, slices=24, depth=4):
             pcie = best
             hip.hipFree(dbuf)
         hip.hipHostFree(hbuf)
-    per = max(1, (rg1 - rg0 + slices - 1) // slices)
-    best = None
-    for _ in range(2):  # the first pass also maps the file pages
-        t = time.perf_counter()
-        with reader.stream(rg0, rg1, per, None, depth) as st:
-            for b in st:
-                b.sync()
-        t = time.perf_counter() - t
-        best = t if best is None else min(best, t)
-    out = {"stream_ms": round(best * 1e3, 2), "stream_rgs_per_slice": per, "stream_depth": depth,
+    # slice sizes: small slices overlap more upload with decode; batches with
+    # strings / lists pay a counting pass per slice whose time is set by their
+    # longest pages, so they want few slices — the best of a few is reported
+    best, per_best, tried = None, None, {}
+    for slices in slice_counts:
+        per = max(1, (rg1 - rg0 + slices - 1) // slices)
+        if per in tried:
+            continue
+        bt = None
+        for _ in range(2):  # the first pass also maps the file pages
+            t = time.perf_counter()
+            with reader.stream(rg0, rg1, per, None, depth) as st:
+                for b in st:
+                    b.sync()
+            t = time.perf_counter() - t
+            bt = t if bt is None else min(bt, t)
+        tried[per] = round(bt * 1e3, 2)
+        if best is None or bt < best:
+            best, per_best = bt, per
+    out = {"stream_ms": round(best * 1e3, 2), "stream_rgs_per_slice": per_best, "stream_depth": depth,
+           "stream_ms_by_rgs_per_slice": tried,
            "GBps_stream_incl_plan_and_h2d": round(stats["output_bytes"] / best / 1e9, 1),
            "h2d_bytes": n}
     if pcie:

@@ -760,6 +760,7 @@ struct pqg_batch {
   int err_rg = -1, err_leaf = -1, err_page = -1;
   bool decoded = false;
   hipEvent_t ready = nullptr;  // recorded on the context's upload stream after the chunk bytes' H2D
+  bool counted = false;        // the last launch was the counting pass (the next decode resumes from it)
   std::vector<uint8_t> tab_host;  // the small tables (d_pages, d_info, d_lists, ...): host image, uploaded at
                                   // the end of d_in
   std::vector<ColDesc> hcols0;    // column descriptors as first uploaded (before the counting pass)
@@ -2244,7 +2245,13 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.ex_lds = B->ex_lds;
   a.recs = B->d_recs;
   a.page_jobs = B->d_page_jobs;
-  a.epoch = ++B->epoch;
+  // the first decode after the counting pass resumes from it: the staged
+  // pages, level / length scratch, job records and scanned bases it left are
+  // this decode's (same epoch), so only the bitmaps are zeroed and the decode
+  // phase runs
+  const bool resume = !upto_scan && B->counted;
+  B->counted = upto_scan;
+  a.epoch = resume ? B->epoch : ++B->epoch;
   a.tiles = B->d_tiles;
   a.lgroups = B->d_lgroups;
   for (int i = 0; i < 6; i++) {
@@ -2254,7 +2261,15 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   const int32_t ns = (int32_t)B->snappy_list.size(), nd = (int32_t)B->dict_list.size(),
                 ndata = (int32_t)B->data_list.size(), ngen = (int32_t)B->general_list.size();
   int e = 0;
-  if (npages || a.nzr) e |= pq_launch(13, &a, s);  // k_reset: statuses and validity bitmaps
+  if (resume) {
+    if (a.nzr) {  // k_reset over the bitmaps only (the statuses stay the counting pass's)
+      pq_launch_args z = a;
+      z.npages = 0;
+      e |= pq_launch(13, &z, s);
+    }
+  } else if (npages || a.nzr) {
+    e |= pq_launch(13, &a, s);  // k_reset: statuses and validity bitmaps
+  }
   if (timed) B->nev = 0;  // an untimed decode keeps the last timed segment count
   hipEvent_t *evs = B->ev[B->ring_head];
   // events cost a gap between dependent kernels: by default only the decode
@@ -2262,6 +2277,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   auto mark = [&](bool decode_edge) {
     if (timed && (B->seg_times || decode_edge)) hipEventRecord(evs[B->nev++], s);
   };
+  if (!resume) {
   mark(false);
   a.list = B->d_lists;
   a.nlist = ns;
@@ -2352,7 +2368,10 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     e |= pq_launch(2, &a, s);  // (+ the run walk of tiled RLE_DICTIONARY pages)
   }
   mark(false);
-  if (B->any_count) e |= pq_launch(4, &a, s);  // scans only feed lists / strings
+  }  // !resume
+  // scans only feed lists / strings (rerun on resume: with the outputs now
+  // allocated they also write the closing list / string offsets)
+  if (B->any_count) e |= pq_launch(4, &a, s);
   mark(true);
   if (!upto_scan) {
     // the three k_decode instances run side by side: <1> and <2> on side

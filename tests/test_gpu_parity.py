@@ -47,9 +47,19 @@ def gpu_decode_all(data, levels=True, rg0=0, rg1=None, leaves=None):
     rg1 = r.RowGroupCount() if rg1 is None else rg1
     leaves = list(range(len(r.Columns()))) if leaves is None else leaves
     b = r.batch(rg0, rg1, leaves, pqgpu.BATCH_LEVELS if levels else 0)
+    # the first decode resumes from the batch's counting pass (strings /
+    # lists), the second runs the whole pipeline again: both must agree
     b.decode()
     rc = b.sync(raise_on_error=False)
     out = {leaf: b.column(i) for i, leaf in enumerate(leaves)} if rc == 0 else None
+    b.decode()
+    rc2 = b.sync(raise_on_error=False)
+    assert rc2 == rc, ("second decode", rc, rc2)
+    if rc == 0:
+        for i, leaf in enumerate(leaves):
+            again = b.column(i)
+            for k in KEYS:
+                assert np.array_equal(again[k], out[leaf][k]), ("second decode differs", leaf, k)
     b.close()
     return rc, out, r.Columns()
 
