@@ -97,6 +97,7 @@ constexpr int LD_MIX_MAX = 32 * 1024;     // k_expand_mix LDS per workgroup with
 // its own launch (the dynamic LDS size is per launch)
 constexpr int BIG_WAVES = 8;
 constexpr int BIG_JOBS = 16;              // jobs per group (default; PQG_BIG_JOBS)
+constexpr int PLAIN_STR_ITEM = 2048;      // k_plain_str: values per work item
 struct LdsGroup {
   int32_t job0, njobs;   // jobs [job0, job0 + njobs) of the launch order
   int32_t dpage;         // the chunk's dictionary page; -1: one job per wave, L1/L2 gathers

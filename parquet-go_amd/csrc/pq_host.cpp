@@ -703,6 +703,7 @@ struct pqg_batch {
   std::vector<int32_t> general_nest;  // k_decode<3> pages (lists of fixed-width values), appended last
   int32_t ngen_flat = 0, ngen_str = 0, ngen_nest = 0;
   std::vector<int32_t> dba_list;      // DELTA_BYTE_ARRAY pages: value bytes by k_dba
+  std::vector<int32_t> pstr_items;    // k_plain_str: (page, first value) pairs of flat required PLAIN strings
   bool data_may_defer = false;        // some data page's Snappy body may hold a deferred literal
   std::vector<TileJob> tiles;         // k_expand work list (XCD-affine order)
   int64_t run_entries = 0, tile_entries = 0;
@@ -1636,6 +1637,15 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
       const bool nest_fw = L.max_rep > 0 && (L.value_width == 4 || L.value_width == 8) &&
                            L.physical_type != T_BYTE_ARRAY && L.physical_type != T_BOOLEAN &&
                            !(cp.flags & COL_EMIT_LEVELS);
+      static const bool pstr_off = getenv("PQG_NO_PLAIN_STR") != nullptr;
+      if (flat_ba && L.max_def == 0 && d.enc == ENC_PLAIN && d.lens_base >= 0 && !pstr_off) {
+        // several waves per page (k_plain_str) over k_prepare's (offset, length) scratch
+        for (int32_t v = 0; v < std::max(d.num_values, 0); v += PLAIN_STR_ITEM) {
+          B->pstr_items.push_back(pi);
+          B->pstr_items.push_back(v);
+        }
+        continue;
+      }
       (flat_fw   ? B->general_flat
        : flat_ba ? B->general_str
        : nest_fw ? B->general_nest
@@ -1955,6 +1965,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     lists.insert(lists.end(), B->data_list.begin(), B->data_list.end());
     lists.insert(lists.end(), B->general_list.begin(), B->general_list.end());
     lists.insert(lists.end(), B->dba_list.begin(), B->dba_list.end());
+    lists.insert(lists.end(), B->pstr_items.begin(), B->pstr_items.end());
     // the small tables: one host image (256-byte aligned entries; the
     // zero-initialised ones are zeros in it) and one copy instead of a
     // synchronous copy or memset each (tens of µs apiece)
@@ -2378,7 +2389,9 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     // streams forked here, joined before anything reads their output
     const int32_t ng0 = ngen - B->ngen_flat - B->ngen_str - B->ngen_nest;
     pqg_ctx *ctx = B->ctx;
-    const bool fork = B->ngen_flat > 0 || B->ngen_str > 0 || B->ngen_nest > 0;
+    const int32_t npstr = (int32_t)(B->pstr_items.size() / 2);
+    const bool str_side = B->ngen_str > 0 || npstr > 0;
+    const bool fork = B->ngen_flat > 0 || str_side || B->ngen_nest > 0;
     if (fork) hipEventRecord(ctx->fork, s);
     if (B->ngen_flat > 0) {
       hipStreamWaitEvent(ctx->side[0], ctx->fork, 0);
@@ -2387,8 +2400,13 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
       e |= pq_launch(14, &a, ctx->side[0]);  // k_decode<1>: flat fixed-width pages
       hipEventRecord(ctx->join[0], ctx->side[0]);
     }
-    if (B->ngen_str > 0) {
+    if (str_side) {
       hipStreamWaitEvent(ctx->side[1], ctx->fork, 0);
+      if (npstr > 0) {  // k_plain_str: flat required PLAIN string pages, items of PLAIN_STR_ITEM values
+        a.list = B->d_lists + ns + nd + ndata + ngen + (int32_t)B->dba_list.size();
+        a.nlist = npstr;
+        e |= pq_launch(23, &a, ctx->side[1]);
+      }
       a.list = B->d_lists + ns + nd + ndata + ng0 + B->ngen_flat;
       a.nlist = B->ngen_str;
       e |= pq_launch(15, &a, ctx->side[1]);  // k_decode<2>: flat BYTE_ARRAY pages
@@ -2404,7 +2422,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     a.list = B->d_lists + ns + nd + ndata;
     a.nlist = ng0;
     e |= pq_launch(3, &a, s);  // k_decode<0>: lists of strings, booleans, level output
-    if (B->ngen_str > 0) hipStreamWaitEvent(s, ctx->join[1], 0);
+    if (str_side) hipStreamWaitEvent(s, ctx->join[1], 0);
     if (!B->dba_list.empty()) {  // DELTA_BYTE_ARRAY value bytes (after k_decode's offsets)
       a.list = B->d_lists + ns + nd + ndata + ngen;
       a.nlist = (int32_t)B->dba_list.size();

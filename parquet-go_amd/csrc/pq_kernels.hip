@@ -2500,6 +2500,159 @@ __device__ __forceinline__ void copy_str(const uint8_t *sp, uint8_t *op, int64_t
   }
 }
 
+// ===========================================================================
+// k_plain_str: flat required PLAIN BYTE_ARRAY pages (type_bytearray.go:13-55)
+// in items of PS_ITEM values, several waves per page.  k_prepare's length walk
+// validated the page's chain and left each value's (offset, length) in the
+// page's scratch; the chain is contiguous ([u32 len][bytes] per value), so the
+// output position of value i inside the page is offset_i - 4 (i + 1) and any
+// item can start on its own (k_decode<2> walks a page with one wave).  Item
+// list: (page, first value) pairs.
+// ===========================================================================
+constexpr int PS_ITEM = PLAIN_STR_ITEM;
+constexpr int PS_STAGE = 10240;  // staged source bytes per wave and step (longer steps: per-lane copies)
+__global__ __launch_bounds__(256) void k_plain_str(KArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t st_all[4][PS_STAGE / 4 + 8];
+  __shared__ int32_t ob_all[4][257];
+  const int wv = (int)ufirst(threadIdx.x >> 6);
+  const int gi = blockIdx.x * 4 + wv;
+  if (gi >= a.nlist) return;
+  const int lane = lane_id();
+  const int page = ufirst(a.list[2 * gi]);
+  const int32_t v0 = ufirst(a.list[2 * gi + 1]);
+  if (page_status(a.status, page) != STATUS_OK) return;
+  const PageDesc d = a.pages[page];
+  const ColDesc c = a.cols[d.col];
+  const PageInfo pi = a.info[page];
+  const int32_t n = max(d.num_values, 0);
+  const int32_t v1 = min(v0 + PS_ITEM, n);
+  const uint8_t *vals = body_ptr(a, d, page) + pi.val_off;
+  const int64_t vlen = pi.val_len, sb = pi.str_base;
+  const int32_t *SO = a.lens + d.lens_base, *SL = SO + n;
+  const int64_t slot0 = d.level_base;
+  uint32_t *st = st_all[wv];
+  int32_t *ob = ob_all[wv];
+  const uint8_t *stb = (const uint8_t *)st;
+  for (int32_t r = v0; r < v1; r += 256) {
+    // value r + 64 k + lane: page-relative output offset out = offset - 4 (i + 1)
+    const int32_t ns = min(256, v1 - r);
+    int64_t o[4], l[4], out[4];
+    bool oob = false;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int32_t i = r + 64 * k + lane;
+      o[k] = l[k] = out[k] = 0;
+      if (i < v1) {
+        o[k] = (uint32_t)SO[i];
+        l[k] = (uint32_t)SL[i];
+        out[k] = o[k] - 4 * (int64_t)(i + 1);
+        // the walk validated the chain: a pair outside the values section or
+        // the page's output is stale scratch (never trusted for the copies)
+        oob |= out[k] < 0 || o[k] + l[k] > vlen || out[k] + l[k] > pi.str_bytes;
+      }
+    }
+    if (ballot(oob)) {
+      set_status(a.status, page, ST_VALUES, E_EOF);
+      return;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int32_t i = r + 64 * k + lane;
+      if (i < v1) c.str_offsets[slot0 + i + 1] = sb + out[k] + l[k];
+    }
+    // the step's output range from its first and last values (wave-uniform loads)
+    const int32_t last = r + ns - 1;
+    const int64_t P0 = (int64_t)(uint32_t)SO[r] - 4 * (int64_t)(r + 1);
+    const int64_t P1 = (int64_t)(uint32_t)SO[last] + (int64_t)(uint32_t)SL[last] - 4 * (int64_t)(last + 1);
+    const int64_t span = P1 - P0 + 4 * (int64_t)ns;  // source bytes: lengths + strings
+    const uintptr_t src0 = (uintptr_t)(vals + (P0 + 4 * (int64_t)r));  // value r's length prefix
+    const uintptr_t A = src0 & ~(uintptr_t)15;
+    const int sh = (int)(src0 - A);
+#ifdef PQ_PSTR_NOSTAGE
+    if (false) {
+#else
+    if (span + sh + 16 <= PS_STAGE) {
+#endif
+#ifdef PQ_PSTR_DEBUG
+      if (lane == 0)
+        printf("PSTR page %d v0 %d r %d ns %d P0 %lld P1 %lld span %lld sh %d sb %lld\n", page, v0, r, ns, (long long)P0,
+               (long long)P1, (long long)span, sh, (long long)sb);
+#endif
+      // 1. the step's source bytes into LDS (16-byte loads; the readable pad
+      //    covers the last chunk) and the values' output starts
+      for (int64_t off = 16 * (int64_t)lane; off < span + sh; off += 1024)
+        *(uint4 *)(st + off / 4) = *(const uint4 *)(A + off);
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (64 * k + lane < ns) ob[64 * k + lane] = (int32_t)(out[k] - P0);
+      if (lane == 0) ob[ns] = 0x7fffffff;
+      wave_lds_sync();
+      // 2. output dwords by their own lanes, 16 bytes a lane a pass, aligned to
+      //    the output buffer: byte p (step-relative) of value v is staged byte
+      //    p + 4 (v + 1) + sh.  Value of a byte: the last value starting at or
+      //    before it (empty values share their successor's start)
+      uint8_t *obase = c.values + sb;
+      const int64_t q0 = (int64_t)(((uintptr_t)(obase + P0)) & ~(uintptr_t)15) - (int64_t)(uintptr_t)obase;  // page-relative
+      const int32_t len = (int32_t)(P1 - P0);
+      for (int64_t q = q0 + 16 * (int64_t)lane; q < P1; q += 1024) {
+        const int32_t pr0 = (int32_t)(q - P0);  // step-relative start of this chunk (may be < 0)
+        // binary search: last v with ob[v] <= max(pr0, 0)
+        const int32_t key = max(pr0, 0);
+        int lo = 0, hi = ns;  // ob[lo] <= key < ob[hi]
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (ob[mid] <= key) lo = mid;
+          else hi = mid;
+        }
+        int v = lo;
+        int32_t nxt = ob[v + 1];
+        uint32_t w4[4];
+        bool full = pr0 >= 0 && pr0 + 16 <= len;
+#pragma unroll
+        for (int dw = 0; dw < 4; dw++) {
+          const int32_t p = pr0 + 4 * dw;
+          uint32_t x = 0;
+          if (p >= 0 && p + 3 < len) {
+            while (nxt <= p) nxt = ob[++v + 1];
+            if (nxt > p + 3) {  // four bytes of one value: an unaligned staged dword
+              const int32_t idx = p + 4 * (v + 1) + sh;
+              x = __builtin_amdgcn_alignbyte(st[(idx >> 2) + 1], st[idx >> 2], (uint32_t)(idx & 3));
+            } else {
+              for (int b = 0; b < 4; b++) {
+                while (nxt <= p + b) nxt = ob[++v + 1];
+                x |= (uint32_t)stb[p + b + 4 * (v + 1) + sh] << (8 * b);
+              }
+            }
+          } else {
+            for (int b = 0; b < 4; b++) {
+              const int32_t pb = p + b;
+              if (pb < 0 || pb >= len) continue;
+              while (nxt <= pb) nxt = ob[++v + 1];
+              x |= (uint32_t)stb[pb + 4 * (v + 1) + sh] << (8 * b);
+            }
+          }
+          w4[dw] = x;
+        }
+        if (full) {
+          *(uint4 *)(obase + q) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        } else {  // a step's edge chunk: only its own bytes (the neighbours' are another step's)
+          for (int b = 0; b < 16; b++) {
+            const int32_t pb = pr0 + b;
+            if (pb >= 0 && pb < len) obase[q + b] = (uint8_t)(w4[b >> 2] >> (8 * (b & 3)));
+          }
+        }
+      }
+      wave_lds_sync();
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int32_t i = r + 64 * k + lane;
+        if (i < v1) copy_str(vals + o[k], c.values + sb + out[k], l[k]);
+      }
+    }
+  }
+}
+
 // Decode one data page with one wavefront, 256 level entries per step, four
 // consecutive entries per lane (page_v1.go:27-55 readValues + data_store.go
 // semantics for validity / list offsets).  For flat columns the steps are
@@ -3939,6 +4092,7 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     case 16: hipLaunchKernelGGL(pq::k_decode<3>, grid, block, 0, s, k); break;
     case 5: hipLaunchKernelGGL(pq::k_level_check, grid, block, 0, s, k); break;
     case 10: hipLaunchKernelGGL(pq::k_dba, grid, block, 0, s, k); break;
+    case 23: hipLaunchKernelGGL(pq::k_plain_str, grid, block, 0, s, k); break;
     default: return 1;
   }
   return hipGetLastError() == hipSuccess ? 0 : 17;

@@ -76,13 +76,17 @@ def check_file(data, ctx, rg0=0, rg1=None):
             key = (e.rg, leaf)
             if first_err is None or key < first_err[0]:
                 first_err = (key, e.code)
-    rc, got, cols = gpu_decode_all(data, True, rg0, rg1)
-    if first_err is not None:
-        assert rc == first_err[1], (ctx, rc, first_err)
-        return
-    assert rc == 0, (ctx, rc, pqgpu.last_error())
-    for leaf, info in enumerate(o.leaves()):
-        assert_same(got[leaf], exp[leaf], info["max_def"], info["max_rep"], "%s leaf %d" % (ctx, leaf))
+    # with level output (k_decode<0> for every page) and without it (the
+    # routes a reader takes: tiled pages, k_decode<1..3>, k_plain_str)
+    for levels in (True, False):
+        rc, got, cols = gpu_decode_all(data, levels, rg0, rg1)
+        if first_err is not None:
+            assert rc == first_err[1], (ctx, levels, rc, first_err)
+            continue
+        assert rc == 0, (ctx, levels, rc, pqgpu.last_error())
+        for leaf, info in enumerate(o.leaves()):
+            assert_same(got[leaf], exp[leaf], info["max_def"], info["max_rep"],
+                        "%s leaf %d levels=%s" % (ctx, leaf, levels))
 
 
 def fixture_names():
@@ -406,6 +410,61 @@ def test_stream_slices_match_oracle(tmp_path, per, depth):
                                 "%s stream slice %d leaf %d" % (ctx, b.rg0, leaf))
                 seen.append(b.rg0)
         assert seen == list(range(0, o.num_row_groups, per)), (ctx, seen)
+
+
+@pytest.mark.parametrize("maxlen", [0, 3, 20, 60, 300])
+def test_plain_required_strings_items(maxlen):
+    """k_plain_str: flat required PLAIN BYTE_ARRAY pages of many items (several
+    waves per page), short strings (steps staged in LDS and copied by output
+    dword) and long ones (per-value copies), empty strings, against the oracle."""
+    pa = pytest.importorskip("pyarrow")
+    rng = np.random.default_rng(300 + maxlen)
+    rows = 30000
+    lens = rng.integers(0, maxlen + 1, rows)
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789", np.uint8)
+    offs = np.zeros(rows + 1, np.int32)
+    offs[1:] = np.cumsum(lens)
+    data = alpha[rng.integers(0, len(alpha), int(offs[-1]))]
+    arr = pa.StringArray.from_buffers(rows, pa.py_buffer(offs.tobytes()), pa.py_buffer(data.tobytes()))
+    t = pa.table({"s": arr}, schema=pa.schema([pa.field("s", pa.string(), nullable=False)]))
+    for comp in ("snappy", "none"):
+        check_file(_pq_bytes(t, compression=comp, use_dictionary=False, row_group_size=12000,
+                             data_page_size=1 << 20), "plain strings maxlen %d %s" % (maxlen, comp))
+
+
+def test_c5_small_row_groups(tmp_path):
+    """C5 shape with 10k-row row groups: l_comment's RLE_DICTIONARY pages then a
+    PLAIN page of several k_plain_str items, whole file and single row groups."""
+    pytest.importorskip("pyarrow")
+    data = _c5_bytes(tmp_path, 70000, 10000, dictionary_pagesize_limit=64 << 10)
+    check_file(data, "c5 10k rg0", 0, 1)
+    check_file(data, "c5 10k")
+
+
+def test_two_live_batches_resume(tmp_path):
+    """Two batches of one file alive together (as a stream holds them), the
+    second created before the first is decoded: each decode bit-exact."""
+    pytest.importorskip("pyarrow")
+    data = _c5_bytes(tmp_path, 70000, 10000, dictionary_pagesize_limit=64 << 10)
+    o = oracle.File(data)
+    r = pqgpu.FileReader(data)
+    leaves = list(range(len(r.Columns())))
+    b0 = r.batch(0, 1, leaves)
+    b1 = r.batch(1, 2, leaves)
+    errs = []
+    for b, rg in ((b0, 0), (b1, 1), (b0, 0)):
+        b.decode()
+        assert b.sync(raise_on_error=False) == 0
+        for i, leaf in enumerate(leaves):
+            info = o.leaves()[leaf]
+            try:
+                assert_same(b.column(i), o.decode(leaf, rg, rg + 1), info["max_def"], info["max_rep"],
+                            "two batches rg %d leaf %d" % (rg, leaf))
+            except AssertionError as e:
+                errs.append(str(e))
+    assert not errs, errs
+    b0.close()
+    b1.close()
 
 
 def test_stream_reports_slice_errors():
