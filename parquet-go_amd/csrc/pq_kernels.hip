@@ -2510,7 +2510,7 @@ __device__ __forceinline__ void copy_str(const uint8_t *sp, uint8_t *op, int64_t
 // list: (page, first value) pairs.
 // ===========================================================================
 constexpr int PS_ITEM = PLAIN_STR_ITEM;
-constexpr int PS_STAGE = 10240;  // staged source bytes per wave and step (longer steps: per-lane copies)
+constexpr int PS_STAGE = 8192;  // staged source bytes per wave and step (longer steps: per-lane copies)
 __global__ __launch_bounds__(256) void k_plain_str(KArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t st_all[4][PS_STAGE / 4 + 8];
   __shared__ int32_t ob_all[4][257];
