@@ -1745,6 +1745,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     };
     std::vector<LdG> ldg;
     std::vector<std::vector<TileJob>> bins(8);
+    std::vector<const std::vector<TileJob> *> gchunks;  // chunks gathering through L1/L2
     for (const auto &ct : chunk_tiles) {
       if (ct.empty() || B->cols[(size_t)B->pages[(size_t)ct[0].page].col].info.value_width != W) continue;
       bool ld = false;
@@ -1781,11 +1782,46 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
           B->pages[(size_t)ct[0].dict].alias_any = 1;
         }
       }
-      if (!ld) {
+      if (!ld) gchunks.push_back(&ct);
+    }
+    // L1/L2 chunks to the 8 XCD residues.  A chunk whose dictionary is large
+    // (> PQG_XCD_SPLIT_KB, default 1 MiB) stays whole on one XCD (two such
+    // dictionaries would not share one 4 MiB L2); the others are then poured
+    // into the least-loaded residues, split at job boundaries where a residue
+    // fills up (their dictionaries are then cached by two L2s), so every XCD
+    // gets the same number of L2-bound jobs (PQG_XCD_SPLIT_KB=0: whole chunks
+    // only, least loaded first)
+    {
+      static const int64_t split_max = getenv("PQG_XCD_SPLIT_KB") ? 1024 * (int64_t)atoi(getenv("PQG_XCD_SPLIT_KB"))
+                                                                  : (int64_t)1 << 20;
+      auto dict_bytes_of = [&](const std::vector<TileJob> &ct) {
+        return ct[0].dict >= 0 ? (int64_t)std::max(B->pages[(size_t)ct[0].dict].num_values, 0) * W : 0;
+      };
+      std::vector<const std::vector<TileJob> *> whole, split;
+      for (auto *ct : gchunks) (split_max > 0 && dict_bytes_of(*ct) <= split_max ? split : whole).push_back(ct);
+      auto least = [&]() {
         size_t best = 0;
         for (size_t q = 1; q < 8; q++)
           if (bins[q].size() < bins[best].size()) best = q;
-        bins[best].insert(bins[best].end(), ct.begin(), ct.end());
+        return best;
+      };
+      for (auto *ct : whole) {
+        const size_t q = least();
+        bins[q].insert(bins[q].end(), ct->begin(), ct->end());
+      }
+      size_t total = 0;
+      for (auto &v : bins) total += v.size();
+      for (auto *ct : split) total += ct->size();
+      const size_t target = (total + 7) / 8;
+      for (auto *ct : split) {
+        size_t k = 0;
+        while (k < ct->size()) {
+          const size_t q = least();
+          const size_t room = bins[q].size() < target ? target - bins[q].size() : ct->size() - k;
+          const size_t take = std::min(room, ct->size() - k);
+          bins[q].insert(bins[q].end(), ct->begin() + (std::ptrdiff_t)k, ct->begin() + (std::ptrdiff_t)(k + take));
+          k += take;
+        }
       }
     }
     size_t maxlen = 0, gjobs = 0, ljobs = 0;
