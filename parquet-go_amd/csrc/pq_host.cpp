@@ -21,6 +21,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <cmath>
 #include <condition_variable>
 #include <functional>
 #include <map>
@@ -1799,27 +1800,33 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
       };
       std::vector<const std::vector<TileJob> *> whole, split;
       for (auto *ct : gchunks) (split_max > 0 && dict_bytes_of(*ct) <= split_max ? split : whole).push_back(ct);
+      // a job of a whole (large-dictionary) chunk weighs PQG_XCD_WHOLE_W jobs
+      // of the split ones (its gathers miss L2 more often)
+      static const double ww = getenv("PQG_XCD_WHOLE_W") ? atof(getenv("PQG_XCD_WHOLE_W")) : 1.0;
+      double load[8] = {};
       auto least = [&]() {
         size_t best = 0;
         for (size_t q = 1; q < 8; q++)
-          if (bins[q].size() < bins[best].size()) best = q;
+          if (load[q] < load[best]) best = q;
         return best;
       };
+      double total = 0;
+      for (auto *ct : whole) total += ww * (double)ct->size();
+      for (auto *ct : split) total += (double)ct->size();
       for (auto *ct : whole) {
         const size_t q = least();
         bins[q].insert(bins[q].end(), ct->begin(), ct->end());
+        load[q] += ww * (double)ct->size();
       }
-      size_t total = 0;
-      for (auto &v : bins) total += v.size();
-      for (auto *ct : split) total += ct->size();
-      const size_t target = (total + 7) / 8;
+      const double target = total / 8;
       for (auto *ct : split) {
         size_t k = 0;
         while (k < ct->size()) {
           const size_t q = least();
-          const size_t room = bins[q].size() < target ? target - bins[q].size() : ct->size() - k;
-          const size_t take = std::min(room, ct->size() - k);
+          const double room = load[q] < target ? std::ceil(target - load[q]) : (double)(ct->size() - k);
+          const size_t take = std::min((size_t)std::max(room, 1.0), ct->size() - k);
           bins[q].insert(bins[q].end(), ct->begin() + (std::ptrdiff_t)k, ct->begin() + (std::ptrdiff_t)(k + take));
+          load[q] += (double)take;
           k += take;
         }
       }
