@@ -2275,9 +2275,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
 // k_prepare and k_decode then read the counts and levels instead of the
 // streams.  MODE as k_prepare (-1 every page, 0 / 1 pages that do not / do
 // wait on k_copy).
-template <int MODE>
+template <int MODE, bool SPLIT>
 __global__ __launch_bounds__(256) void k_levels(KArgs a) {
-  const int gi = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
+  // SPLIT (batches with repeated columns): two waves per page — the
+  // repetition and the definition streams are independent (each its own run
+  // chain) and are decoded side by side; errors meet in the page status
+  // (atomicMin: ST_REP before ST_DEF, the reference's order).  Otherwise one
+  // wave per page decodes both in turn.
+  const int wv = (int)ufirst(threadIdx.x >> 6);
+  const int gi = SPLIT ? blockIdx.x * 2 + (wv >> 1) : blockIdx.x * 4 + wv;
+  const int part = SPLIT ? (wv & 1) : 2;  // 0: repetition levels, 1: definition levels, 2: both
   if (gi >= a.nlist) return;
   const int lane = lane_id();
   const int page = ufirst(a.list[gi]);
@@ -2298,27 +2305,30 @@ __global__ __launch_bounds__(256) void k_levels(KArgs a) {
     return;
   }
   const int n = d.num_values;
-  Hyb rep, def;
-  rep.init(ps.lvl + ps.rep_off, ps.rep_len, bits_len(c.max_rep));
-  def.init(ps.lvl + ps.def_off, ps.def_len, bits_len(c.max_def));
   uint8_t *lv = a.lvl + d.lvl_base;
-  int64_t rows = 0, slots = 0, nn = 0, unused = 0;
-  if (c.max_rep > 0) {
+  if (part != 1 && c.max_rep > 0) {
+    Hyb rep;
+    rep.init(ps.lvl + ps.rep_off, ps.rep_len, bits_len(c.max_rep));
+    int64_t rows = 0, unused = 0;
     e = rep.count2(n, 0u, 0xffffffffu, rows, unused, lv);
     if (e) {
       set_status(a.status, page, ST_REP, e);
       return;
     }
-    lv += n;
+    if (lane == 0) a.info[page].rows = rows;
   }
+  if (part == 0) return;
+  Hyb def;
+  def.init(ps.lvl + ps.def_off, ps.def_len, bits_len(c.max_def));
+  int64_t slots = 0, nn = 0;
+  if (c.max_rep > 0) lv += n;
   e = def.count2(n, (uint32_t)c.max_def, c.max_rep > 0 ? (uint32_t)c.rep_def : 0u, nn, slots, lv);
   if (e) {
     set_status(a.status, page, ST_DEF, e);
     return;
   }
-  if (c.max_rep == 0) rows = n;
   if (lane == 0) {
-    a.info[page].rows = rows;
+    if (c.max_rep == 0) a.info[page].rows = n;
     a.info[page].slots = slots;
     a.info[page].non_null = nn;
   }
@@ -4083,9 +4093,13 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     case 1: hipLaunchKernelGGL(pq::k_dict_prepare, grid, block, 0, s, k); break;
     case 2: hipLaunchKernelGGL(pq::k_prepare<-1>, grid, block, 0, s, k); break;
     case 11: hipLaunchKernelGGL(pq::k_prepare<1>, grid, block, 0, s, k); break;
-    case 19: hipLaunchKernelGGL(pq::k_levels<-1>, grid, block, 0, s, k); break;
-    case 20: hipLaunchKernelGGL(pq::k_levels<0>, grid, block, 0, s, k); break;
-    case 21: hipLaunchKernelGGL(pq::k_levels<1>, grid, block, 0, s, k); break;
+    case 19: hipLaunchKernelGGL((pq::k_levels<-1, false>), grid, block, 0, s, k); break;
+    case 20: hipLaunchKernelGGL((pq::k_levels<0, false>), grid, block, 0, s, k); break;
+    case 21: hipLaunchKernelGGL((pq::k_levels<1, false>), grid, block, 0, s, k); break;
+    // two waves a page (batches with repeated columns)
+    case 24: hipLaunchKernelGGL((pq::k_levels<-1, true>), dim3((k.nlist + 1) / 2), block, 0, s, k); break;
+    case 25: hipLaunchKernelGGL((pq::k_levels<0, true>), dim3((k.nlist + 1) / 2), block, 0, s, k); break;
+    case 26: hipLaunchKernelGGL((pq::k_levels<1, true>), dim3((k.nlist + 1) / 2), block, 0, s, k); break;
     case 3: hipLaunchKernelGGL(pq::k_decode<0>, grid, block, 0, s, k); break;
     case 14: hipLaunchKernelGGL(pq::k_decode<1>, grid, block, 0, s, k); break;
     case 15: hipLaunchKernelGGL(pq::k_decode<2>, grid, block, 0, s, k); break;
