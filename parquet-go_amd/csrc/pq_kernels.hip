@@ -2578,16 +2578,7 @@ __global__ __launch_bounds__(256) void k_plain_str(KArgs a) {
     const uintptr_t src0 = (uintptr_t)(vals + (P0 + 4 * (int64_t)r));  // value r's length prefix
     const uintptr_t A = src0 & ~(uintptr_t)15;
     const int sh = (int)(src0 - A);
-#ifdef PQ_PSTR_NOSTAGE
-    if (false) {
-#else
     if (span + sh + 16 <= PS_STAGE) {
-#endif
-#ifdef PQ_PSTR_DEBUG
-      if (lane == 0)
-        printf("PSTR page %d v0 %d r %d ns %d P0 %lld P1 %lld span %lld sh %d sb %lld\n", page, v0, r, ns, (long long)P0,
-               (long long)P1, (long long)span, sh, (long long)sb);
-#endif
       // 1. the step's source bytes into LDS (16-byte loads; the readable pad
       //    covers the last chunk) and the values' output starts
       for (int64_t off = 16 * (int64_t)lane; off < span + sh; off += 1024)
