@@ -2350,7 +2350,12 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     // pages defer literals to k_copy (after the join).
     const int32_t nall = (int32_t)(B->snap_items.size() / 2), nwhole = B->n_whole_items, ndict = B->n_dict_items;
     pqg_ctx *ctx = B->ctx;
-    const bool side = (nall > nwhole || nd > 0) && !B->seg_times;
+    // without segmented pages or string dictionaries to prepare, the whole
+    // data pages and the dictionary pages are one launch on the context
+    // stream (items [0, nwhole + ndict) are contiguous): the fork / join
+    // around a side stream cost ~10 us of gaps per decode (C2)
+    const bool one = B->walk_list.empty() && nd == 0 && nall == nwhole + ndict;
+    const bool side = !one && (nall > nwhole || nd > 0) && !B->seg_times;
     // the serial chain (walk -> segments -> ...) goes on the context stream,
     // dispatched first, and the whole data pages on the side stream: a chain
     // on the side stream was dispatched after the whole pages had taken the
@@ -2365,26 +2370,32 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
       hipEventRecord(ctx->fork, s);
       hipStreamWaitEvent(ctx->side[0], ctx->fork, 0);
     }
-    e |= pq_launch(17, &a, ss);  // k_snappy_walk
-    if (!walk_side) {
+    if (one) {
+      a.nitems = nwhole + ndict;
+      e |= pq_launch(0, &a, s);  // k_snappy: every page (whole data pages, then dictionary pages)
+    }
+    if (!one) e |= pq_launch(17, &a, ss);  // k_snappy_walk
+    if (!walk_side && !one) {
       a.nitems = nwhole;
       e |= pq_launch(0, &a, sw);  // k_snappy: whole data pages (side stream)
     }
     pq_launch_args aw = a;
-    aw.sitems = B->d_sitems + 2 * (size_t)(nwhole + ndict);
-    aw.nitems = nall - nwhole - ndict;
-    e |= pq_launch(0, &aw, ss);  // k_snappy: segments
-    e |= pq_launch(18, &a, ss);  // serial fallback for pages whose segments did not decode alone
-    aw.sitems = B->d_sitems + 2 * (size_t)nwhole;
-    aw.nitems = ndict;
-    e |= pq_launch(0, &aw, ss);  // k_snappy: whole dictionary pages
+    if (!one) {
+      aw.sitems = B->d_sitems + 2 * (size_t)(nwhole + ndict);
+      aw.nitems = nall - nwhole - ndict;
+      e |= pq_launch(0, &aw, ss);  // k_snappy: segments
+      e |= pq_launch(18, &a, ss);  // serial fallback for pages whose segments did not decode alone
+      aw.sitems = B->d_sitems + 2 * (size_t)nwhole;
+      aw.nitems = ndict;
+      e |= pq_launch(0, &aw, ss);  // k_snappy: whole dictionary pages
+    }
     if (side) {
       aw = a;
       aw.list = B->d_lists + ns;
       aw.nlist = nd;
       e |= pq_launch(1, &aw, ss);  // k_dict_prepare (its pages are all decoded on this stream)
     }
-    if (walk_side) {
+    if (walk_side && !one) {
       a.nitems = nwhole;
       e |= pq_launch(0, &a, sw);  // k_snappy: whole data pages
     }
