@@ -1201,8 +1201,8 @@ struct HostBuf {  // the device input buffer's layout: byte ranges of the (mappe
   };
   std::vector<Range> ranges;
   size_t n = 0;
-  size_t append(const uint8_t *src, size_t k, size_t align = 16) {
-    const size_t off = (n + align - 1) & ~(align - 1);
+  size_t append(const uint8_t *src, size_t k, size_t align = 16, size_t phase = 0) {
+    const size_t off = ((n + align - 1) & ~(align - 1)) + phase;
     ranges.push_back({src, off, k});
     n = off + k;
     return off;
@@ -1327,8 +1327,29 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
     count += h.compressed;
     ord++;
   }
-  // upload the chunk bytes once
-  size_t base = in.append(f->data + chunk_lo, (size_t)(chunk_hi - chunk_lo));
+  // upload the chunk bytes once.  A chunk with a dictionary page is placed
+  // so that the dictionary's values start 16-byte aligned: uncompressed, its
+  // payload; Snappy, the data of its first literal (an incompressible
+  // dictionary is one literal, which k_snappy then leaves in place instead of
+  // copying it, and L1/L2 gathers read it aligned)
+  size_t phase = 0;
+  if (!walked.empty() && walked[0].h.type == 2 && (C.codec == PQG_CODEC_UNCOMPRESSED || device_codec)) {
+    int64_t h = 0;
+    const int64_t p0 = walked[0].payload, pend = std::min<int64_t>(p0 + walked[0].h.compressed, (int64_t)f->len);
+    if (device_codec) {  // varint decoded length, then the tag (+ 1..4 length bytes for literals >= 61 bytes)
+      int64_t q = p0;
+      while (q < pend && (f->data[q] & 0x80)) q++;
+      q++;
+      if (q < pend && (f->data[q] & 3) == 0) {
+        const uint32_t x = f->data[q] >> 2;
+        h = (q - p0) + 1 + (x >= 60 ? (int64_t)(x - 59) : 0);
+      } else {
+        h = -1;  // not a literal first: nothing to align
+      }
+    }
+    if (h >= 0 && p0 >= chunk_lo) phase = (size_t)((16 - ((p0 - chunk_lo + h) & 15)) & 15);
+  }
+  size_t base = in.append(f->data + chunk_lo, (size_t)(chunk_hi - chunk_lo), 16, phase);
   B->input_bytes += chunk_hi - chunk_lo;
 
   int32_t dict_idx = -1;
