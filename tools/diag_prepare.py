@@ -8,17 +8,16 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "parquet-go_amd"))
-sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+os.environ["PQGPU_LIB"] = "libpqgpu_diag.so"
 import pqgpu  # noqa: E402
-
-pqgpu._LIB_PATH = os.path.join(ROOT, "parquet-go_amd", "libpqgpu_diag.so")
-import bench  # noqa: E402
+import synth  # noqa: E402
 
 bw = int(sys.argv[1])
 rows = int(sys.argv[2]) if len(sys.argv) > 2 else 20_000_000
 path = "/tmp/diag_bw%d_%d.parquet" % (bw, rows)
 if not os.path.exists(path):
-    bench.make_file(path, rows, 1 << 20, fixed_bw=bw)
+    synth.make("c2", path, rows, 1 << 20, fixed_bw=bw)
 b = pqgpu.FileReader(path).batch()
 for _ in range(3):
     b.decode()
