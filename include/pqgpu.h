@@ -121,6 +121,12 @@ typedef struct {
 } pqg_column_info;
 
 int pqg_file_open_path(const char *path, pqg_file **out);
+/* Many files' footers parsed in parallel (a dataset of
+ * many files before its row groups are sharded): out[i] is the opened file or
+ * NULL; returns the first failing file's status (its index in *failed) or
+ * PQG_OK.  threads <= 0: one per file up to the host's cores.  The reference
+ * opens one file per NewFileReader (file_reader.go:27, file_meta.go:14-62). */
+int pqg_file_open_many(const char *const *paths, int n, int threads, pqg_file **out, int *failed);
 /* `data` must stay valid while the file is open unless `copy` is nonzero. */
 int pqg_file_open_buffer(const uint8_t *data, size_t len, int copy, pqg_file **out);
 void pqg_file_close(pqg_file *f);

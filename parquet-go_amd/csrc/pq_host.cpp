@@ -21,6 +21,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <condition_variable>
 #include <functional>
@@ -1124,6 +1125,37 @@ int pqg_file_open_path(const char *path, pqg_file **out) {
     return rc;
   }
   *out = f;
+  return PQG_OK;
+}
+
+int pqg_file_open_many(const char *const *paths, int n, int threads, pqg_file **out, int *failed) {
+  if (failed) *failed = -1;
+  if (n < 0 || (n > 0 && (!paths || !out))) {
+    set_err("bad arguments");
+    return PQG_ERR_ARG;
+  }
+  for (int i = 0; i < n; i++) out[i] = nullptr;
+  std::vector<int> rcs((size_t)n, PQG_OK);
+  std::vector<std::string> errs((size_t)n);
+  int nt = threads > 0 ? threads : (int)std::max(1u, std::thread::hardware_concurrency());
+  nt = std::max(1, std::min(nt, n));
+  std::atomic<int> next{0};
+  auto work = [&] {
+    for (int i; (i = next.fetch_add(1)) < n;) {
+      rcs[(size_t)i] = pqg_file_open_path(paths[i], &out[i]);
+      if (rcs[(size_t)i]) errs[(size_t)i] = g_err;  // this thread's message
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; t++) th.emplace_back(work);
+  work();
+  for (auto &t : th) t.join();
+  for (int i = 0; i < n; i++)
+    if (rcs[(size_t)i]) {
+      if (failed) *failed = i;
+      set_err("%s: %s", paths[i], errs[(size_t)i].c_str());
+      return rcs[(size_t)i];
+    }
   return PQG_OK;
 }
 

@@ -56,7 +56,7 @@ EXPORTS = [
     "pqg_file_last_error", "pqg_batch_create", "pqg_batch_decode", "pqg_batch_sync",
     "pqg_batch_error_location", "pqg_batch_column", "pqg_batch_copy", "pqg_batch_stats_get",
     "pqg_batch_kernel_times", "pqg_batch_set_timing", "pqg_batch_destroy",
-    "pqg_stream_open", "pqg_stream_next", "pqg_stream_close",
+    "pqg_stream_open", "pqg_stream_next", "pqg_stream_close", "pqg_file_open_many",
 ]
 
 
@@ -135,6 +135,7 @@ def lib():
                 "pqg_stream_open": (i32, [vp, vp, i32, i32, P(ctypes.c_int), i32, i32, i32, i32, P(vp)]),
                 "pqg_stream_next": (i32, [vp, P(vp), P(ctypes.c_int)]),
                 "pqg_stream_close": (None, [vp]),
+                "pqg_file_open_many": (i32, [P(ctypes.c_char_p), i32, i32, P(vp), P(ctypes.c_int)]),
             }
             for name, (res, args) in sig.items():
                 fn = getattr(L, name)
@@ -480,6 +481,32 @@ class FileReader:
 
 def NewFileReader(source, *columns, **kw):
     return FileReader(source, *columns, **kw)
+
+
+def OpenFiles(paths, *columns, threads=0, **kw):
+    """FileReaders for many files, their footers parsed in parallel by the
+    library (pqg_file_open_many).  Raises on the first file that fails."""
+    n = len(paths)
+    arr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
+    hs = (ctypes.c_void_p * max(n, 1))()
+    failed = ctypes.c_int(-1)
+    rc = lib().pqg_file_open_many(arr, n, int(threads), hs, ctypes.byref(failed))
+    if rc != OK:
+        for i in range(n):
+            if hs[i]:
+                lib().pqg_file_close(hs[i])
+        raise PqgError(rc, last_error())
+    out = []
+    for i in range(n):
+        r = FileReader.__new__(FileReader)
+        r._h = ctypes.c_void_p(hs[i])
+        r._buf = None
+        r._ctx = kw.get("ctx")
+        r._device = kw.get("device", 0)
+        r.selected = r._select(columns)
+        r.row_group_position = 0
+        out.append(r)
+    return out
 
 
 def plan_row_group_shards(sizes, world):

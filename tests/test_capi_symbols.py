@@ -95,3 +95,21 @@ def test_column_selection_prefix():
 def test_malformed_files_error_not_crash(blob):
     with pytest.raises(pqgpu.PqgError):
         pqgpu.FileReader(blob)
+
+
+def test_open_many_footers_in_parallel(tmp_path):
+    """pqg_file_open_many: every golden file's footer parsed by a thread pool
+    agrees with the single-file open; a bad file reports its index."""
+    names = sorted(json.load(open(os.path.join(GOLDEN, "manifest.json"))))[:12]
+    paths = [os.path.join(GOLDEN, n + ".parquet") for n in names]
+    readers = pqgpu.OpenFiles(paths, threads=4)
+    for p, r in zip(paths, readers):
+        one = pqgpu.FileReader(p)
+        assert r.NumRows() == one.NumRows() and r.RowGroupCount() == one.RowGroupCount()
+        assert r.Columns() == one.Columns()
+        one.close()
+        r.close()
+    bad = tmp_path / "bad.parquet"
+    bad.write_bytes(b"PAR1" + b"\0" * 20 + b"PAR1")
+    with pytest.raises(pqgpu.PqgError):
+        pqgpu.OpenFiles(paths[:2] + [str(bad)])
