@@ -658,7 +658,13 @@ struct Delta {
     min_delta = md;
     if (pos + mb_count > len) return E_EOF;  // io.ReadFull of the widths
     int lane = lane_id();
-    uint32_t wv = lane < mb_count ? p[pos + lane] : 0u;
+    // the widths from the register window (usually resident after the
+    // varint): no global round trip of its own per block
+    uint32_t wv = 0u;
+    for (int q = 0; q < mb_count; q++) {
+      const uint32_t b = W.byte_at(p + pos + q);
+      if (lane == q) wv = b;
+    }
     pos += mb_count;
     uint32_t maxw = is32 ? 32u : 64u;
     if (ballot(lane < mb_count && wv > maxw)) return E_BITWIDTH;
@@ -703,10 +709,22 @@ struct Delta {
   }
 
   // four per lane: value j of the next n (<= 256) goes to lane j >> 2, element j & 3
+  // The step's miniblocks are walked first (headers only: each lane notes
+  // where its values' bits are), then every value is unpacked with all loads
+  // in flight together (one dependent round trip for the step, not one per
+  // miniblock).
+  template <bool BATCH = true>
   __device__ uint32_t next4(int n, uint64_t (&out)[4]) {
     const int lane = lane_id();
+    int32_t bk[4], wk[4];
+    int64_t mdk[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) out[k] = 0;
+    for (int k = 0; k < 4; k++) {
+      out[k] = 0;
+      bk[k] = -1;
+      wk[k] = 0;
+      mdk[k] = 0;
+    }
     if (position + n > total) return E_EOF;
     int got = 0;
     while (got < n) {
@@ -728,11 +746,24 @@ struct Delta {
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         int j = 4 * lane + k;
-        if (j >= got && j < got + take) out[k] = unpack_u64(p, len, bit0 + (int64_t)j * mb_w, mb_w) + (uint64_t)min_delta;
+        if (j >= got && j < got + take) {
+          if (BATCH) {
+            bk[k] = (int32_t)(bit0 + (int64_t)j * mb_w);  // pages < 256 MiB
+            wk[k] = mb_w;
+            mdk[k] = min_delta;
+          } else {  // fewer registers (a register-bound caller): unpacked here
+            out[k] = unpack_u64(p, len, bit0 + (int64_t)j * mb_w, mb_w) + (uint64_t)min_delta;
+          }
+        }
       }
       mb_vi += take;
       position += take;
       got += take;
+    }
+    if (BATCH) {
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (bk[k] >= 0) out[k] = unpack_u64(p, len, bk[k], wk[k]) + (uint64_t)mdk[k];
     }
     return E_OK;
   }

@@ -2660,7 +2660,7 @@ __global__ __launch_bounds__(256) void k_plain_str(KArgs a) {
 // aligned to 256 output slots so each lane owns a 16-byte-aligned slice of
 // the values and whole validity words.
 template <int KIND>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ? 5 : KIND == 2 ? 3 : KIND == 3 ? 4 : 1))) void k_decode(KArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ? 5 : KIND == 2 ? 3 : KIND == 3 ? 2 : 1))) void k_decode(KArgs a) {
   const int gi = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
   if (gi >= a.nlist) return;
   const int lane = lane_id();
@@ -2910,7 +2910,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
         sbase_ptr = dict_vals;
       } else if (KIND != 2 && d.enc == ENC_DELTA_BP) {
         uint64_t dv[4];
-        err = dz.next4(m, dv);
+        err = dz.template next4<KIND != 3>(m, dv);  // <3> is register-bound
         if (err) {
           err_stage = ST_VALUES;
           break;
