@@ -15,19 +15,25 @@ A "step" decodes every page of the rank's shard once.  For N > 1 the file holds
 N x 100M rows and each rank decodes a contiguous, byte-balanced slice of its
 row groups (pqgpu.plan_row_group_shards) on its own GPU: weak scaling, no
 collective on the data path; value = decoded bytes of all ranks / max-over-ranks
-time.  `--allgather` additionally times the optional column all-gather over
+time.  `--gpus N` without WORLD_SIZE in the environment starts the N rank
+processes itself (spawn_ranks); under torch.distributed.run WORLD_SIZE must
+equal N.  `--allgather` additionally times the optional column all-gather over
 RCCL (pqgather, never inside the timed steps).
 
 Besides the timed loop (rank 0, N = 1), outside the timed region:
   * every pipeline phase is timed with HIP events on a second batch of the
     same shard (PQG_SEGMENT_TIMES=1); the longest phase is `roofline`'s, with
     its own algorithmic bytes;
-  * a `rocprofv3 --kernel-trace --stats` child run gives per-kernel average
-    durations (`config.kernel_trace_us`; `roofline.kernel` = the longest kernel
-    of that phase) and two `--pmc` child runs give FETCH_SIZE / WRITE_SIZE per
-    kernel (`roofline.traffic` for the phase's kernels);
-  * one row group is decoded again and compared bit-exactly with the oracle;
-  * the CPU oracle decodes a bounded sample of the same file (cpu_baseline).
+  * a `rocprofv3 --kernel-trace --stats` child run gives per-kernel durations
+    and calls of its last CHILD_STEPS decode steps (`roofline.kernel` = the
+    longest kernel of that phase, `frac_from_trace` = the phase's bytes over
+    its kernels' traced time per step) and two `--pmc` child runs give
+    FETCH_SIZE / WRITE_SIZE per kernel per step (`roofline.traffic`: every
+    dispatch of the phase's kernels in a step);
+  * every row group of the shard is decoded again and compared bit-exactly
+    with the oracle;
+  * the CPU oracle (and pyarrow, when importable) decodes a bounded sample of
+    the same file (cpu_baseline).
 
 Prints ONE JSON line (rank 0).
 """
@@ -172,9 +178,29 @@ def _child_cmd(args, steps=3):
     return cmd
 
 
+# every full decode ends with k_level_check (pq_host.cpp launch_all), and the
+# child's timed loop is the last thing it launches: the dispatches after the
+# (CHILD_STEPS + 1)-th last k_level_check are exactly CHILD_STEPS decode steps
+CHILD_STEPS = 3
+STEP_END = "k_level_check"
+
+
+def _last_steps(rows, key_id, key_name, steps=CHILD_STEPS):
+    """Rows of the last `steps` decode steps, in dispatch (host submission) order."""
+    rows = sorted(rows, key=lambda r: int(r[key_id]))
+    ends = [i for i, r in enumerate(rows) if _kname(r[key_name]) == STEP_END]
+    if len(ends) < steps + 1:
+        return None
+    return rows[ends[-steps - 1] + 1:ends[-1] + 1]
+
+
 def kernel_trace(args):
-    """Per-kernel average duration (us) and calls from a rocprofv3
-    --kernel-trace --stats child run of this same bench (None if unavailable)."""
+    """Per-kernel figures of the timed steps of a rocprofv3 --kernel-trace
+    --stats child run of this same bench: {kernel: {avg_us, calls_per_step,
+    us_per_step}} over the child's last CHILD_STEPS decode steps (None if
+    rocprofv3 is unavailable).  With PQG_BENCH_PROF_DIR the run's own
+    kernel_stats.csv, its per-dispatch kernel_trace.csv and the per-step
+    summary (rocprof_kernel_steps_<cfg>.csv) are kept there."""
     import csv
     import glob
     import shutil
@@ -184,29 +210,50 @@ def kernel_trace(args):
         return None
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
         cmd = ["timeout", "-s", "KILL", "150", "rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv",
-               "-d", td, "-o", "run", "--"] + _child_cmd(args)
+               "-d", td, "-o", "run", "--"] + _child_cmd(args, CHILD_STEPS)
         try:
             subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, check=True, timeout=180)
         except Exception:
             return None
-        out = {}
-        keep = os.environ.get("PQG_BENCH_PROF_DIR")  # keep the rocprofv3 summary (profiles/)
-        for f in glob.glob(os.path.join(td, "**", "*kernel_stats.csv"), recursive=True):
-            if keep:
-                os.makedirs(keep, exist_ok=True)
-                shutil.copy(f, os.path.join(keep, "rocprof_kernel_stats_%s.csv" % args.config))
-            for r in csv.DictReader(open(f)):
-                name = _kname(r["Name"])
-                out[name] = {"avg_us": float(r["AverageNs"]) / 1e3, "calls": int(r["Calls"])}
-        return out or None
+        keep = os.environ.get("PQG_BENCH_PROF_DIR")  # keep the rocprofv3 output (profiles/)
+        if keep:
+            os.makedirs(keep, exist_ok=True)
+            for pat, dst in (("*kernel_stats.csv", "rocprof_kernel_stats_%s.csv"),
+                             ("*kernel_trace.csv", "rocprof_kernel_trace_%s.csv")):
+                for f in glob.glob(os.path.join(td, "**", pat), recursive=True):
+                    shutil.copy(f, os.path.join(keep, dst % args.config))
+        rows = []
+        for f in glob.glob(os.path.join(td, "**", "*kernel_trace.csv"), recursive=True):
+            rows += list(csv.DictReader(open(f)))
+    step = _last_steps(rows, "Dispatch_Id", "Kernel_Name")
+    if not step:
+        return None
+    out = {}
+    for r in step:
+        k = out.setdefault(_kname(r["Kernel_Name"]), {"calls": 0, "ns": 0})
+        k["calls"] += 1
+        k["ns"] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    res = {k: {"avg_us": v["ns"] / v["calls"] / 1e3, "calls_per_step": v["calls"] / CHILD_STEPS,
+               "us_per_step": v["ns"] / CHILD_STEPS / 1e3} for k, v in out.items()}
+    if keep:
+        with open(os.path.join(keep, "rocprof_kernel_steps_%s.csv" % args.config), "w") as f:
+            f.write("# bench.py --config %s: the %d timed decode steps of the rocprofv3 --kernel-trace child run "
+                    "(dispatches after the %d-th last %s), per kernel\n" % (args.config, CHILD_STEPS,
+                                                                            CHILD_STEPS + 1, STEP_END))
+            f.write("Name,CallsPerStep,AverageNs,NsPerStep\n")
+            for k, v in sorted(res.items(), key=lambda kv: -kv[1]["us_per_step"]):
+                f.write("%s,%g,%.0f,%.0f\n" % (k, v["calls_per_step"], v["avg_us"] * 1e3, v["us_per_step"] * 1e3))
+    return res
 
 
 def pmc_traffic(args):
-    """HBM bytes per launch of every kernel from rocprofv3 PMC counters,
+    """HBM bytes per decode step of every kernel from rocprofv3 PMC counters,
     collected in separate passes (FETCH_SIZE, then WRITE_SIZE) over a short
-    child run of this same bench; MI355X_MICROARCH.md: on gfx950 FETCH_SIZE
-    reports half of a wide streaming read, so it is doubled.  Returns
-    {kernel: {"fetch": B, "write": B}} or None."""
+    child run of this same bench, summed over each kernel's dispatches in the
+    child's last CHILD_STEPS decode steps and divided by CHILD_STEPS.
+    MI355X_MICROARCH.md: on gfx950 FETCH_SIZE reports half of a wide streaming
+    read, so it is doubled.  Returns {kernel: {"fetch", "write",
+    "dispatches_per_step"}} (bytes per step) or None."""
     import csv
     import glob
     import shutil
@@ -215,26 +262,33 @@ def pmc_traffic(args):
     if not shutil.which("rocprofv3"):
         return None
     per = {}
+    keep = os.environ.get("PQG_BENCH_PROF_DIR")
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
             out = os.path.join(td, ctr)
             cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", ctr, "--output-format", "csv",
-                   "-d", out, "-o", "run", "--"] + _child_cmd(args)
+                   "-d", out, "-o", "run", "--"] + _child_cmd(args, CHILD_STEPS)
             try:
                 subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, check=True, timeout=150)
             except Exception:
                 return None
+            rows = []
             for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
-                for r in csv.DictReader(open(f)):
-                    if r["Counter_Name"] != ctr:
-                        continue
-                    name = _kname(r["Kernel_Name"])
-                    per.setdefault(name, {}).setdefault(ctr, []).append(float(r["Counter_Value"]) * 1024)
+                if keep:
+                    os.makedirs(keep, exist_ok=True)
+                    shutil.copy(f, os.path.join(keep, "rocprof_pmc_%s_%s.csv" % (ctr.lower(), args.config)))
+                rows += [r for r in csv.DictReader(open(f)) if r["Counter_Name"] == ctr]
+            step = _last_steps(rows, "Dispatch_Id", "Kernel_Name")
+            if not step:
+                return None
+            for r in step:
+                k = per.setdefault(_kname(r["Kernel_Name"]), {})
+                k.setdefault(ctr, []).append(float(r["Counter_Value"]) * 1024)  # kilobytes per dispatch
     res = {}
     for name, c in per.items():
         f, w = c.get("FETCH_SIZE", []), c.get("WRITE_SIZE", [])
-        # kilobytes per dispatch, averaged over the kernel's dispatches
-        res[name] = {"fetch": 2 * float(np.mean(f)) if f else 0.0, "write": float(np.mean(w)) if w else 0.0}
+        res[name] = {"fetch": 2 * sum(f) / CHILD_STEPS, "write": sum(w) / CHILD_STEPS,
+                     "dispatches_per_step": max(len(f), len(w)) / CHILD_STEPS}
     return res or None
 
 
@@ -264,21 +318,32 @@ def e2e_rates(reader, rg0, rg1, stats, slice_counts=(4, 8, 24), depth=8):
     pqg_stream — the host worker plans and uploads slice k + 1 (pinned ring,
     PQG_UPLOAD_THREADS gather threads) while the GPU decodes slice k — timed
     from opening the stream to the last slice's sync; beside it the bare PCIe
-    rate, one hipMemcpy of the shard's input bytes from pinned host memory."""
+    rates of the shard's input bytes from pinned host memory: one hipMemcpy,
+    and 16 MiB hipMemcpyAsync chunks queued back to back (the yardstick is
+    the faster of the two)."""
     hip = ctypes.CDLL("libamdhip64.so")
     n = int(stats["h2d_bytes"] or stats["input_bytes"])
-    hbuf, dbuf = ctypes.c_void_p(), ctypes.c_void_p()
-    pcie = None
+    hbuf, dbuf, strm = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+    pcie, pcie_chunked = None, None
     if hip.hipHostMalloc(ctypes.byref(hbuf), ctypes.c_size_t(n), 0) == 0:
         if hip.hipMalloc(ctypes.byref(dbuf), ctypes.c_size_t(n)) == 0:
             ctypes.memset(hbuf, 1, n)
-            best = None
+            hip.hipStreamCreate(ctypes.byref(strm))
+            chunk = 16 << 20
             for _ in range(3):
                 t = time.perf_counter()
                 hip.hipMemcpy(dbuf, hbuf, ctypes.c_size_t(n), 1)  # hipMemcpyHostToDevice
                 t = time.perf_counter() - t
-                best = t if best is None else min(best, t)
-            pcie = best
+                pcie = t if pcie is None else min(pcie, t)
+                # the same bytes as 16 MiB asynchronous copies queued back to back
+                t = time.perf_counter()
+                for off in range(0, n, chunk):
+                    hip.hipMemcpyAsync(ctypes.c_void_p(dbuf.value + off), ctypes.c_void_p(hbuf.value + off),
+                                       ctypes.c_size_t(min(chunk, n - off)), 1, strm)
+                hip.hipStreamSynchronize(strm)
+                t = time.perf_counter() - t
+                pcie_chunked = t if pcie_chunked is None else min(pcie_chunked, t)
+            hip.hipStreamDestroy(strm)
             hip.hipFree(dbuf)
         hip.hipHostFree(hbuf)
     # slice sizes: small slices overlap more upload with decode; batches with
@@ -307,35 +372,110 @@ def e2e_rates(reader, rg0, rg1, stats, slice_counts=(4, 8, 24), depth=8):
     if pcie:
         out["pcie_only_ms"] = round(pcie * 1e3, 2)
         out["pcie_only_GBps_in"] = round(n / pcie / 1e9, 1)
+        out["pcie_chunked_ms"] = round(pcie_chunked * 1e3, 2)
+        out["pcie_chunked_GBps_in"] = round(n / pcie_chunked / 1e9, 1)
         # the decoded-bytes rate a pure upload of the shard's input would allow
-        out["GBps_pcie_only_decoded_equiv"] = round(stats["output_bytes"] / pcie / 1e9, 1)
-        out["stream_vs_pcie_only"] = round(pcie / best, 3)
+        # (the faster of one copy and 16 MiB async chunks: the yardstick)
+        yard = min(pcie, pcie_chunked)
+        out["GBps_pcie_only_decoded_equiv"] = round(stats["output_bytes"] / yard / 1e9, 1)
+        out["stream_vs_pcie_only"] = round(yard / best, 3)
     return out
 
 
-def parity_check(reader, rg):
-    """Row group `rg` of the bench file decoded again on the GPU (outside the
-    timed region) and compared bit-exactly, buffer by buffer, with the oracle."""
+def parity_check(reader, rg0, rg1, threads):
+    """Every row group of the rank's shard decoded again on the GPU (one
+    batch per row group, outside the timed region) and compared bit-exactly,
+    buffer by buffer, with the oracle's decode of the same row group (oracle
+    decodes run on `threads` host threads ahead of the GPU comparisons)."""
+    import concurrent.futures as cf
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     cols = reader.Columns()
-    b = reader.batch(rg, rg + 1, list(range(len(cols))))
+    o = oracle.File(open(reader.path, "rb").read())
+    keys = ("values", "validity", "list_offsets", "list_validity", "str_offsets")
+
+    def want(rg):
+        return [o.decode(i, rg, rg + 1) for i in range(len(cols))]
+
+    ok, t0 = 0, time.perf_counter()
+    with cf.ThreadPoolExecutor(max(1, threads)) as ex:
+        pending = {}
+        nxt = rg0
+        for rg in range(rg0, rg1):
+            while nxt < rg1 and nxt < rg + 2 * max(1, threads):
+                pending[nxt] = ex.submit(want, nxt)
+                nxt += 1
+            b = reader.batch(rg, rg + 1, list(range(len(cols))))
+            try:
+                b.decode()
+                b.sync()
+                ref = pending.pop(rg).result()
+                for i, info in enumerate(cols):
+                    got = b.column(i)
+                    for k in keys:
+                        if k == "validity" and info["max_def"] == 0:
+                            continue
+                        if k in ("list_offsets", "list_validity") and info["max_rep"] != 1:
+                            continue
+                        if not np.array_equal(got[k], ref[i][k]):
+                            for f in pending.values():
+                                f.cancel()
+                            return "MISMATCH in row group %d leaf %s buffer %s" % (rg, info["name"], k)
+            finally:
+                b.close()
+            ok += 1
+    return "bit-exact vs oracle: %d/%d row groups of the shard, %d leaves, every buffer (%.1f s)" % (
+        ok, rg1 - rg0, len(cols), time.perf_counter() - t0)
+
+
+def pyarrow_baseline(path, cores, out_bytes, total_rows, budget_s=4.0):
+    """pq.read_table(use_threads=True) on the same file, row group by row
+    group until ~budget_s (an independent CPU decoder beside
+    the oracle port); decoded bytes counted as the GPU counts them (the
+    shard's B_out scaled by the rows read).  None without pyarrow."""
     try:
-        b.decode()
-        b.sync()
-        o = oracle.File(open(reader.path, "rb").read())
-        for i, info in enumerate(cols):
-            got, want = b.column(i), o.decode(i, rg, rg + 1)
-            for k in ("values", "validity", "list_offsets", "list_validity", "str_offsets"):
-                if k == "validity" and info["max_def"] == 0:
-                    continue
-                if k in ("list_offsets", "list_validity") and info["max_rep"] != 1:
-                    continue
-                if not np.array_equal(got[k], want[k]):
-                    return "MISMATCH in row group %d leaf %s buffer %s" % (rg, info["name"], k)
-        return "bit-exact vs oracle: row group %d, %d leaves, every buffer" % (rg, len(cols))
-    finally:
-        b.close()
+        import pyarrow as pa
+        import pyarrow.parquet as pq
+    except Exception:
+        return None
+    pa.set_cpu_count(cores)
+    pa.set_io_thread_count(cores)
+    pf = pq.ParquetFile(path)
+    n = pf.num_row_groups
+    rows, rgs, t0 = 0, 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        k = rgs % n
+        t = pf.read_row_groups([k], use_threads=True)
+        rows += t.num_rows
+        rgs += 1
+        del t
+    dt = time.perf_counter() - t0
+    return {"value": round(out_bytes * rows / total_rows / dt / 1e9, 3), "unit": "GB/s", "threads": cores,
+            "pyarrow": pa.__version__,
+            "sample": "ParquetFile.read_row_groups([rg], use_threads=True), %d row-group reads (%d rows), %.1f s"
+                      % (rgs, rows, dt)}
+
+
+def spawn_ranks(args):
+    """`bench.py --gpus N` without an external launcher: start N rank
+    processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set) before anything
+    touches the GPU, wait for all, and exit with the worst status.  Rank 0's
+    JSON line is the job's line."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    for p in procs:
+        rc = max(rc, abs(p.wait()))
+    return rc
 
 
 def main():
@@ -351,8 +491,12 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-prof", action="store_true", help="skip the rocprofv3 child runs (kernel trace, PMC)")
     ap.add_argument("--no-pmc", action="store_true", help="(compat) same as --no-prof")
+    ap.add_argument("--no-parity", action="store_true", help="skip the whole-shard oracle comparison")
     ap.add_argument("--child", action="store_true", help="internal: a profiled child run (timed loop only)")
     ap.add_argument("--allgather", action="store_true", help="N > 1: time the optional column all-gather (RCCL)")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="N > 1: process group backend for the barrier / max-time reduction (gloo: ranks may "
+                         "share a GPU, as in the CPU-box test)")
     ap.add_argument("--bw", type=int, default=0, help="analysis: one dictionary bit width for every row group")
     args = ap.parse_args()
     args.rows = args.rows or synth.DEFAULTS[args.config][0]
@@ -360,15 +504,24 @@ def main():
     if args.child:
         args.no_cpu = args.no_prof = True
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
+    if world != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    dist, device = None, 0
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        ndev = max(1, torch.cuda.device_count())  # counts devices without initialising HIP
+        device = local % ndev
+        if args.dist_backend == "nccl":
+            if local >= ndev:
+                sys.exit("bench.py: %d local ranks on %d GPUs need --dist-backend gloo" % (world, ndev))
+            torch.cuda.set_device(device)
+        dist.init_process_group(args.dist_backend)
 
     def barrier():
         if dist is not None:
@@ -382,7 +535,7 @@ def main():
         synth.make(args.config, path, total_rows, args.rg_rows, fixed_bw=args.bw)
     barrier()
 
-    ctx = pqgpu.Context(local if world > 1 else 0)
+    ctx = pqgpu.Context(device)
     reader = pqgpu.FileReader(path, ctx=ctx)
     reader.path = path
     sizes = [reader.RowGroupByteSize(i) for i in range(reader.RowGroupCount())]
@@ -403,9 +556,9 @@ def main():
     # the decode phase is bracketed by HIP events on a sample of the timed steps
     # (each event pair costs a few us of launch gap); at least 5 samples
     batch.set_timing(max(1, args.steps // 5))
-    barrier()
     hip = ctypes.CDLL("libamdhip64.so")
     hip.hipDeviceSynchronize()
+    barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -418,20 +571,21 @@ def main():
     job_out = out_b
     if dist is not None:
         import torch
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dev = torch.device("cuda", device) if args.dist_backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)  # the slowest rank sets the job time
         dt = float(t.item())
-        nb = torch.tensor([out_b], dtype=torch.float64, device="cuda")
+        nb = torch.tensor([out_b], dtype=torch.float64, device=dev)
         dist.all_reduce(nb, op=dist.ReduceOp.SUM)  # every rank's decoded bytes
         job_out = float(nb.item())
     per_step = dt / args.steps
     value = job_out * args.steps / dt / 1e9
 
     allgather = None
-    if dist is not None and args.allgather:
+    if dist is not None and args.allgather and args.dist_backend == "nccl":
         import torch
         import pqgather
-        dev = torch.device("cuda", local)
+        dev = torch.device("cuda", device)
         shard = pqgather.shard_tensors(batch, 0, dev)
         torch.cuda.synchronize(dev)
         barrier()
@@ -462,6 +616,7 @@ def main():
         "data": "synthetic (seeded pyarrow writer on the box, tools/synth.py %s)" % args.config,
         "config": {"workload": synth.DESCR[args.config] % (args.rows, args.rg_rows),
                    "rows_per_gpu": args.rows, "row_groups": [rg0, rg1],
+                   "job_B_out": job_out,
                    "pages": stats["data_pages"], "dict_pages": stats["dict_pages"],
                    "B_in": in_b, "B_out": out_b, "staged": stats["staged_bytes"],
                    "snappy_in": stats["snappy_in_bytes"],
@@ -469,7 +624,9 @@ def main():
                    # PCIe-inclusive rate (not `value`): host planning + H2D upload + one step
                    "e2e": {"batch_create_ms": round(t_create * 1e3, 2),
                            "GBps_incl_plan_and_h2d": round(out_b / (t_create + per_step) / 1e9, 1)},
-                   "parallelism": "row-group shards, one process per GPU, no data-path collective"},
+                   "parallelism": "row-group shards, one process per GPU, no data-path collective"
+                                  + ("" if world == 1 else " (%s for the barrier / time reduction)"
+                                     % args.dist_backend)},
     }
     if allgather:
         line["config"]["allgather"] = allgather
@@ -478,30 +635,46 @@ def main():
         line["config"]["phase_ms"] = {k: round(v, 4) for k, v in seg.items()}
         dom = max(seg, key=seg.get)
         ach = phase_bytes(dom, stats) / (seg[dom] * 1e-3) / 1e9
-        trace = None if args.no_prof or args.no_pmc else kernel_trace(args)
-        kern = dom
-        if trace:
-            line["config"]["kernel_trace_us"] = {k: round(v["avg_us"], 2) for k, v in
-                                                 sorted(trace.items(), key=lambda kv: -kv[1]["avg_us"])}
-            mine = {k: v for k, v in trace.items() if k.startswith(PHASE_KERNELS[dom])}
-            if mine:
-                kern = max(mine, key=lambda k: mine[k]["avg_us"])
-        line["roofline"] = {"bound": "hbm", "kernel": kern, "phase": dom, "phase_ms": round(seg[dom], 4),
+        # the dominant phase's roofline: live HIP events around the phase;
+        # beside it the same bytes over the phase's kernels' per-step time in
+        # the bench's own rocprofv3 trace (profiles/.../rocprof_kernel_steps_*)
+        line["roofline"] = {"bound": "hbm", "kernel": dom, "phase": dom, "phase_ms": round(seg[dom], 4),
                             "algorithmic_bytes": phase_bytes(dom, stats),
                             "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                             "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
                             "pipeline_frac": round((in_b + out_b) / per_step / 1e9 / HBM_PEAK_GBPS, 4)}
+        trace = None if args.no_prof or args.no_pmc else kernel_trace(args)
+        if trace:
+            line["config"]["kernel_trace_us_per_step"] = {
+                k: [round(v["us_per_step"], 2), v["calls_per_step"]]
+                for k, v in sorted(trace.items(), key=lambda kv: -kv[1]["us_per_step"])}
+            mine = {k: v for k, v in trace.items() if k.startswith(PHASE_KERNELS[dom])}
+            if mine:
+                kern = max(mine, key=lambda k: mine[k]["us_per_step"])
+                tsum = sum(v["us_per_step"] for v in mine.values())
+                line["roofline"].update({
+                    "kernel": kern, "kernel_avg_us": round(mine[kern]["avg_us"], 2),
+                    "kernel_calls_per_step": mine[kern]["calls_per_step"],
+                    "phase_kernels_us_per_step": round(tsum, 2),
+                    # equals `frac` when the phase is one kernel on one stream;
+                    # lower when its kernels overlap on side streams
+                    "frac_from_trace": round(phase_bytes(dom, stats) / (tsum * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)})
         if not (args.no_prof or args.no_pmc):
             pmc = pmc_traffic(args)
             if pmc:
-                line["config"]["pmc_MB_per_launch"] = {k: {"fetch": round(v["fetch"] / 1e6, 1),
-                                                           "write": round(v["write"] / 1e6, 1)}
-                                                       for k, v in sorted(pmc.items())}
+                line["config"]["pmc_MB_per_step"] = {k: {"fetch": round(v["fetch"] / 1e6, 1),
+                                                         "write": round(v["write"] / 1e6, 1),
+                                                         "dispatches": v["dispatches_per_step"]}
+                                                     for k, v in sorted(pmc.items())}
                 ks = [k for k in pmc if k.startswith(PHASE_KERNELS[dom])]
                 if ks:
-                    line["roofline"]["traffic"] = round(sum(pmc[k]["fetch"] + pmc[k]["write"] for k in ks) / 1e6, 1)
-                    line["roofline"]["traffic_unit"] = "MB per launch of the phase's kernels (FETCH_SIZE x 2 + WRITE_SIZE)"
-        line["config"]["parity"] = parity_check(reader, rg0)
+                    tr = sum(pmc[k]["fetch"] + pmc[k]["write"] for k in ks)
+                    line["roofline"]["traffic"] = round(tr / 1e6, 1)
+                    line["roofline"]["traffic_unit"] = ("MB per decode step, summed over every dispatch of the "
+                                                        "phase's kernels (FETCH_SIZE x 2 + WRITE_SIZE)")
+                    line["roofline"]["traffic_vs_algorithmic"] = round(tr / phase_bytes(dom, stats), 3)
+        if not args.no_parity:
+            line["config"]["parity"] = parity_check(reader, rg0, rg1, cpu_cores()[0])
         line["config"]["e2e"].update(e2e_rates(reader, rg0, rg1, stats))
     if "roofline" not in line:
         # N > 1: the decode phase, HIP events over the timed steps (per rank)
@@ -512,12 +685,19 @@ def main():
                                 "phase_ms": round(dms, 4), "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
                                 "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
                                 "pipeline_frac": round((in_b + out_b) / per_step / 1e9 / HBM_PEAK_GBPS, 4)}
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(path, args.cpu_budget)
+        pa_line = pyarrow_baseline(path, line["cpu_baseline"]["cores"], out_b, stats_rows(reader, rg0, rg1))
+        if pa_line:
+            line["cpu_baseline"]["pyarrow_read_table"] = pa_line
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def stats_rows(reader, rg0, rg1):
+    return sum(reader.RowGroupNumRows(i) for i in range(rg0, rg1))
 
 
 if __name__ == "__main__":

@@ -204,3 +204,81 @@ def test_gpu_shards_allgather(tmp_path, name, leaf, world):
         if k == "validity" and info["max_def"] == 0:
             continue
         assert np.array_equal(got[k].view(np.uint8).ravel(), whole[k]), k
+
+
+def _bench_line(tmp_path, gpus, path):
+    import json
+    import subprocess
+    env = dict(os.environ, TMPDIR=str(tmp_path))
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--config", "c1",
+                          "--rows", "300000", "--rg-rows", "50000", "--steps", "3", "--warmup", "1", "--file", path,
+                          "--no-prof", "--no-cpu", "--no-parity", "--dist-backend", "gloo"],
+                         env=env, capture_output=True, text=True, timeout=240, check=True)
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout + out.stderr
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_bench_gpus_2_spawns_two_ranks(tmp_path):
+    """`bench.py --gpus 2` without a launcher starts two rank processes
+    (sharing cuda:0 over gloo here; one GPU each over RCCL on a node): the
+    line reports n_gpus 2 and the job's decoded bytes equal a 1-rank run's."""
+    pytest.importorskip("pyarrow")
+    pytest.importorskip("torch")
+    path = str(tmp_path / "c1_small.parquet")
+    two = _bench_line(tmp_path, 2, path)
+    one = _bench_line(tmp_path, 1, path)
+    assert two["n_gpus"] == 2 and one["n_gpus"] == 1
+    assert two["config"]["job_B_out"] == one["config"]["job_B_out"] == one["config"]["B_out"]
+    assert 0 < two["config"]["B_out"] < one["config"]["B_out"]  # rank 0 decoded its shard only
+    assert two["value"] > 0
+
+
+def _gpu_rccl_main(rank, world, port, path, leaf, out_dir):
+    import torch
+    import torch.distributed as dist
+    sys.path[:0] = [os.path.join(ROOT, "parquet-go_amd")]
+    import pqgather
+    import pqgpu
+    torch.cuda.set_device(rank)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    r = pqgpu.FileReader(path)
+    sizes = [r.RowGroupByteSize(i) for i in range(r.RowGroupCount())]
+    rg0, rg1 = pqgpu.plan_row_group_shards(sizes, world)[rank]
+    b = r.batch(rg0, rg1, [leaf])
+    b.decode()
+    shard = pqgather.shard_tensors(b, 0, torch.device("cuda", rank))
+    b.close()
+    col = pqgather.allgather_column(shard)  # device tensors through RCCL
+    assert all(v.is_cuda for v in col.values() if hasattr(v, "is_cuda"))
+    col = pqgather.to_numpy(col)
+    if rank == 0:
+        np.savez(os.path.join(out_dir, "gathered.npz"), **{k: np.asarray(v) for k, v in col.items()})
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("name,leaf", [("c4_list_str", 0), ("c4_list_str", 1), ("c3_delta_v2", 1)])
+def test_gpu_allgather_rccl_device_tensors(tmp_path, name, leaf):
+    """allgather_column over RCCL on device tensors (one rank per GPU the box
+    has: RCCL does not put two ranks on one GPU); the gloo tests above cover
+    the re-packing at shard boundaries with more ranks."""
+    import torch
+    import torch.multiprocessing as mp
+    import oracle
+    world = max(1, torch.cuda.device_count())
+    path = os.path.join(GOLDEN, name + ".parquet")
+    mp.spawn(_gpu_rccl_main, args=(world, _free_port(), path, leaf, str(tmp_path)), nprocs=world, join=True)
+    got = np.load(str(tmp_path / "gathered.npz"))
+    o = oracle.File(open(path, "rb").read())
+    whole, info = o.decode(leaf), o.leaves()[leaf]
+    assert int(got["slots"]) == whole["slots"]
+    for k in ("values", "validity", "list_offsets", "list_validity", "str_offsets"):
+        if k == "validity" and info["max_def"] == 0:
+            continue
+        assert np.array_equal(got[k].view(np.uint8).ravel(), whole[k]), k
