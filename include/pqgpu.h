@@ -81,7 +81,13 @@ typedef struct pqg_batch pqg_batch;
 
 /* ---- context ----------------------------------------------------------- */
 int pqg_ctx_create(int device, pqg_ctx **out);
+/* Destroys the context and releases the device's idle cached buffers. */
 void pqg_ctx_destroy(pqg_ctx *ctx);
+/* Device buffers of destroyed batches are kept per device for reuse (at most
+   PQG_DEV_CACHE_MB, default min(1/8 of device memory, 8 GiB)); this frees the
+   idle ones of `device` (-1: every device) for other allocators.  No
+   reference counterpart (the Go reader allocates per page). */
+int pqg_release_cache(int device);
 /* HIP stream the context launches on (hipStream_t as void*). */
 void *pqg_ctx_stream(pqg_ctx *ctx);
 /* Copies the calling thread's / context's last error text into buf. */

@@ -928,7 +928,7 @@ typedef struct {
   struct {
     int32_t block_size, mb_count, values_count, mb_value_count;
     int64_t prev, min_delta;
-    uint8_t widths[256];
+    uint8_t *widths;        /* mb_count bytes of the current block */
     int32_t cur_mb;
     uint8_t cur_w;
     int32_t mb_pos, position;
@@ -949,11 +949,15 @@ static int delta_read_mb_header(page_reader *p) { /* :248-271 / :95-121 */
   if (p->dl_state.is32 && (md > 0x7fffffffLL || md < -0x80000000LL)) return PQR_ERR_DELTA;
   p->dl_state.min_delta = md;
   int32_t m = p->dl_state.mb_count;
-  if (m > 256) { /* widths buffer; more miniblocks than this is never produced */
-    uint8_t tmp;
-    for (int32_t i = 0; i < m; i++)
-      if (rd_full(&p->vr, &tmp, 1)) return PQR_ERR_EOF;
-    return PQR_ERR_UNSUPPORTED;
+  /* make([]uint8, miniBlockCount) + io.ReadFull: any count; a count past the
+     stream's end fails the read (allocated only when the bytes are there) */
+  if ((size_t)m > p->vr.n - p->vr.pos) {
+    p->vr.pos = p->vr.n;
+    return PQR_ERR_EOF;
+  }
+  if (!p->dl_state.widths) {
+    p->dl_state.widths = (uint8_t *)malloc((size_t)m);
+    if (!p->dl_state.widths) return PQR_ERR_DELTA;
   }
   if (rd_full(&p->vr, p->dl_state.widths, (size_t)m)) return PQR_ERR_EOF;
   int maxw = p->dl_state.is32 ? 32 : 64;
@@ -962,7 +966,12 @@ static int delta_read_mb_header(page_reader *p) { /* :248-271 / :95-121 */
   p->dl_state.cur_mb = 0;
   return 0;
 }
+static void delta_free(page_reader *p) {
+  free(p->dl_state.widths);
+  p->dl_state.widths = NULL;
+}
 static int delta_init(page_reader *p, int is32) { /* :197-246 */
+  delta_free(p);
   memset(&p->dl_state, 0, sizeof(p->dl_state));
   p->dl_state.is32 = is32;
   int32_t bs, mc, vc;
@@ -1134,7 +1143,7 @@ static int supported_value_encoding(const pqref_leaf *L, int enc, int has_dict) 
     case PQR_BYTE_ARRAY:
       return enc == ENC_PLAIN || enc == ENC_RLE_DICT || enc == ENC_DELTA_LBA || enc == ENC_DELTA_BA ? 0 : PQR_ERR_ENCODING;
     case PQR_FLBA:
-      return enc == ENC_PLAIN || enc == ENC_RLE_DICT ? 0 : enc == ENC_DELTA_BA ? PQR_ERR_UNSUPPORTED : PQR_ERR_ENCODING;
+      return enc == ENC_PLAIN || enc == ENC_RLE_DICT || enc == ENC_DELTA_BA ? 0 : PQR_ERR_ENCODING;
     case PQR_FLOAT:
     case PQR_DOUBLE:
     case PQR_INT96:
@@ -1169,8 +1178,11 @@ static int values_init(page_reader *p, const pqref_leaf *L) {
     return 0;
   }
   if (enc == ENC_DELTA_BP) return delta_init(p, L->physical_type == PQR_INT32);
-  if ((enc == ENC_DELTA_LBA || enc == ENC_DELTA_BA) && L->physical_type == PQR_BYTE_ARRAY) {
-    /* byteArrayDeltaDecoder.init :186-209 (prefix lengths, then the suffixes'
+  if ((enc == ENC_DELTA_LBA && L->physical_type == PQR_BYTE_ARRAY) ||
+      (enc == ENC_DELTA_BA && (L->physical_type == PQR_BYTE_ARRAY || L->physical_type == PQR_FLBA))) {
+    /* FIXED_LEN_BYTE_ARRAY DELTA_BYTE_ARRAY: the same byteArrayDeltaDecoder
+       (getFixedLenByteArrayValuesDecoder chunk_reader.go:86-96);
+       byteArrayDeltaDecoder.init :186-209 (prefix lengths, then the suffixes'
        DELTA_LENGTH stream); byteArrayDeltaLengthDecoder.init :98-108 */
     int e;
     if (enc == ENC_DELTA_BA) {
@@ -1289,7 +1301,17 @@ static int values_decode(page_reader *p, const pqref_leaf *L, const dictionary *
       if (pl > 0) bb_put(&v, p->prev.p, (size_t)pl);
       bb_put(&v, suffix, (size_t)size);
       len = (int64_t)v.n;
-      bb_put(&dp->lens, &len, 8);
+      if (L->physical_type == PQR_FLBA) {
+        /* a fixed-size slot holds type_length bytes: a value of another length
+           (the reference keeps it as a []byte) cannot be laid out -- the one
+           documented deviation */
+        if (len != (int64_t)w) {
+          free(v.p);
+          return PQR_ERR_BYTE_ARRAY;
+        }
+      } else {
+        bb_put(&dp->lens, &len, 8);
+      }
       bb_put(&dp->vals, v.p, v.n);
       free(p->prev.p);
       p->prev = v;
@@ -1647,6 +1669,7 @@ int pqref_decode(const pqref_file *f, int leaf, int rg0, int rg1, pqref_result *
       free(pages[i].pre);
       free(pages[i].suf);
       free(pages[i].prev.p);
+      delta_free(&pages[i]);
     }
     free(pages);
     free(dict.fixed);

@@ -638,15 +638,26 @@ struct Delta {
   const uint8_t *p;
   int64_t len, pos;
   int32_t block_size, mb_count, mbvc, total;
+  // the reference reads 8 values a group and starts a miniblock only where the
+  // value position is a multiple of both 8 and mbvc (:121-136): every adv =
+  // lcm(8, mbvc) values, all read at one width; adv == mbvc for the
+  // spec-conformant multiples of 8
+  int32_t adv;
   int64_t first, min_delta;
   int32_t cur_mb;       // miniblocks started in the current block
   int32_t mb_w;         // width of the current miniblock
   int64_t mb_data;      // first data byte of the current miniblock
-  int32_t mb_vi;        // values consumed in the current miniblock (== mbvc: exhausted)
+  int32_t mb_vi;        // values consumed in the current miniblock (== adv: exhausted)
+  int32_t mb_v0;        // value position where the current miniblock started
   int32_t position;     // deltas consumed
-  uint32_t widths;      // lane j: width of miniblock j of the current block
+  uint32_t widths;      // mb_count <= 64: lane j holds the width of miniblock j of the current block
+  int64_t wpos;         // mb_count > 64: stream offset of the current block's widths (read on demand)
   int32_t is32;
   Win W;
+
+  __device__ __forceinline__ int32_t width_of(int32_t j) {
+    return mb_count <= 64 ? (int32_t)__builtin_amdgcn_readlane(widths, j) : (int32_t)W.byte_at(p + wpos + j);
+  }
 
   __device__ uint32_t read_mb_header() {  // :248-271
     uint64_t u;
@@ -657,18 +668,27 @@ struct Delta {
     if (is32 && (md > 0x7fffffffll || md < -0x80000000ll)) return E_DELTA;
     min_delta = md;
     if (pos + mb_count > len) return E_EOF;  // io.ReadFull of the widths
-    int lane = lane_id();
-    // the widths from the register window (usually resident after the
-    // varint): no global round trip of its own per block
-    uint32_t wv = 0u;
-    for (int q = 0; q < mb_count; q++) {
-      const uint32_t b = W.byte_at(p + pos + q);
-      if (lane == q) wv = b;
+    const int lane = lane_id();
+    const uint32_t maxw = is32 ? 32u : 64u;
+    if (mb_count <= 64) {
+      // the widths from the register window (usually resident after the
+      // varint): no global round trip of its own per block
+      uint32_t wv = 0u;
+      for (int q = 0; q < mb_count; q++) {
+        const uint32_t b = W.byte_at(p + pos + q);
+        if (lane == q) wv = b;
+      }
+      if (ballot(lane < mb_count && wv > maxw)) return E_BITWIDTH;
+      widths = wv;
+    } else {
+      // any number of miniblocks (:97-106): every width checked, 64 a load
+      for (int32_t q0 = 0; q0 < mb_count; q0 += 64) {
+        const uint32_t b = q0 + lane < mb_count ? (uint32_t)p[pos + q0 + lane] : 0u;
+        if (ballot(b > maxw)) return E_BITWIDTH;
+      }
+      wpos = pos;
     }
     pos += mb_count;
-    uint32_t maxw = is32 ? 32u : 64u;
-    if (ballot(lane < mb_count && wv > maxw)) return E_BITWIDTH;
-    widths = wv;
     cur_mb = 0;
     return E_OK;
   }
@@ -691,6 +711,11 @@ struct Delta {
     if (mb_count <= 0 || block_size % mb_count != 0) return E_DELTA;
     mbvc = block_size / mb_count;
     if (mbvc == 0) return E_DELTA;
+    {
+      const int64_t g = (mbvc & 7) == 0 ? 8 : (mbvc & 3) == 0 ? 4 : (mbvc & 1) == 0 ? 2 : 1;  // gcd(8, mbvc)
+      const int64_t l = (int64_t)mbvc * (8 / g);
+      adv = (int32_t)min<int64_t>(l, 0x7ffffff8ll);  // past any int32 position: one miniblock for the page
+    }
     e = read_uvarint(W, p, len, pos, u, ovf);
     if (e || u > 0x7fffffffull) return e == E_EOF ? E_EOF : E_DELTA;
     total = (int32_t)u;
@@ -698,13 +723,46 @@ struct Delta {
     if (e) return e == E_EOF ? E_EOF : E_DELTA;
     first = (int64_t)(u >> 1) ^ -(int64_t)(u & 1);
     if (is32 && (first > 0x7fffffffll || first < -0x80000000ll)) return E_DELTA;
-    // a non-multiple-of-8 miniblock or >64 miniblocks is outside the spec and this decoder
-    if ((mbvc & 7) != 0 || mb_count > 64) return E_UNSUPPORTED;
     e = read_mb_header();
     if (e) return e;
-    mb_vi = mbvc;  // no miniblock started yet
+    mb_vi = adv;  // no miniblock started yet
+    mb_v0 = 0;
+    mb_data = pos;
+    mb_w = 0;
     cur_mb = 0;
     position = 0;
+    return E_OK;
+  }
+
+  // A miniblock starts at the current position (:123-136).
+  __device__ __forceinline__ uint32_t start_mb() {
+    if (cur_mb >= mb_count) {
+      uint32_t e = read_mb_header();
+      if (e) return e;
+    }
+    mb_w = width_of(cur_mb);
+    mb_data = pos;
+    pos = mb_data + (int64_t)(adv >> 3) * mb_w;
+    cur_mb++;
+    mb_vi = 0;
+    mb_v0 = position;
+    return E_OK;
+  }
+
+  // The checks of the groups of values [position, position + take) of the
+  // current miniblock: io.ReadFull of each group (:138-143), then, at the
+  // group holding the last header value, the padding length of :150-155
+  // ((mbvc / 8) * w minus the bytes read in this miniblock; < 0 -> error:
+  // only a miniblock whose size is not a multiple of 8 gets there).
+  __device__ __forceinline__ uint32_t check_groups(int take) {
+    const int64_t last_group = (mb_vi + take - 1) >> 3;
+    if (mb_data + (last_group + 1) * mb_w > len) return E_EOF;
+    if (total > 0) {
+      const int32_t pchk = (total - 1) & ~7;  // the only group with position + 8 >= total
+      if (pchk >= position && pchk < position + take && mb_w > 0 &&
+          (int64_t)((pchk - mb_v0) >> 3) + 1 > (int64_t)(mbvc >> 3))
+        return E_DELTA;
+    }
     return E_OK;
   }
 
@@ -728,20 +786,13 @@ struct Delta {
     if (position + n > total) return E_EOF;
     int got = 0;
     while (got < n) {
-      if (mb_vi >= mbvc) {
-        if (cur_mb >= mb_count) {
-          uint32_t e = read_mb_header();
-          if (e) return e;
-        }
-        mb_w = (int32_t)__builtin_amdgcn_readlane(widths, cur_mb);
-        mb_data = pos;
-        pos = mb_data + (int64_t)(mbvc >> 3) * mb_w;
-        cur_mb++;
-        mb_vi = 0;
+      if (mb_vi >= adv) {
+        uint32_t e = start_mb();
+        if (e) return e;
       }
-      const int take = min(mbvc - mb_vi, n - got);
-      int64_t last_group = (mb_vi + take - 1) >> 3;
-      if (mb_data + (last_group + 1) * mb_w > len) return E_EOF;
+      const int take = min(adv - mb_vi, n - got);
+      uint32_t e = check_groups(take);
+      if (e) return e;
       const int64_t bit0 = mb_data * 8 + (int64_t)(mb_vi - got) * mb_w;
 #pragma unroll
       for (int k = 0; k < 4; k++) {
@@ -775,20 +826,13 @@ struct Delta {
     if (position + n > total) return E_EOF;  // d.position >= d.valuesCount
     int got = 0;
     while (got < n) {
-      if (mb_vi >= mbvc) {  // start a miniblock (:280-295)
-        if (cur_mb >= mb_count) {
-          uint32_t e = read_mb_header();
-          if (e) return e;
-        }
-        mb_w = (int32_t)__builtin_amdgcn_readlane(widths, cur_mb);
-        mb_data = pos;
-        pos = mb_data + (int64_t)(mbvc >> 3) * mb_w;
-        cur_mb++;
-        mb_vi = 0;
+      if (mb_vi >= adv) {  // start a miniblock (:280-295)
+        uint32_t e = start_mb();
+        if (e) return e;
       }
-      int take = min(mbvc - mb_vi, n - got);
-      int64_t last_group = (mb_vi + take - 1) >> 3;
-      if (mb_data + (last_group + 1) * mb_w > len) return E_EOF;  // io.ReadFull of a group
+      int take = min(adv - mb_vi, n - got);
+      uint32_t e = check_groups(take);
+      if (e) return e;
       if (lane >= got && lane < got + take) {
         uint64_t d = unpack_u64(p, len, mb_data * 8 + (int64_t)(mb_vi + lane - got) * mb_w, mb_w);
         out = d + (uint64_t)min_delta;
@@ -840,9 +884,11 @@ __device__ inline uint32_t delta_len_stream(const uint8_t *p, int64_t len, int64
     }
     prev += (uint32_t)__builtin_amdgcn_readlane(incl, 63);
   }
-  int64_t fin = dz.pos;
+  // the padding read of :150-155 ends the current miniblock at (mbvc / 8) * w
+  // bytes past its data (checked >= the bytes read by check_groups)
+  int64_t fin = count > 0 ? dz.mb_data + (int64_t)(dz.mbvc >> 3) * dz.mb_w : dz.pos;
   if (count > 0 && dz.cur_mb < dz.mb_count) {
-    const int32_t w = (int32_t)__builtin_amdgcn_readlane(dz.widths, dz.cur_mb);
+    const int32_t w = dz.width_of(dz.cur_mb);
     fin += (int64_t)(dz.mb_count - dz.cur_mb) * (dz.mbvc >> 3) * w;
   }
   pos += min<int64_t>(fin, len - pos);

@@ -763,6 +763,7 @@ struct pqg_batch {
   int err_rg = -1, err_leaf = -1, err_page = -1;
   bool decoded = false;
   hipEvent_t ready = nullptr;  // recorded on the context's upload stream after the chunk bytes' H2D
+  bool ready_final = false;    // `ready` recorded after every set-up copy (else copies may be in flight)
   bool counted = false;        // the last launch was the counting pass (the next decode resumes from it)
   std::vector<uint8_t> tab_host;  // the small tables (d_pages, d_info, d_lists, ...): host image, uploaded at
                                   // the end of d_in
@@ -854,6 +855,7 @@ void pqg_ctx_destroy(pqg_ctx *ctx) {
     if (ctx->pin[i]) hipHostFree(ctx->pin[i]);
     if (ctx->pin_ev[i]) hipEventDestroy(ctx->pin_ev[i]);
   }
+  pqg_release_cache(ctx->device);  // the device's idle cached buffers
   delete ctx;
 }
 
@@ -1212,9 +1214,8 @@ static int supported_encoding(int ptype, int enc) {
   switch (ptype) {
     case T_BYTE_ARRAY:
       return enc == ENC_PLAIN || enc == ENC_RLE_DICT || enc == ENC_DELTA_LBA || enc == ENC_DELTA_BA ? 0 : PQG_ERR_ENCODING;
-    case T_FLBA:
-      if (enc == ENC_PLAIN || enc == ENC_RLE_DICT) return 0;
-      return enc == ENC_DELTA_BA ? PQG_ERR_UNSUPPORTED : PQG_ERR_ENCODING;
+    case T_FLBA:  // getFixedLenByteArrayValuesDecoder chunk_reader.go:86-96
+      return enc == ENC_PLAIN || enc == ENC_RLE_DICT || enc == ENC_DELTA_BA ? 0 : PQG_ERR_ENCODING;
     case T_FLOAT: case T_DOUBLE: case T_INT96:
       return enc == ENC_PLAIN || enc == ENC_RLE_DICT ? 0 : PQG_ERR_ENCODING;
     case T_INT32: case T_INT64:
@@ -1511,7 +1512,8 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
         B->pages.back().lvl_base = B->lvl_bytes;
         B->lvl_bytes += (((int64_t)(L.max_rep > 0 ? 2 : 1) * d.num_values) + 15) & ~(int64_t)15;
       }
-      if (L.physical_type == T_BYTE_ARRAY && (d.enc == ENC_DELTA_LBA || d.enc == ENC_DELTA_BA)) {
+      if ((L.physical_type == T_BYTE_ARRAY && (d.enc == ENC_DELTA_LBA || d.enc == ENC_DELTA_BA)) ||
+          (L.physical_type == T_FLBA && d.enc == ENC_DELTA_BA)) {
         B->pages.back().lens_base = B->lens_entries;  // suffix lengths, then prefix lengths
         B->lens_entries += 2 * (int64_t)std::max(d.num_values, 0);
       } else if (L.physical_type == T_BYTE_ARRAY && d.enc == ENC_PLAIN && L.value_width <= 0) {
@@ -1573,6 +1575,24 @@ void release_idle(DevCache &c, int dev) {  // caller holds c.mu
 }  // namespace
 extern "C" {
 
+// Idle bytes the cache may hold: PQG_DEV_CACHE_MB, else an eighth of the
+// device's memory capped at 8 GiB (torch's allocator or another process on
+// the device cannot reclaim what the cache holds; a failed hipMalloc here
+// releases it, pqg_ctx_destroy and pqg_release_cache too).
+static size_t dev_cache_cap() {
+  if (getenv("PQG_DEV_CACHE_MB")) return (size_t)atoll(getenv("PQG_DEV_CACHE_MB")) << 20;
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess || tot == 0) tot = (size_t)64 << 30;
+  return std::min(tot / 8, (size_t)8 << 30);
+}
+
+int pqg_release_cache(int device) {
+  DevCache &c = dev_cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  release_idle(c, device);
+  return PQG_OK;
+}
+
 static int alloc_dev(void **p, size_t n) {
   int dev = 0;
   hipGetDevice(&dev);
@@ -1610,7 +1630,7 @@ static void free_dev(void *p) {
     hipFree(p);
     return;
   }
-  static const size_t cap = (getenv("PQG_DEV_CACHE_MB") ? (size_t)atoll(getenv("PQG_DEV_CACHE_MB")) : 32768) << 20;
+  static const size_t cap = dev_cache_cap();
   const auto key = it->second;
   c.live.erase(it);
   if (c.idle_bytes + key.second > cap) {
@@ -1684,13 +1704,15 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     if (!tiled) {
       // flat fixed-width pages (DELTA, nullable, PLAIN inside non-tiled
       // columns) go to the k_decode<1> instance, the rest to k_decode<0>
+      // (FIXED_LEN_BYTE_ARRAY DELTA_BYTE_ARRAY pages: k_decode<0> + k_dba)
+      const bool fl_dba = L.physical_type == T_FLBA && d.enc == ENC_DELTA_BA;
       const bool flat_fw = L.max_rep == 0 && (L.value_width == 4 || L.value_width == 8) &&
                            L.physical_type != T_BYTE_ARRAY && L.physical_type != T_BOOLEAN &&
-                           !(cp.flags & COL_EMIT_LEVELS);
+                           !(cp.flags & COL_EMIT_LEVELS) && !fl_dba;
       const bool flat_ba = L.max_rep == 0 && L.physical_type == T_BYTE_ARRAY && !(cp.flags & COL_EMIT_LEVELS);
       const bool nest_fw = L.max_rep > 0 && (L.value_width == 4 || L.value_width == 8) &&
                            L.physical_type != T_BYTE_ARRAY && L.physical_type != T_BOOLEAN &&
-                           !(cp.flags & COL_EMIT_LEVELS);
+                           !(cp.flags & COL_EMIT_LEVELS) && !fl_dba;
       static const bool pstr_off = getenv("PQG_NO_PLAIN_STR") != nullptr;
       if (flat_ba && L.max_def == 0 && d.enc == ENC_PLAIN && d.lens_base >= 0 && !pstr_off) {
         // several waves per page (k_plain_str) over k_prepare's (offset, length) scratch
@@ -1705,7 +1727,9 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
        : nest_fw ? B->general_nest
                  : B->general_list)
           .push_back(pi);
-      if (L.physical_type == T_BYTE_ARRAY && d.enc == ENC_DELTA_BA) B->dba_list.push_back(pi);
+      if ((L.physical_type == T_BYTE_ARRAY || fl_dba) && d.enc == ENC_DELTA_BA) B->dba_list.push_back(pi);
+      // k_prepare validates DELTA_BYTE_ARRAY lengths on the count path
+      if (fl_dba) B->cols[(size_t)d.col].flags |= COL_NEEDS_COUNT;
       continue;
     }
     const int32_t n = std::max(d.num_values, 0);
@@ -2285,6 +2309,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     }
   }
   HIPCHK(hipEventRecord(B->ready, ctx->upload));  // decodes wait for every set-up copy
+  B->ready_final = true;
   phase("outputs+tables");
   return PQG_OK;
 }
@@ -2753,7 +2778,10 @@ int pqg_batch_kernel_times(pqg_batch *B, const char **names, float *ms, int cap)
 void pqg_batch_destroy(pqg_batch *B) {
   if (!B) return;
   hipSetDevice(B->ctx->device);
-  if (B->ready) hipEventSynchronize(B->ready);  // an upload never decoded may still be in flight
+  // an upload never decoded may still be in flight; a batch whose set-up
+  // failed part-way may have copies queued after its last `ready` record
+  if (B->ready_final) hipEventSynchronize(B->ready);
+  else hipStreamSynchronize(B->ctx->upload);
   hipStreamSynchronize(B->ctx->stream);
   for (auto &cp : B->cols) {
     free_dev(cp.values);

@@ -905,6 +905,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     for (int64_t p = F + lane; p < dl; p += 64) dst[p] = ring[p & RING_MASK];
   if (err == E_OK && !write) err = E_SIZE;  // compress.go:117-119
   if (seg) {
+    // the last segment must end the stream exactly (decode_other.go:16-99
+    // rejects tokens or bytes after the decoded length)
+    if (err == E_OK && seg_k == a.seg_base[gi + 1] - a.seg_base[gi] - 1 && s != slen) err = E_SNAPPY;
     // a segment that does not decode on its own: the page is decoded again
     // serially (which also finds the exact error of a corrupt stream)
     if (err && lane == 0) atomicMax(&a.seg_flag[gi], 1u);
@@ -2027,7 +2030,9 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
   // DELTA_(LENGTH_)BYTE_ARRAY: every length stream is decoded at init
   // (type_bytearray.go:98-108, :186-209); lengths go to the page's scratch
   int32_t dstr_data = 0, dstr_cnt = 0;
-  const bool dstr = c.ptype == T_BYTE_ARRAY && (d.enc == ENC_DELTA_LBA || d.enc == ENC_DELTA_BA) && d.lens_base >= 0;
+  const bool dstr = ((c.ptype == T_BYTE_ARRAY && (d.enc == ENC_DELTA_LBA || d.enc == ENC_DELTA_BA)) ||
+                     (c.ptype == T_FLBA && d.enc == ENC_DELTA_BA)) &&
+                    d.lens_base >= 0;
   if (dstr) {
     const int32_t nvp = max(d.num_values, 0);
     int32_t *S = a.lens + d.lens_base, *P = S + nvp;
@@ -2148,7 +2153,7 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
   PSTAMP(page, 6, __builtin_amdgcn_s_memrealtime());
   // string bytes of the non-null values
   int64_t sbytes = 0;
-  if (c.ptype == T_BYTE_ARRAY && nn > 0) {
+  if ((c.ptype == T_BYTE_ARRAY || dstr) && nn > 0) {
     if (d.enc == ENC_PLAIN) {
       // length prefixes by pointer jumping (ba_walk), in the run walk's LDS
       // each value's (offset, length) goes to the page's scratch for k_decode
@@ -2234,6 +2239,9 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
           const int64_t pv = (int64_t)shfl64((uint64_t)vl, lane > 0 ? lane - 1 : 0);
           const int64_t plen_prev = lane == 0 ? prevlen : pv;
           if (act && !code && (pl + s < 0 || plen_prev < pl)) code = E_BYTE_ARRAY;  // "invalid prefix len"
+          // FIXED_LEN_BYTE_ARRAY: a value must fill its type_length slot (the
+          // reference would keep an odd-length []byte: a documented deviation)
+          if (act && !code && c.ptype == T_FLBA && vl != c.width) code = E_BYTE_ARRAY;
         }
         const uint64_t bad = ballot(act && code != 0);
         if (bad) {
@@ -2244,7 +2252,7 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
         acc_v += (int64_t)shfl64((uint64_t)wave_incl_scan64(act ? vl : 0), 63);
         prevlen = (int64_t)shfl64((uint64_t)vl, cnt - 1);
       }
-      sbytes = acc_v;
+      sbytes = c.ptype == T_FLBA ? 0 : acc_v;  // FIXED_LEN_BYTE_ARRAY: fixed-width slots, no string bytes
     } else {
       set_status(a.status, page, ST_VALUES, E_UNSUPPORTED);
       return;
@@ -2719,7 +2727,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   int64_t spos = 0;
   // DELTA strings: lengths decoded and validated by k_prepare (scratch); suffix
   // bytes start at str_data.  DELTA_BYTE_ARRAY bytes are written by k_dba.
-  const bool dstr = is_ba && (d.enc == ENC_DELTA_LBA || d.enc == ENC_DELTA_BA) && d.lens_base >= 0;
+  // FIXED_LEN_BYTE_ARRAY DELTA_BYTE_ARRAY (KIND 0 only): slots zeroed here,
+  // the values written by k_dba
+  const bool fl_dba = KIND == 0 && c.ptype == T_FLBA && d.enc == ENC_DELTA_BA && d.lens_base >= 0;
+  const bool dstr = (is_ba && (d.enc == ENC_DELTA_LBA || d.enc == ENC_DELTA_BA) && d.lens_base >= 0) || fl_dba;
   const bool defer_bytes = dstr && d.enc == ENC_DELTA_BA;
   int64_t dpos = pi.str_data;
 
@@ -3116,7 +3127,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
               for (int q = 0; q < k; q++) vi += valid[q];
               sp = vals + (nn_run + vbase + vi) * (int64_t)w;
             }
-            for (int b = 0; b < w; b++) op[b] = valid[k] ? sp[b] : 0;
+            for (int b = 0; b < w; b++) op[b] = valid[k] && !fl_dba ? sp[b] : 0;
           }
           si++;
         }
@@ -3810,13 +3821,42 @@ __global__ __launch_bounds__(BIG_WAVES * 64) void k_expand_big(KArgs a) {
 // ===========================================================================
 // K5b: k_dba — DELTA_BYTE_ARRAY value bytes (type_bytearray.go:211-240): value
 // i = previous value[:prefix_i] + suffix_i, rebuilt in value order by one wave
-// per page over an LDS copy of the previous value (updated in place: only the
-// suffix is written).  Lengths were decoded and validated by k_prepare, and the
-// string offsets / validity written by k_decode; a batch's suffix bytes are
-// contiguous in the page and staged in LDS when they fit.  Values longer than
-// DBA_PREV bytes are reported PQG_ERR_UNSUPPORTED (a documented limit).
+// per page.  The first DBA_PREV bytes of the previous value are kept in LDS
+// (updated in place: only the suffix is written); a prefix reaching past them
+// is read back from the previous value in the output (every value is written
+// there), so values of any length decode.  Lengths were decoded and validated
+// by k_prepare, and the string offsets / validity written by k_decode; a
+// batch's suffix bytes are contiguous in the page and staged in LDS when they
+// fit.  FIXED_LEN_BYTE_ARRAY pages (getFixedLenByteArrayValuesDecoder,
+// chunk_reader.go:86-96) write value i to the slot of the i-th defined level.
 // ===========================================================================
 constexpr int DBA_PREV = 16384, DBA_STAGE = 8192;  // per wave: 96 KiB of LDS per workgroup
+
+// One value: out[0, plen + s) = prev value[0, plen) + suffix[0, s), where the
+// previous value starts at `pv` in the output and its first DBA_PREV bytes
+// are in `prev` (LDS), which then holds the new value's.
+__device__ __forceinline__ void dba_value(uint8_t *prev, const uint8_t *suffix, int32_t plen, int32_t s, uint8_t *out,
+                                          const uint8_t *pv, int lane) {
+  const int32_t vl = plen + s;
+  if (vl <= DBA_PREV) {
+    for (int32_t b = lane; b < s; b += 64) prev[plen + b] = suffix[b];
+    for (int32_t b = lane; b < vl; b += 64) out[b] = prev[b];
+    return;
+  }
+  if (plen > DBA_PREV) {
+    // the previous value's bytes past the LDS copy, from the output this wave
+    // wrote: its stores retired, then read at device scope (past a stale L1 line)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    for (int32_t b = DBA_PREV + lane; b < plen; b += 64)
+      out[b] = (uint8_t)__hip_atomic_load(pv + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  for (int32_t b = lane; b < min(plen, DBA_PREV); b += 64) out[b] = prev[b];
+  for (int32_t b = lane; b < s; b += 64) {
+    const uint8_t x = suffix[b];
+    out[plen + b] = x;
+    if (plen + b < DBA_PREV) prev[plen + b] = x;
+  }
+}
 
 __global__ __launch_bounds__(256) void k_dba(KArgs a) {
   __shared__ uint8_t prev_all[4][DBA_PREV];
@@ -3835,8 +3875,40 @@ __global__ __launch_bounds__(256) void k_dba(KArgs a) {
   const int32_t nvp = max(d.num_values, 0);
   const int32_t *S = a.lens + d.lens_base, *P = S + nvp;
   uint8_t *prev = prev_all[wv], *stage = stage_all[wv];
+  if (c.ptype == T_FLBA) {
+    // every value is c.width bytes (k_prepare checked prefix + suffix ==
+    // width); value i goes to the slot of the i-th level with def == max_def,
+    // found 64 levels at a time from k_levels' bytes
+    const int w = c.width;
+    const bool flat = c.max_rep == 0;
+    uint8_t *vout = c.values + (flat ? d.level_base : pi.slot_base) * (int64_t)w;
+    const uint8_t *ld = c.max_def > 0 ? a.lvl + d.lvl_base + (c.max_rep > 0 ? (int64_t)nvp : 0) : nullptr;
+    int64_t i = 0, slot_run = 0, soff = 0;
+    const uint8_t *pv = vout;
+    for (int64_t e0 = 0; e0 < nvp && i < nn; e0 += 64) {
+      const int cnt = (int)min<int64_t>(64, nvp - e0);
+      const int dl = lane < cnt ? (ld ? (int)ld[e0 + lane] : c.max_def) : -1;
+      const uint64_t vm = ballot(lane < cnt && dl == c.max_def);
+      const uint64_t sm = ballot(lane < cnt && (flat || dl >= c.rep_def));
+      const uint32_t my_slot = (uint32_t)__builtin_popcountll(sm & ((1ull << lane) - 1));  // within the 64
+      uint64_t rem = vm;
+      while (rem && i < nn) {
+        const int t = (int)__builtin_ctzll(rem);
+        rem &= rem - 1;
+        const int64_t slot = slot_run + (int64_t)__builtin_amdgcn_readlane(my_slot, t);
+        const int32_t pl = P[i], plen = pl > 0 ? pl : 0;
+        uint8_t *op = vout + slot * (int64_t)w;
+        dba_value(prev, data + soff, plen, w - plen, op, pv, lane);
+        pv = op;
+        soff += w - plen;
+        i++;
+      }
+      slot_run += __builtin_popcountll(sm);
+    }
+    return;
+  }
   uint8_t *out = c.values + pi.str_base;
-  int64_t soff = 0, ooff = 0;
+  int64_t soff = 0, ooff = 0, poff = 0;
   for (int64_t i0 = 0; i0 < nn; i0 += 64) {
     const int cnt = (int)min<int64_t>(64, nn - i0);
     const int32_t s_l = lane < cnt ? S[i0 + lane] : 0;
@@ -3850,14 +3922,10 @@ __global__ __launch_bounds__(256) void k_dba(KArgs a) {
       const int32_t s = (int32_t)__builtin_amdgcn_readlane((uint32_t)s_l, t);
       const int32_t pl = (int32_t)__builtin_amdgcn_readlane((uint32_t)p_l, t);
       const int32_t so = (int32_t)__builtin_amdgcn_readlane((uint32_t)sexcl, t);
-      const int32_t plen = pl > 0 ? pl : 0, vl = plen + s;
-      if (vl > DBA_PREV) {
-        set_status(a.status, page, ST_VALUES, E_UNSUPPORTED);
-        return;
-      }
-      for (int32_t b = lane; b < s; b += 64) prev[plen + b] = staged ? stage[so + b] : data[soff + so + b];
-      for (int32_t b = lane; b < vl; b += 64) out[ooff + b] = prev[b];
-      ooff += vl;
+      const int32_t plen = pl > 0 ? pl : 0;
+      dba_value(prev, staged ? stage + so : data + soff + so, plen, s, out + ooff, out + poff, lane);
+      poff = ooff;
+      ooff += plen + s;
     }
     soff += stot;
   }

@@ -56,7 +56,7 @@ EXPORTS = [
     "pqg_file_last_error", "pqg_batch_create", "pqg_batch_decode", "pqg_batch_sync",
     "pqg_batch_error_location", "pqg_batch_column", "pqg_batch_copy", "pqg_batch_stats_get",
     "pqg_batch_kernel_times", "pqg_batch_set_timing", "pqg_batch_destroy",
-    "pqg_stream_open", "pqg_stream_next", "pqg_stream_close", "pqg_file_open_many",
+    "pqg_stream_open", "pqg_stream_next", "pqg_stream_close", "pqg_file_open_many", "pqg_release_cache",
 ]
 
 
@@ -136,6 +136,7 @@ def lib():
                 "pqg_stream_next": (i32, [vp, P(vp), P(ctypes.c_int)]),
                 "pqg_stream_close": (None, [vp]),
                 "pqg_file_open_many": (i32, [P(ctypes.c_char_p), i32, i32, P(vp), P(ctypes.c_int)]),
+                "pqg_release_cache": (i32, [i32]),
             }
             for name, (res, args) in sig.items():
                 fn = getattr(L, name)
@@ -158,6 +159,11 @@ def _check(rc, what=""):
 
 def device_count():
     return lib().pqg_device_count()
+
+
+def release_cache(device=-1):
+    """Free the idle device buffers the library keeps for reuse (pqg_release_cache)."""
+    _check(lib().pqg_release_cache(int(device)), "pqg_release_cache")
 
 
 class Context:

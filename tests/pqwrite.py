@@ -160,3 +160,46 @@ def write(schema, columns):
     fmd = _S().i32(1, 1).list(2, T_STRUCT, elems).i64(3, num_rows or 0).list(4, T_STRUCT, [rg]).done()
     out += fmd + struct.pack("<i", len(fmd)) + b"PAR1"
     return bytes(out)
+
+
+def write_column(pages, ptype=1, encoding=5, optional=False, type_length=0, dict_page=None, dict_count=0):
+    """One leaf `v` (parquet.Type `ptype`, REQUIRED or OPTIONAL), one row group,
+    V1 uncompressed data pages whose values sections are given as bytes:
+    pages = [(num_values, def_levels or None, values_section_bytes)].  With
+    `optional`, def levels go in front of each values section as one
+    bit-packed hybrid run (bit width 1).  Returns the file bytes."""
+    elems = [_S().str(4, "schema").i32(5, 1)]
+    leaf = _S().i32(1, ptype)
+    if type_length:
+        leaf.i32(2, type_length)
+    leaf.i32(3, 1 if optional else 0).str(4, "v")
+    elems.append(leaf)
+    out = bytearray(b"PAR1")
+    first = len(out)
+    dict_off = None
+    if dict_page is not None:
+        dph = _S().i32(1, dict_count).i32(2, 0)
+        ph = _S().i32(1, 2).i32(2, len(dict_page)).i32(3, len(dict_page)).struct(7, dph).done()
+        dict_off = len(out)
+        out += ph + dict_page
+    data_off = len(out)
+    n_total = 0
+    for n, dl, body in pages:
+        b = bytearray()
+        if optional:
+            s = hybrid_bitpacked(dl, 1)
+            b += struct.pack("<I", len(s)) + s
+        b += body
+        dph = _S().i32(1, n).i32(2, encoding).i32(3, 3).i32(4, 3)
+        out += _S().i32(1, 0).i32(2, len(b)).i32(3, len(b)).struct(5, dph).done() + b
+        n_total += n
+    size = len(out) - first
+    meta = (_S().i32(1, ptype).list(2, T_I32, [0, 3, encoding]).list(3, T_BINARY, ["v"]).i32(4, 0).i64(5, n_total)
+            .i64(6, size).i64(7, size).i64(9, data_off))
+    if dict_off is not None:
+        meta.i64(11, dict_off)
+    chunk = _S().i64(2, first).struct(3, meta)
+    rg = _S().list(1, T_STRUCT, [chunk]).i64(2, size).i64(3, n_total)
+    fmd = _S().i32(1, 1).list(2, T_STRUCT, elems).i64(3, n_total).list(4, T_STRUCT, [rg]).done()
+    out += fmd + struct.pack("<i", len(fmd)) + b"PAR1"
+    return bytes(out)

@@ -202,6 +202,13 @@ def test_snappy_segments_and_fallback():
     for n in (65536, 65537, 200000, 1 << 20, (1 << 20) + 12345):
         data = (np.round(rng.standard_normal(n // 8 + 1), 2).tobytes() + b"x" * 7)[:n]
         both(pa.compress(data, codec="snappy", asbytes=True), n)
+        if n >= 200000:
+            # bytes or a token after the decoded length end the stream corrupt
+            # (decode_other.go:16-99), segmented or not
+            s = pa.compress(data, codec="snappy", asbytes=True)
+            both(s + b"\x00", n)
+            both(s + bytes([0x01, 0x05]), n)
+            both(s + bytes([0x00, 0x41]), n)
     # a copy that reaches back across the 64 KiB boundary (a token starts there): fallback
     lit = rng.integers(0, 256, 65536, dtype=np.uint8).tobytes()
     stream = _uvarint(65536 + 64) + bytes([62 << 2]) + (65536 - 1).to_bytes(3, "little") + lit
