@@ -97,6 +97,11 @@ constexpr int LD_MIX_MAX = 32 * 1024;     // k_expand_mix LDS per workgroup with
 // its own launch (the dynamic LDS size is per launch)
 constexpr int BIG_WAVES = 8;
 constexpr int BIG_JOBS = 16;              // jobs per group (default; PQG_BIG_JOBS)
+// k_expand_pass: workgroups of PASS_WAVES_H waves (one job each) streaming a
+// dictionary too large for LDS through it in slices of the launch's LDS
+// (PQG_PASS_WAVES=8: half-size workgroups and slices, two per CU)
+int pass_waves_h();
+inline int pass_waves(int width) { return width == 4 ? pass_waves_h() : pass_waves_h() / 2; }
 constexpr int PLAIN_STR_ITEM = 2048;      // k_plain_str: values per work item
 struct LdsGroup {
   int32_t job0, njobs;   // jobs [job0, job0 + njobs) of the launch order

@@ -35,6 +35,15 @@
 #include "../../include/pqgpu.h"
 #include "pq_common.h"
 
+namespace pq {
+// k_expand_pass workgroup size (PQG_PASS_WAVES=8: half-size groups and slices)
+int pass_waves_h() {
+  static const int n = getenv("PQG_PASS_WAVES") && atoi(getenv("PQG_PASS_WAVES")) == 8 ? 8 : 16;
+  return n;
+}
+}  // namespace pq
+
+
 using namespace pq;
 
 extern "C" {
@@ -82,6 +91,7 @@ struct pq_launch_args {
   uint32_t *seg_flag;
 };
 int pq_launch(int which, const pq_launch_args *p, hipStream_t s);
+extern int pq_launch_fail_which, pq_launch_fail_err;
 static constexpr int64_t kSnapSeg = 65536;  // pq_kernels.hip SNAP_SEG
 }
 
@@ -712,6 +722,7 @@ struct pqg_batch {
   bool any_count = false;
   std::vector<ChunkError> chunk_errors;
   int64_t input_bytes = 0, staged_bytes = 0, h2d_bytes = 0, host_inflated = 0, dict_entries = 0;
+  int64_t literal_pages = 0;  // Snappy pages that are one literal, read in place (no k_snappy work)
   // device
   uint8_t *d_in = nullptr, *d_stage = nullptr;
   uint8_t *d_in_alloc = nullptr;  // the allocation d_in lives in (PQG_DEBUG_INPUT_HIGH_WORD shifts d_in inside it)
@@ -1209,6 +1220,37 @@ int pqg_file_last_error(const pqg_file *f, char *buf, size_t cap) {
 // ---------------------------------------------------------------------------
 // batch planning
 // ---------------------------------------------------------------------------
+// Raw Snappy block (decode.go:32-75) that is exactly one literal holding
+// `expect` bytes: the uvarint decoded length equals `expect`, the first tag is
+// a literal of that length and the stream ends with it.  *data = offset of
+// the literal's bytes.  Anything else (including a corrupt stream) is left to
+// k_snappy, which reports the reference's error.
+static bool snappy_single_literal(const uint8_t *p, int64_t n, int64_t expect, int64_t *data) {
+  uint64_t v = 0;
+  int64_t i = 0;
+  for (int sh = 0;; sh += 7) {
+    if (i >= n || i >= 5) return false;
+    const uint8_t b = p[i++];
+    v |= (uint64_t)(b & 0x7f) << sh;
+    if (b < 0x80) break;
+  }
+  if (v == 0 || v != (uint64_t)expect || v > 0xffffffffull || i >= n) return false;
+  const uint8_t tag = p[i];
+  if (tag & 3) return false;
+  uint64_t x = tag >> 2;
+  int64_t hs = 1;
+  if (x >= 60) {
+    const int extra = (int)x - 59;
+    hs = 1 + extra;
+    if (i + hs > n) return false;
+    x = 0;
+    for (int k = 0; k < extra; k++) x |= (uint64_t)p[i + 1 + k] << (8 * k);
+  }
+  if (x + 1 != v || i + hs + (int64_t)v != n) return false;
+  *data = i + hs;
+  return true;
+}
+
 static int supported_encoding(int ptype, int enc) {
   if (enc == ENC_PLAIN_DICT) enc = ENC_RLE_DICT;  // chunk_reader.go:145-147
   switch (ptype) {
@@ -1458,7 +1500,19 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
       } else if (!registered) {
         fail(ST_DECOMPRESS, PQG_ERR_CODEC);
       } else if (device_codec) {
-        needs_device_codec = true;
+        // a block that is exactly one literal (an incompressible page: C2's
+        // keys, random values) is its own content: the page is read in place
+        // as if uncompressed, no k_snappy work (k_snappy's alias1 check,
+        // decided here from the payload the host already has)
+        int64_t lit = -1;
+        if (C.codec == PQG_CODEC_SNAPPY && snappy_single_literal(f->data + w.payload + lsize, comp, body, &lit) &&
+            (h.type != 2 || ((d.src + (uint64_t)(lsize + lit)) & 7) == 0)) {
+          d.body_src = BODY_RAW;
+          d.body = d.src + (uint64_t)(lsize + lit);
+          B->literal_pages++;
+        } else {
+          needs_device_codec = true;
+        }
       } else if (builtin && C.codec == PQG_CODEC_UNCOMPRESSED) {
         if (comp != body) fail(ST_DECOMPRESS, PQG_ERR_SIZE);
       } else {
@@ -1485,7 +1539,7 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
       d.body = (uint64_t)stage_off;
       stage_off += ((body + 15) & ~15) + 16;
       B->staged_bytes += body;
-    } else if (d.body_src == BODY_RAW) {
+    } else if (d.body_src == BODY_RAW && !d.body) {
       d.body = d.src + (uint64_t)lsize;
     }
     int32_t my_index = (int32_t)B->pages.size();
@@ -1778,11 +1832,18 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   // the machine for the whole launch.
   B->ex_lds = (B->ex_lds + 255) & ~255;  // LDS-DMA pieces of 16 bytes per lane, the last one partial
   const bool ld_off = getenv("PQG_NO_LDS_DICT") != nullptr;
-  std::vector<TileJob> slot_tiles, ld_tiles, big_tiles;
-  std::vector<LdsGroup> big_groups[2];
+  std::vector<TileJob> slot_tiles, ld_tiles, big_tiles, pass_tiles;
+  std::vector<LdsGroup> big_groups[2], pass_groups[2];
   const int64_t ld_max = getenv("PQG_LD_MAX_KB") ? 1024 * (int64_t)atoi(getenv("PQG_LD_MAX_KB")) : LD_MIX_MAX;
   const int64_t big_jobs = getenv("PQG_BIG_JOBS") ? std::max(1, atoi(getenv("PQG_BIG_JOBS"))) : BIG_JOBS;
   // which chunks fit the mixed launch's LDS groups, or only k_expand_big's
+  // k_expand_pass (opt-in, PQG_PASS=1; measured slower than the L1/L2
+  // gathers it replaces): dictionaries past the mixed launch's
+  // LDS groups up to PQG_PASS_MAX_KB (default 1 MiB)
+  static const bool pass_on = getenv("PQG_PASS") != nullptr && getenv("PQG_PASS")[0] == '1';
+  static const int64_t pass_max =
+      getenv("PQG_PASS_MAX_KB") ? 1024 * (int64_t)atoi(getenv("PQG_PASS_MAX_KB")) : (int64_t)1 << 20;
+  const int64_t pass_lds = pass_waves_h() == 16 ? LD_LDS_MAX : LD_LDS_MAX / 2;
   auto ld_class = [&](const std::vector<TileJob> &ct, int32_t W, int64_t &dbytes, int32_t &ks) {
     dbytes = 0;
     ks = 0;
@@ -1791,9 +1852,11 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     for (const TileJob &tj : ct) ks = std::max(ks, page_need[(size_t)tj.page]);
     ks = (ks + 255) & ~255;
     const int64_t J = (int64_t)ct.size();
-    if (dbytes <= 0 || ks <= 0 || dbytes * 4 > J * EX_WAVE_VALUES * W) return 0;
-    if (dbytes + (int64_t)LD_WAVES_H * ks <= ld_max) return 1;
-    if (dbytes + (int64_t)BIG_WAVES * ks <= LD_LDS_MAX) return 2;
+    if (dbytes <= 0 || ks <= 0) return 0;
+    const bool amortised = dbytes * 4 <= J * EX_WAVE_VALUES * W;
+    if (amortised && dbytes + (int64_t)LD_WAVES_H * ks <= ld_max) return 1;
+    if (pass_on && dbytes <= pass_max && (int64_t)pass_waves(W) * ks <= pass_lds) return 3;
+    if (amortised && dbytes + (int64_t)BIG_WAVES * ks <= LD_LDS_MAX) return 2;
     return 0;
   };
   // k_expand_big is its own launch: it pays when its chunks are a good part
@@ -1824,6 +1887,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     std::vector<LdG> ldg;
     std::vector<std::vector<TileJob>> bins(8);
     std::vector<const std::vector<TileJob> *> gchunks;  // chunks gathering through L1/L2
+    std::vector<std::pair<const std::vector<TileJob> *, int32_t>> pass_chunks;  // (chunk, kspan)
     for (const auto &ct : chunk_tiles) {
       if (ct.empty() || B->cols[(size_t)B->pages[(size_t)ct[0].page].col].info.value_width != W) continue;
       bool ld = false;
@@ -1841,6 +1905,13 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
           for (int64_t q = 0; q < ng; q++) ldg.push_back({&ct, q * J / ng, (q + 1) * J / ng, (int32_t)dbytes, ks});
           ld = true;
           B->pages[(size_t)ct[0].dict].alias_any = 1;  // copied into LDS with a funnel shift anyway
+        } else if (cls == 3) {
+          // k_expand_pass: groups of pass_waves(W) jobs; a chunk's groups go
+          // to one XCD residue (its dictionary stays in that L2), chunks
+          // dealt to the least-loaded residue
+          pass_chunks.push_back({&ct, ks});
+          ld = true;
+          B->pages[(size_t)ct[0].dict].alias_any = 1;  // copied into LDS with a funnel shift
         } else if (!big_off) {
           // a dictionary past the mixed launch's LDS that one CU holds beside
           // BIG_WAVES waves' keys: groups of big_jobs jobs in k_expand_big
@@ -1955,6 +2026,41 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
       else lr++;
     }
     B->ldn[ws] = (int32_t)B->lgroups.size() - nb0;
+    if (!pass_chunks.empty()) {
+      std::vector<std::vector<LdsGroup>> res(8);
+      int64_t load[8] = {};
+      std::stable_sort(pass_chunks.begin(), pass_chunks.end(),
+                       [](const auto &x, const auto &y) { return x.first->size() > y.first->size(); });
+      for (auto &pc : pass_chunks) {
+        const std::vector<TileJob> &ct = *pc.first;
+        size_t q = 0;
+        for (size_t r = 1; r < 8; r++)
+          if (load[r] < load[q]) q = r;
+        const int64_t J = (int64_t)ct.size();
+        const int64_t ng = (J + pass_waves(W) - 1) / pass_waves(W);
+        for (int64_t k = 0; k < ng; k++) {
+          LdsGroup g = {};
+          g.job0 = -1 - (int32_t)pass_tiles.size();  // rebased below
+          for (int64_t jj = k * J / ng; jj < (k + 1) * J / ng; jj++) pass_tiles.push_back(ct[(size_t)jj]);
+          g.njobs = (int32_t)((k + 1) * J / ng - k * J / ng);
+          g.dpage = ct[0].dict;
+          g.dict_bytes = pass_lds;  // slice bytes: the launch's whole LDS
+          g.kspan = pc.second;
+          res[q].push_back(g);
+        }
+        load[q] += J;
+      }
+      size_t rounds = 0;
+      for (auto &v : res) rounds = std::max(rounds, v.size());
+      for (size_t r = 0; r < rounds; r++)
+        for (size_t q = 0; q < 8; q++) {
+          LdsGroup g = {};
+          g.dpage = -1;
+          if (r < res[q].size()) g = res[q][r];
+          pass_groups[ws].push_back(g);
+        }
+      B->ldl[4 + ws] = (int32_t)pass_lds;
+    }
   }
   // job indices are relative to the launch's first slot (the 8-byte launch
   // starts at block ldn[0])
@@ -1973,9 +2079,19 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     }
     B->ldn[2 + ws] = (int32_t)big_groups[ws].size();
   }
+  // k_expand_pass groups last, absolute job indices
+  const size_t pass_base = big_base + big_tiles.size();
+  for (int ws = 0; ws < 2; ws++) {
+    for (LdsGroup g : pass_groups[ws]) {
+      if (g.njobs > 0) g.job0 = (int32_t)pass_base + (-1 - g.job0);
+      B->lgroups.push_back(g);
+    }
+    B->ldn[4 + ws] = (int32_t)pass_groups[ws].size();
+  }
   B->tiles = std::move(slot_tiles);
   B->tiles.insert(B->tiles.end(), ld_tiles.begin(), ld_tiles.end());
   B->tiles.insert(B->tiles.end(), big_tiles.begin(), big_tiles.end());
+  B->tiles.insert(B->tiles.end(), pass_tiles.begin(), pass_tiles.end());
 
   // k_snappy takes pages in list order, one wave each: the longest bodies
   // first (longest-processing-time order), so that the long serial token
@@ -2581,6 +2697,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     e |= pq_launch(9, &a, s);  // k_expand_mix (tiled pages)
     if (big && big_order == 0) e |= pq_launch(22, &a, s);
     if (big && big_order == 2) hipStreamWaitEvent(s, ctx->join[1], 0);
+    if (B->ldn[4] + B->ldn[5] > 0) e |= pq_launch(27, &a, s);  // k_expand_pass (wide dictionaries)
     if (B->ngen_flat > 0) hipStreamWaitEvent(s, ctx->join[0], 0);
     if (B->ngen_nest > 0) hipStreamWaitEvent(s, ctx->join[2], 0);
     mark(true);
@@ -2590,7 +2707,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     mark(false);
   }
   if (e) {
-    set_err("kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+    set_err("kernel launch failed: kernel id %d: %s", pq_launch_fail_which, hipGetErrorString((hipError_t)pq_launch_fail_err));
     return PQG_ERR_DEVICE;
   }
   if (timed) {

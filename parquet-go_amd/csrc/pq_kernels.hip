@@ -3702,6 +3702,276 @@ __device__ __forceinline__ void expand_job(const KArgs &a, const TileJob &tj, co
 
 
 // ===========================================================================
+// K5p: k_expand_pass — RLE_DICTIONARY jobs whose dictionary is too large for
+// the mixed launch's LDS groups (C2's bit widths 14-20: 64 KiB .. 4 MiB).
+// Gathering those through L1/L2 is bound by the L2's request rate (about one
+// request per value, ~230 Gvalues/s for the whole chip); here a workgroup of
+// pass_waves(WIDTH) waves takes pass_waves(WIDTH) jobs of one chunk, extracts their keys into
+// registers (staged key bytes in LDS, as k_expand_mix does), and then streams
+// the dictionary through its LDS in slices of the launch's whole LDS: per
+// slice, every key inside it gathers with ds_read.  The dictionary reaches
+// the CU as 16-byte loads (a slice is ~1-3 K L2 requests instead of one per
+// value), at the cost of one pass over the keys per slice; the host sends
+// only dictionaries of a few slices here (PQG_PASS_MAX_KB).
+// ===========================================================================
+
+// The keys of job tj (values [v0, lim) of its page) into key[][][] (value
+// v0 + 256 r + 4 lane + q -> key[r / HR][r % HR][q]), with the run-window and
+// staging logic of expand_job.  Returns 0 (keys valid, every one < dict_n),
+// 1 (the job does not fit the staged form: the caller decodes it with
+// expand_direct) or 2 (a dictionary index out of range: status set).
+template <int WIDTH>
+__device__ __forceinline__ int job_keys(const KArgs &a, const TileJob &tj, const ExRec &rc, uint32_t *kspan,
+                                        int ex_lds, uint32_t (&key)[2][EX_ROWS / 2][4]) {
+  constexpr int HR = EX_ROWS / 2;
+  const int lane = lane_id();
+  const int32_t v0 = rc.v0, lim = rc.lim;
+  const int bw = rc.bw;
+  const uint8_t *ks = rc.vals + 1;
+  const int64_t slen = (int64_t)rc.val_len - 1;
+  RunWin W;
+  W.load(rc.runs, rc.nr, rc.first_run);
+  const int64_t byte_lo = rc.byte_lo, byte_hi = (int64_t)rc.byte_hi + 16;
+  const uintptr_t A = ((uintptr_t)ks + (uintptr_t)byte_lo) & ~(uintptr_t)15;
+  const int64_t nb = (int64_t)((uintptr_t)ks + (uintptr_t)byte_hi - A);
+  const bool staged = nb <= ex_lds;
+  if (staged) {
+    const uintptr_t src = A + 16 * (uintptr_t)lane;
+    for (int32_t off = 0; off < nb; off += 1024)
+      if (off + 16 * lane < nb)
+        __builtin_amdgcn_global_load_lds((const void *)(src + off),
+                                         (__attribute__((address_space(3))) void *)(kspan + off / 4), 16, 0, 0);
+  }
+  const int32_t rs = W.start > v0 && W.start < lim && ((W.start - v0) & (EX_ROW - 1)) ? (W.start - v0) / EX_ROW : -1 - lane;
+  const int32_t rs_next = (int32_t)shfl32((uint32_t)rs, min(lane + 1, 63));
+  const bool fits = staged && (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, 63) >= lim &&
+                    !ballot(lane < 63 && rs >= 0 && rs == rs_next);
+  if (!fits) return 1;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the staged bytes (LDS-DMA) and the window
+  const int64_t lbase = (int64_t)(A - (uintptr_t)ks) * 8;
+  const int32_t end_bit32 = (int32_t)(slen * 8);
+  const uint32_t mask = bw >= 32 ? 0xffffffffu : ((1u << bw) - 1);
+  const int32_t w_end = (int32_t)shfl32((uint32_t)W.start, min(lane + 1, 63));
+  const int32_t w_c = (int32_t)(W.prm * 8) - W.start * bw - (int32_t)lbase;
+  const uint64_t okm = ballot(!W.rle && W.start != 0x7fffffff &&
+                              (int64_t)W.prm * 8 + (int64_t)(min(w_end, lim) - W.start) * bw <= slen * 8);
+  bool bad = false;
+  uint32_t kmax = 0;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+#pragma unroll
+    for (int r = 0; r < HR; r++) {
+      const int32_t rl = v0 + (h * HR + r) * EX_ROW;
+      const int32_t j0 = rl + 4 * lane;
+#pragma unroll
+      for (int q = 0; q < 4; q++) key[h][r][q] = 0;
+      if (rl >= lim) continue;
+      const int32_t rh = min(rl + EX_ROW, lim);
+      const uint64_t m = ballot(W.start <= rl);
+      const int32_t ri = max((int32_t)__popcll(m) - 1, 0);
+      const int32_t s1 = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, ri + 1);
+      const int32_t c0 = (int32_t)__builtin_amdgcn_readlane((uint32_t)w_c, ri);
+      const bool one = s1 >= rh;
+      const bool fast = ((okm >> ri) & 1) && (one || ((okm >> (ri + 1)) & 1)) && rh - rl == EX_ROW;
+      if (fast) {  // full row, bit-packed runs only, nothing past the stream end
+        const int32_t c1 = one ? c0 : (int32_t)__builtin_amdgcn_readlane((uint32_t)w_c, ri + 1);
+        const uint32_t lb0 = (uint32_t)((j0 >= s1 ? c1 : c0) + j0 * bw);
+        if (bw <= 8) row_keys<0>(kspan, lb0, bw, mask, key[h][r]);
+        else if (bw <= 16) row_keys<1>(kspan, lb0, bw, mask, key[h][r]);
+        else row_keys<2>(kspan, lb0, bw, mask, key[h][r]);
+        if (!one && j0 < s1 && j0 + 3 >= s1) {  // the one lane of the row where a run starts
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            const int32_t j = j0 + q;
+            const uint32_t lb = (uint32_t)((j >= s1 ? c1 : c0) + j * bw);
+            const uint32_t *dq = kspan + (lb >> 5);
+            key[h][r][q] = __builtin_amdgcn_alignbit(dq[1], dq[0], lb & 31) & mask;
+          }
+        }
+        kmax = max(kmax, max(max(key[h][r][0], key[h][r][1]), max(key[h][r][2], key[h][r][3])));
+        continue;
+      }
+      const int32_t s0 = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, ri);
+      const uint32_t p0 = __builtin_amdgcn_readlane(W.prm, ri), f0 = __builtin_amdgcn_readlane(W.rle, ri);
+      const uint32_t p1 = __builtin_amdgcn_readlane(W.prm, ri + 1), f1 = __builtin_amdgcn_readlane(W.rle, ri + 1);
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int32_t j = j0 + q;
+        const bool act = j < lim;
+        const bool sel = j >= s1;
+        const uint32_t pr = sel ? p1 : p0, fr = sel ? f1 : f0;
+        const int32_t sr = sel ? s1 : s0;
+        const int32_t bb = (int32_t)pr * 8 + (j - sr) * bw;
+        const uint32_t lb = (fr || !act) ? 0u : (uint32_t)(bb - (int32_t)lbase);
+        const uint32_t *dw = kspan + (lb >> 5);
+        uint32_t kv = __builtin_amdgcn_alignbit(dw[1], dw[0], lb & 31) & mask;
+        const int32_t avail = end_bit32 - bb;  // zero-fill past the stream end (hybrid_decoder.go:133-141)
+        kv &= avail >= bw ? 0xffffffffu : avail <= 0 ? 0u : ((1u << avail) - 1);
+        kv = fr ? pr : kv;
+        bad |= act && kv >= rc.dict_n;
+        key[h][r][q] = act ? kv : 0u;
+      }
+    }
+  }
+  if (ballot(bad || kmax >= rc.dict_n)) {
+    set_status(a.status, tj.page, ST_VALUES, E_DICT);  // type_dict.go:51-53
+    return 2;
+  }
+  return 0;
+}
+
+template <int WIDTH, int NW>
+__global__ __launch_bounds__(NW * 64) void k_expand_pass(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
+  constexpr int HR = EX_ROWS / 2;
+  typedef typename std::conditional<WIDTH == 4, uint32_t, uint64_t>::type VT;
+  const LdsGroup g = sload(a.lgroups + blockIdx.x);
+  const int wv = (int)ufirst(threadIdx.x >> 6);
+  const int lane = lane_id();
+  const int j = g.job0 + wv;
+  TileJob tj = {};
+  ExRec rc = {};
+  bool act = false;
+  uint32_t key[2][HR][4];
+  VT val[2][HR][4];
+#pragma unroll
+  for (int h = 0; h < 2; h++)
+#pragma unroll
+    for (int r = 0; r < HR; r++)
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        key[h][r][q] = 0;
+        val[h][r][q] = 0;
+      }
+  if (wv < g.njobs) {
+    tj = sload(a.tiles + j);
+    rc = sload(a.recs + j);
+    if (rc.epoch == a.epoch && rc.v0 < rc.lim) {
+      if (rc.bw < 0) {  // PLAIN (a dictionary chunk's fallback page): a copy of the job's bytes
+        copy_tile<EX_WAVE * 8 / 1024>(rc.vals + (int64_t)rc.v0 * WIDTH, tj.out + (int64_t)rc.v0 * WIDTH,
+                                      (int64_t)(rc.lim - rc.v0) * WIDTH, lane);
+      } else {
+        const int k = job_keys<WIDTH>(a, tj, rc, lds_dyn + wv * (g.kspan / 4), g.kspan, key);
+        if (k == 1) {  // outside the staged form: straight from HBM / L2
+          ExPage P;
+          P.nr = rc.nr;
+          P.bw = rc.bw;
+          P.val_len = rc.val_len;
+          P.dict_n = rc.dict_n;
+          P.vals = rc.vals;
+          P.dict = rc.dict;
+          P.runs = rc.runs;
+          for (int32_t c = rc.v0; c < rc.lim; c += 512)
+            expand_direct(a, P, tj.page, WIDTH, tj.out, c, min(c + 512, rc.lim),
+                          a.tile_info[tj.tf + (c - rc.v0) / RUN_TILE].x);
+        }
+        act = k == 0;
+      }
+    }
+  }
+  // the chunk's dictionary (every job of the group has the same one): the
+  // group's first record (written by this decode's k_prepare), or the
+  // dictionary page itself when that job failed or is PLAIN
+  // (no __syncthreads_or here: its static LDS would not fit beside the
+  // launch's 160 KiB; a group whose waves all failed still streams the slices)
+  __syncthreads();  // every wave's staged keys are in registers: the LDS is the slices'
+  if (g.njobs <= 0) return;  // an empty slot of the XCD dealing (block-uniform)
+  const ExRec r0 = sload(a.recs + g.job0);
+  const uint8_t *dict;
+  uint32_t dn;
+  if (r0.epoch == a.epoch && r0.dict) {
+    dict = r0.dict;
+    dn = r0.dict_n;
+  } else {  // a failed or PLAIN first page: the dictionary page itself (its size checked on the host)
+    if (page_status(a.status, g.dpage) != STATUS_OK) return;
+    const PageDesc dp = a.pages[g.dpage];
+    dict = body_ptr(a, dp, g.dpage);
+    dn = (uint32_t)max(dp.num_values, 0);
+  }
+  const uint32_t SE = (uint32_t)(g.dict_bytes / WIDTH);  // entries per slice (the launch's LDS)
+  const uint32_t dsh = (uint32_t)((uintptr_t)dict & 3);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)((uintptr_t)dict & ~(uintptr_t)3), (short)0, (int)((dn * (uint32_t)WIDTH + dsh + 3) & ~3u), 0x00020000);
+  constexpr uint32_t T = NW * 64;
+  for (uint32_t base = 0; base < dn; base += SE) {
+    const uint32_t nbytes = min(dn - base, SE) * (uint32_t)WIDTH;
+    const uint32_t n16 = (nbytes + 15) / 16, b0 = base * (uint32_t)WIDTH;
+    if (base > 0) __syncthreads();  // the previous slice's gathers are done
+    for (uint32_t i0 = threadIdx.x; i0 < n16; i0 += 4 * T) {
+      u32x4 x[4];
+      uint32_t y[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t i = i0 + q * T;
+        x[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, b0 + 16 * i, 0, 0);  // out of range: zeros
+        y[q] = dsh ? __builtin_amdgcn_raw_buffer_load_b32(rs, b0 + 16 * i + 16, 0, 0) : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t i = i0 + q * T;
+        if (i < n16)
+          *(u32x4 *)(lds_dyn + 4 * i) =
+              u32x4{__builtin_amdgcn_alignbyte(x[q].y, x[q].x, dsh), __builtin_amdgcn_alignbyte(x[q].z, x[q].y, dsh),
+                    __builtin_amdgcn_alignbyte(x[q].w, x[q].z, dsh), __builtin_amdgcn_alignbyte(y[q], x[q].w, dsh)};
+      }
+    }
+    __syncthreads();
+    if (act) {
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int r = 0; r < HR; r++)
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            const uint32_t rel = key[h][r][q] - base;
+            if (rel < SE) {
+              if (WIDTH == 4) val[h][r][q] = lds_dyn[rel];
+              else val[h][r][q] = ((const uint64_t *)lds_dyn)[rel];
+            }
+          }
+    }
+  }
+  if (!act) return;
+  // stores: 16 / 32 contiguous bytes per lane per row (as expand_job)
+  const int32_t v0 = rc.v0, lim = rc.lim;
+  const __amdgpu_buffer_rsrc_t ors =
+      __builtin_amdgcn_make_buffer_rsrc((void *)tj.out, (short)0, (int)((uint32_t)lim * (uint32_t)WIDTH), 0x00020000);
+  const bool out_al = ((uintptr_t)tj.out & 15) == 0;
+#pragma unroll
+  for (int h = 0; h < 2; h++)
+#pragma unroll
+    for (int r = 0; r < HR; r++) {
+      const int32_t j0 = v0 + (h * HR + r) * EX_ROW + 4 * lane;
+      const uint32_t off = (uint32_t)j0 * (uint32_t)WIDTH;
+      if (j0 + 4 <= lim && out_al) {
+        if (WIDTH == 4) {
+          __builtin_amdgcn_raw_buffer_store_b128(
+              u32x4{(uint32_t)val[h][r][0], (uint32_t)val[h][r][1], (uint32_t)val[h][r][2], (uint32_t)val[h][r][3]},
+              ors, off, 0, 0);
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b128(
+              u32x4{(uint32_t)val[h][r][0], (uint32_t)((uint64_t)val[h][r][0] >> 32), (uint32_t)val[h][r][1],
+                    (uint32_t)((uint64_t)val[h][r][1] >> 32)},
+              ors, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(
+              u32x4{(uint32_t)val[h][r][2], (uint32_t)((uint64_t)val[h][r][2] >> 32), (uint32_t)val[h][r][3],
+                    (uint32_t)((uint64_t)val[h][r][3] >> 32)},
+              ors, off + 16, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          if (j0 + q >= lim) continue;
+          if (WIDTH == 4) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)val[h][r][q], ors, off + 4 * q, 0, 0);
+          else
+            __builtin_amdgcn_raw_buffer_store_b64(
+                u32x2{(uint32_t)val[h][r][q], (uint32_t)((uint64_t)val[h][r][q] >> 32)}, ors, off + 8 * q, 0, 0);
+        }
+      }
+    }
+}
+
+// ===========================================================================
 // K5m: k_expand_mix — the tiled decode in 256-thread workgroups, one per
 // LdsGroup (host-built, see the planner in pq_host.cpp):
 //  * dpage >= 0: consecutive jobs of one column chunk whose dictionary fits in
@@ -4077,16 +4347,27 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   return k;
 }
 
+// the last failed launch (kernel id, HIP error), for the host's error text
+int pq_launch_fail_which = -1;
+int pq_launch_fail_err = 0;
+static int launch_status(int which) {
+  const hipError_t e = hipGetLastError();
+  if (e == hipSuccess) return 0;
+  pq_launch_fail_which = which;
+  pq_launch_fail_err = (int)e;
+  return 17;
+}
+
 int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
   pq::KArgs k = to_k(p);
   if (which == 4) {
     if (k.ncols <= 0) return 0;
     hipLaunchKernelGGL(pq::k_scan, dim3(k.ncols), dim3(256), 0, s, k);
-    return hipGetLastError() == hipSuccess ? 0 : 17;
+    return launch_status(which);
   }
   if (which == 13) {  // k_reset
     hipLaunchKernelGGL(pq::k_reset, dim3(64, 1 + (k.nzr > 0 ? k.nzr : 0)), dim3(256), 0, s, k);
-    return hipGetLastError() == hipSuccess ? 0 : 17;
+    return launch_status(which);
   }
   if (which == 12) {  // k_prepare_copy: the prepare blocks, then the copy grid
     const uint32_t items = k.max_jobs * pq::COPY_ITEMS;
@@ -4094,22 +4375,43 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     const uint32_t pb = ((uint32_t)(k.nlist > 0 ? k.nlist : 0) + 3) / 4;
     if (pb + cb == 0) return 0;
     hipLaunchKernelGGL(pq::k_prepare_copy, dim3(pb + (cb ? cb : 1)), dim3(256), 0, s, k);
-    return hipGetLastError() == hipSuccess ? 0 : 17;
+    return launch_status(which);
   }
   if (which == 6) {  // deferred literal copies: fixed grid, the job count lives on the device
     if (k.max_jobs == 0) return 0;
     const uint32_t items = k.max_jobs * pq::COPY_ITEMS;
     hipLaunchKernelGGL(pq::k_copy, dim3(items < 4096 ? items : 4096), dim3(256), 0, s, k);
-    return hipGetLastError() == hipSuccess ? 0 : 17;
+    return launch_status(which);
   }
-  if (which == 9 || which == 22) {  // k_expand_mix (9) / k_expand_big (22): one workgroup per LdsGroup
+  if (which == 9 || which == 22 || which == 27) {  // k_expand_mix (9) / _big (22) / _pass (27): one workgroup per LdsGroup
     static bool attr = false;
     if (!attr) {
+      hipFuncSetAttribute((const void *)pq::k_expand_pass<4, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      hipFuncSetAttribute((const void *)pq::k_expand_pass<4, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      hipFuncSetAttribute((const void *)pq::k_expand_pass<8, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      hipFuncSetAttribute((const void *)pq::k_expand_pass<8, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       hipFuncSetAttribute((const void *)pq::k_expand_mix<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       hipFuncSetAttribute((const void *)pq::k_expand_mix<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       hipFuncSetAttribute((const void *)pq::k_expand_big<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       hipFuncSetAttribute((const void *)pq::k_expand_big<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr = true;
+    }
+    if (which == 27) {
+      // k_expand_pass: groups after the mixed ones, absolute job indices; g.dict_bytes = slice bytes
+      const pq::LdsGroup *pg = (const pq::LdsGroup *)p->lgroups + p->ldn[0] + p->ldn[1] + p->ldn[2] + p->ldn[3];
+      const int nw = pq::pass_waves(4);
+      for (int w = 0; w < 2; w++) {
+        if (p->ldn[4 + w] <= 0) continue;
+        pq::KArgs kb = k;
+        kb.lgroups = pg + (w ? p->ldn[4] : 0);
+        const dim3 grid(p->ldn[4 + w]);
+        const size_t lds = (size_t)p->ldl[4 + w];
+        if (w == 0 && nw == 16) hipLaunchKernelGGL((pq::k_expand_pass<4, 16>), grid, dim3(16 * 64), lds, s, kb);
+        else if (w == 0) hipLaunchKernelGGL((pq::k_expand_pass<4, 8>), grid, dim3(8 * 64), lds, s, kb);
+        else if (nw == 16) hipLaunchKernelGGL((pq::k_expand_pass<8, 8>), grid, dim3(8 * 64), lds, s, kb);
+        else hipLaunchKernelGGL((pq::k_expand_pass<8, 4>), grid, dim3(4 * 64), lds, s, kb);
+      }
+      return launch_status(which);
     }
     if (which == 22) {
       // k_expand_big: big-dictionary groups after the mixed ones, absolute job indices
@@ -4123,7 +4425,7 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
       else
         hipLaunchKernelGGL(pq::k_expand_big<8>, dim3(p->ldn[3]), dim3(pq::BIG_WAVES * 64), (size_t)p->ldl[3], s, kb);
       }
-      return hipGetLastError() == hipSuccess ? 0 : 17;
+      return launch_status(which);
     }
     const dim3 blk(pq::LD_WAVES_H * 64);
     if (p->ldn[0] > 0) hipLaunchKernelGGL(pq::k_expand_mix<4>, dim3(p->ldn[0]), blk, (size_t)p->ldl[0], s, k);
@@ -4133,18 +4435,18 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
       k.recs = (pq::ExRec *)p->recs + (size_t)p->ldn[0] * pq::LD_WAVES_H;           // are launch-relative
       hipLaunchKernelGGL(pq::k_expand_mix<8>, dim3(p->ldn[1]), blk, (size_t)p->ldl[1], s, k);
     }
-    return hipGetLastError() == hipSuccess ? 0 : 17;
+    return launch_status(which);
   }
   if (which == 0) {  // k_snappy over work items (pages, or segments of long pages)
     if (k.nitems <= 0) return 0;
     hipLaunchKernelGGL(pq::k_snappy<pq::SNAP_ITEMS>, dim3((k.nitems + 3) / 4), dim3(256), 0, s, k);
-    return hipGetLastError() == hipSuccess ? 0 : 17;
+    return launch_status(which);
   }
   if (which == 17 || which == 18) {  // k_snappy_walk / serial fallback over the segmented pages
     if (k.nwalk <= 0) return 0;
     if (which == 17) hipLaunchKernelGGL(pq::k_snappy_walk, dim3(k.nwalk), dim3(64), 0, s, k);
     else hipLaunchKernelGGL(pq::k_snappy<pq::SNAP_FALLBACK>, dim3((k.nwalk + 3) / 4), dim3(256), 0, s, k);
-    return hipGetLastError() == hipSuccess ? 0 : 17;
+    return launch_status(which);
   }
   if (k.nlist <= 0) return 0;
   dim3 grid((k.nlist + 3) / 4), block(256);
@@ -4166,9 +4468,11 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     case 5: hipLaunchKernelGGL(pq::k_level_check, grid, block, 0, s, k); break;
     case 10: hipLaunchKernelGGL(pq::k_dba, grid, block, 0, s, k); break;
     case 23: hipLaunchKernelGGL(pq::k_plain_str, grid, block, 0, s, k); break;
-    default: return 1;
+    default:
+      pq_launch_fail_which = which;
+      return 1;
   }
-  return hipGetLastError() == hipSuccess ? 0 : 17;
+  return launch_status(which);
 }
 
 }  // extern "C"
