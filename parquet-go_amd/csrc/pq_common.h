@@ -40,6 +40,11 @@ enum : uint32_t {
   ST_REP = 16,        // decodePackedArray(rDecoder) page_v1.go:37
   ST_DEF = 17,
   ST_VALUES = 18,     // valuesDecoder.decodeValues page_v1.go:48-52
+  // device-internal: a k_decode<3> part after the first met an error; the
+  // page is decoded again whole (serially) by the redo launch, which replaces
+  // this with the reference's status.  Above every real stage: a real status
+  // from the page's first part wins the atomicMin.
+  ST_REDO = 0x7FFF,
 };
 __host__ __device__ inline uint32_t make_status(uint32_t stage, uint32_t code) { return (stage << 16) | code; }
 constexpr uint32_t STATUS_OK = 0xFFFFFFFFu;

@@ -63,6 +63,13 @@ __device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {  // wrappin
   }
   return v;
 }
+// wave sum (uniform)
+__device__ __forceinline__ int32_t wave_sum32(int32_t v) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += (int32_t)shfl32((uint32_t)v, lane ^ d);
+  return (int32_t)ufirst((uint32_t)v);
+}
 // exclusive wave prefix sum; *total receives the wave total (uniform)
 __device__ __forceinline__ int32_t wave_excl_scan32(int32_t v, int32_t *total) {
   int32_t incl = wave_incl_scan32_impl(v);
@@ -611,6 +618,53 @@ struct HybT {
       }
       rem -= take;
       left -= take;
+      vdone += take;
+    }
+    return E_OK;
+  }
+
+  // Consume the next k values without producing them (a k_decode part that
+  // starts mid-page seeks its key stream here).  Runs are stepped over by
+  // their headers; after a bit-packed run, a train of identical headers (an
+  // encoder's stream of high-entropy keys) is accepted up to 64 runs a step,
+  // lane j checking the header one stride j further.  Returns an error where
+  // reading the values would fail (the caller then leaves the page to a
+  // whole-page decode that reports the reference's error).
+  __device__ uint32_t skip(int64_t k) {
+    const int lane = lane_id();
+    if (bw == 0 || k <= 0) {
+      vdone += k > 0 ? k : 0;
+      return E_OK;
+    }
+    while (k > 0) {
+      if (rem == 0) {
+        const int64_t h0 = pos;
+        const uint32_t e = header();
+        if (e) return e;
+        if (!rle && rem < k) {
+          // this run is skipped whole; try the train of identical headers after it
+          const int64_t hl = data - h0, g = rem >> 3, stride = hl + g * (int64_t)bw;
+          const int64_t c = pos + (int64_t)lane * stride;  // candidate header of run + 1 + lane
+          bool ok = (int64_t)(lane + 1) * rem < k - rem + 1 && c + stride <= len;
+          if (ok)
+            for (int q = 0; q < (int)hl; q++) ok &= p[c + q] == p[h0 + q];
+          const uint64_t okm = ballot(ok);
+          const int m = ~okm ? (int)__builtin_ctzll(~okm) : 64;
+          if (m > 0) {
+            pos += (int64_t)m * stride;
+            k -= (int64_t)m * rem;
+            vdone += (int64_t)m * rem;
+          }
+        }
+      }
+      const int64_t take = min<int64_t>(rem, k);
+      if (!rle) {
+        const int ok = readable((int)take);
+        if (ok < take) return E_EOF;
+        vi += take;
+      }
+      rem -= take;
+      k -= take;
       vdone += take;
     }
     return E_OK;

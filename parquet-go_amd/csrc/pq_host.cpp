@@ -89,6 +89,8 @@ struct pq_launch_args {
   const int32_t *walk, *seg_base;
   int64_t *segs;
   uint32_t *seg_flag;
+  const int32_t *parts;  // k_decode<3>: (page, first level, end level) triplets instead of `list`
+  int32_t redo;          // k_decode<3>: decode again (whole) the pages whose parts failed
 };
 int pq_launch(int which, const pq_launch_args *p, hipStream_t s);
 extern int pq_launch_fail_which, pq_launch_fail_err;
@@ -715,6 +717,7 @@ struct pqg_batch {
   std::vector<int32_t> general_nest;  // k_decode<3> pages (lists of fixed-width values), appended last
   int32_t ngen_flat = 0, ngen_str = 0, ngen_nest = 0;
   std::vector<int32_t> dba_list;      // DELTA_BYTE_ARRAY pages: value bytes by k_dba
+  std::vector<int32_t> nest_parts;    // k_decode<3> waves: (page, first level, end level) triplets
   std::vector<int32_t> pstr_items;    // k_plain_str: (page, first value) pairs of flat required PLAIN strings
   bool data_may_defer = false;        // some data page's Snappy body may hold a deferred literal
   std::vector<TileJob> tiles;         // k_expand work list (XCD-affine order)
@@ -736,6 +739,7 @@ struct pqg_batch {
   ColDesc *d_cols = nullptr;
   uint64_t *d_dict = nullptr;
   int32_t *d_lists = nullptr;
+  int32_t *d_parts = nullptr;  // nest_parts on the device
   void *d_jobs = nullptr;        // deferred long-literal copy jobs (k_snappy -> k_copy)
   uint32_t *d_njobs = nullptr;   // per Snappy page: jobs written
   int32_t *d_job_base = nullptr, *d_job_owner = nullptr;
@@ -745,6 +749,10 @@ struct pqg_batch {
   int32_t *d_lens = nullptr;       // DELTA string pages: length scratch
   int64_t lens_entries = 0;
   int64_t lvl_bytes = 0;     // decoded-level scratch (PageDesc::lvl_base)
+  // a level page whose streams sit in a compressed V1 body, or whose chunk has
+  // a dictionary: k_levels must follow the Snappy phase; otherwise (V2 pages:
+  // raw level bytes) it runs beside it (lvl_early)
+  bool lvl_late = false;
   uint8_t *d_lvl = nullptr;
   uint64_t *d_dbg = nullptr;     // diagnostic stamps (PQ_STAMPS builds only)
   uint64_t *d_dbg2 = nullptr;
@@ -1565,6 +1573,7 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
       if (L.max_def > 0 && L.max_def < 256 && d.num_values > 0) {
         B->pages.back().lvl_base = B->lvl_bytes;
         B->lvl_bytes += (((int64_t)(L.max_rep > 0 ? 2 : 1) * d.num_values) + 15) & ~(int64_t)15;
+        if (d.kind != PAGE_V2 || d.dict >= 0) B->lvl_late = true;
       }
       if ((L.physical_type == T_BYTE_ARRAY && (d.enc == ENC_DELTA_LBA || d.enc == ENC_DELTA_BA)) ||
           (L.physical_type == T_FLBA && d.enc == ENC_DELTA_BA)) {
@@ -2192,6 +2201,34 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   B->general_list.insert(B->general_list.end(), B->general_str.begin(), B->general_str.end());
   B->general_str.clear();
   B->ngen_nest = (int32_t)B->general_nest.size();
+  {
+    // list pages split into parts of whole 256-entry steps, one k_decode<3>
+    // wave each, up to about a wave per SIMD (1,024) for the batch: a batch
+    // of few list pages (a stream slice) otherwise leaves most SIMDs idle.
+    // Past that it does not pay: C4 (1,012 pages) in 4,096 parts took as long
+    // (2.27 vs 2.30 ms), its waves are issue-bound, not chain-bound.  A part
+    // counts what comes before it from the level bytes and seeks the key
+    // stream, so only pages with level scratch and PLAIN / RLE_DICTIONARY
+    // values are split.  PQG_NEST_PART: entries per part (0: whole pages).
+    int64_t tot = 0;
+    for (int32_t pg : B->general_nest) tot += std::max(B->pages[(size_t)pg].num_values, 0);
+    const int64_t env_part = getenv("PQG_NEST_PART") ? atoll(getenv("PQG_NEST_PART")) : -1;
+    int64_t plen = env_part >= 0 ? env_part : std::max<int64_t>(8192, (tot / 1024 + 255) & ~(int64_t)255);
+    if (plen > 0) plen = (plen + 255) & ~(int64_t)255;
+    B->nest_parts.clear();
+    for (int32_t pg : B->general_nest) {
+      const PageDesc &pd = B->pages[(size_t)pg];
+      const int64_t n = std::max(pd.num_values, 0);
+      const int64_t np = plen > 0 && pd.lvl_base >= 0 && (pd.enc == ENC_RLE_DICT || pd.enc == ENC_PLAIN) ? n / plen : 1;
+      const int64_t step = np > 1 ? ((n + np - 1) / np + 255) & ~(int64_t)255 : std::max<int64_t>(n, 1);
+      for (int64_t e = 0; e < n || e == 0; e += step) {
+        B->nest_parts.push_back(pg);
+        B->nest_parts.push_back((int32_t)e);
+        B->nest_parts.push_back((int32_t)std::min(e + step, n));
+        if (n == 0) break;
+      }
+    }
+  }
   B->general_list.insert(B->general_list.end(), B->general_nest.begin(), B->general_nest.end());
   B->general_nest.clear();
   {
@@ -2218,6 +2255,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     tab.put((void **)&B->d_pages, B->pages.data(), sizeof(PageDesc) * npages);
     tab.put((void **)&B->d_status0, B->status0.data(), sizeof(uint32_t) * npages);
     tab.put((void **)&B->d_lists, lists.data(), sizeof(int32_t) * lists.size());
+    tab.put((void **)&B->d_parts, B->nest_parts.data(), sizeof(int32_t) * B->nest_parts.size());
     tab.put((void **)&B->d_lgroups, B->lgroups.data(), sizeof(LdsGroup) * (B->lgroups.size() + 1));
     tab.put((void **)&B->d_page_jobs, pj.data(), sizeof(int32_t) * pj.size());
     tab.put((void **)&B->d_sitems, B->snap_items.data(), 4 * B->snap_items.size());
@@ -2525,8 +2563,32 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   auto mark = [&](bool decode_edge) {
     if (timed && (B->seg_times || decode_edge)) hipEventRecord(evs[B->nev++], s);
   };
+  // k_levels with two waves a page (repetition and definition streams side by
+  // side) when a selected column is repeated: C4's lists 2.05 -> 1.61 ms; a
+  // flat batch keeps four pages a workgroup (C3's def-only pages: 0.77 vs 0.96 ms)
+  bool any_rep = false;
+  for (const auto &cp : B->cols) any_rep |= cp.info.max_rep > 0;
+  const int lv_id = any_rep ? 24 : 19;
+  // V2 level streams are raw bytes of the chunk: with no page waiting on a
+  // dictionary, k_levels needs nothing the Snappy phase writes and runs beside
+  // it on a side stream (C3: its 0.73 ms left the critical path)
+  // PQG_LEVELS_LATE=1 (analysis): k_levels back after the Snappy phase
+  static const bool lvl_late_env = getenv("PQG_LEVELS_LATE") != nullptr;
+  const bool lvl_early = !resume && B->lvl_bytes > 0 && !B->lvl_late && !B->seg_times && !lvl_late_env;
   if (!resume) {
   mark(false);
+  // (k_levels first on the context stream with k_snappy on the side stream
+  // was measured slower on C3: 6.4 vs 5.3 ms, the two launches' waves
+  // sharing every CU for the whole phase)
+  if (lvl_early) {
+    pq_launch_args al = a;
+    al.list = B->d_lists + ns + nd;
+    al.nlist = ndata;
+    hipEventRecord(B->ctx->fork, s);
+    hipStreamWaitEvent(B->ctx->side[2], B->ctx->fork, 0);
+    e |= pq_launch(lv_id, &al, B->ctx->side[2]);  // k_levels<-1>: every level page
+    hipEventRecord(B->ctx->join[2], B->ctx->side[2]);
+  }
   a.list = B->d_lists;
   a.nlist = ns;
   a.sitems = B->d_sitems;
@@ -2560,6 +2622,9 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     }();
     hipStream_t ss = side && walk_side ? ctx->side[0] : s;   // the serial chain
     hipStream_t sw = side && !walk_side ? ctx->side[0] : s;  // whole data pages
+    // (the whole dictionary pages and k_dict_prepare stay on the chain: a
+    // BYTE_ARRAY dictionary page may itself be segmented — C5's l_comment
+    // dictionaries — and k_dict_prepare reads what its segments write)
     if (side) {
       hipEventRecord(ctx->fork, s);
       hipStreamWaitEvent(ctx->side[0], ctx->fork, 0);
@@ -2603,19 +2668,15 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   // in one launch and those pages after it (with string dictionaries, the
   // string pages would all wait: measured slower)
   const bool fused = nd == 0 && B->max_jobs > 0 && !B->seg_times;
-  // k_levels with two waves a page (repetition and definition streams side by
-  // side) when a selected column is repeated: C4's lists 2.05 -> 1.61 ms; a
-  // flat batch keeps four pages a workgroup (C3's def-only pages: 0.77 vs 0.96 ms)
-  bool any_rep = false;
-  for (const auto &cp : B->cols) any_rep |= cp.info.max_rep > 0;
-  const int lv_id = any_rep ? 24 : 19;
+  if (lvl_early) hipStreamWaitEvent(s, B->ctx->join[2], 0);  // the levels and counts k_prepare reads
+  const bool lvl_now = B->lvl_bytes && !lvl_early;
   if (fused) {
     a.list = B->d_lists + ns + nd;
     a.nlist = ndata;
-    if (B->lvl_bytes) e |= pq_launch(lv_id + 1, &a, s);  // k_levels: pages that do not wait on k_copy
+    if (lvl_now) e |= pq_launch(lv_id + 1, &a, s);  // k_levels: pages that do not wait on k_copy
     e |= pq_launch(12, &a, s);  // k_prepare_copy (+ the run walk of tiled RLE_DICTIONARY pages)
     if (B->data_may_defer) {    // pages that waited on k_copy
-      if (B->lvl_bytes) e |= pq_launch(lv_id + 2, &a, s);
+      if (lvl_now) e |= pq_launch(lv_id + 2, &a, s);
       e |= pq_launch(11, &a, s);
     }
   } else {
@@ -2629,7 +2690,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     mark(false);
     a.list = B->d_lists + ns + nd;
     a.nlist = ndata;
-    if (B->lvl_bytes) e |= pq_launch(lv_id, &a, s);  // k_levels
+    if (lvl_now) e |= pq_launch(lv_id, &a, s);  // k_levels
     e |= pq_launch(2, &a, s);  // (+ the run walk of tiled RLE_DICTIONARY pages)
   }
   mark(false);
@@ -2670,12 +2731,26 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
       hipStreamWaitEvent(ctx->side[2], ctx->fork, 0);
       a.list = B->d_lists + ns + nd + ndata + ng0 + B->ngen_flat + B->ngen_str;
       a.nlist = B->ngen_nest;
-      e |= pq_launch(16, &a, ctx->side[2]);  // k_decode<3>: lists of fixed-width values
+      const int32_t nparts = (int32_t)(B->nest_parts.size() / 3);
+      if (nparts > B->ngen_nest) {
+        pq_launch_args ap = a;
+        ap.parts = B->d_parts;
+        ap.nlist = nparts;
+        e |= pq_launch(16, &ap, ctx->side[2]);  // k_decode<3>: parts of list pages of fixed-width values
+        ap = a;
+        ap.redo = 1;
+        e |= pq_launch(16, &ap, ctx->side[2]);  // k_decode<3>: pages whose later parts failed, whole
+      } else {
+        e |= pq_launch(16, &a, ctx->side[2]);  // k_decode<3>: lists of fixed-width values
+      }
       hipEventRecord(ctx->join[2], ctx->side[2]);
     }
     a.list = B->d_lists + ns + nd + ndata;
     a.nlist = ng0;
     e |= pq_launch(3, &a, s);  // k_decode<0>: lists of strings, booleans, level output
+    // (k_plain_str beside k_decode<2> on another side stream, and the tiled
+    // expand beside both, were measured on C5: 24.50 vs 24.28 ms — the three
+    // are throughput-bound and only slowed each other)
     if (str_side) hipStreamWaitEvent(s, ctx->join[1], 0);
     if (!B->dba_list.empty()) {  // DELTA_BYTE_ARRAY value bytes (after k_decode's offsets)
       a.list = B->d_lists + ns + nd + ndata + ngen;

@@ -90,6 +90,8 @@ struct KArgs {
   const int32_t *seg_base;  // per Snappy-list position: first entry in segs (nseg = next - this)
   int64_t *segs;          // per segment: stream offset of its first token (k_snappy_walk)
   uint32_t *seg_flag;     // per Snappy-list position: 0 segments ok, 1 serial fallback, 2 nothing to do
+  const int32_t *parts;   // k_decode<3>: (page, first level, end level) per wave, instead of `list`
+  int32_t redo;           // k_decode<3>: the pages left at ST_REDO by their parts, decoded whole
 };
 
 #ifdef PQ_STAMPS
@@ -2672,8 +2674,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   const int gi = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
   if (gi >= a.nlist) return;
   const int lane = lane_id();
-  const int page = ufirst(a.list[gi]);
-  if (page_status(a.status, page) != STATUS_OK) return;
+  // KIND 3 with a.parts: this wave decodes level entries [e_lo, e_hi) of its
+  // page (a list page has ~80k entries: one wave per page left most of the
+  // GPU idle, C4).  Rows, slots and values before e_lo are counted from
+  // k_levels' level bytes, the key stream is skipped to the part's first
+  // value.  A part after the first that meets an error marks the page
+  // ST_REDO, and the redo launch decodes it whole for the reference's status.
+  const bool part = KIND == 3 && a.parts != nullptr;
+  int page;
+  int64_t e_lo = 0, e_hi = 0x7fffffffffffll;
+  if (part) {
+    page = ufirst(a.parts[3 * gi]);
+    e_lo = ufirst(a.parts[3 * gi + 1]);
+    e_hi = ufirst(a.parts[3 * gi + 2]);
+  } else {
+    page = ufirst(a.list[gi]);
+  }
+  if (KIND == 3 && a.redo) {
+    if (page_status(a.status, page) != make_status(ST_REDO, 0)) return;
+    if (lane == 0) __hip_atomic_store(&a.status[page], STATUS_OK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (page_status(a.status, page) != STATUS_OK) {
+    return;
+  }
   const PageDesc d = a.pages[page];
   if (d.dict >= 0 && page_status(a.status, d.dict) != STATUS_OK) return;
   const ColDesc c = a.cols[d.col];
@@ -2737,8 +2759,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   const int64_t slot_base = flat ? d.level_base : pi.slot_base;
   int64_t e0 = 0, slot_run = 0, row_run = 0, nn_run = 0, str_run = pi.str_base;
   uint32_t err = E_OK, err_stage = 0;
+  const int64_t e_end = part ? min<int64_t>(e_hi, (int64_t)n) : (int64_t)n;
+  if (part && e_lo > 0) {
+    // rows (rep 0), slots (def >= rep_def) and values (def == max_def) of the
+    // entries before the part: 16 level bytes of each stream a lane a pass
+    const uint8_t *lr = a.lvl + d.lvl_base, *ld = lr + n;
+    const uint32_t dsh = (uint32_t)((uintptr_t)ld & 3);
+    const uint32_t *la = (const uint32_t *)lr, *da = (const uint32_t *)((uintptr_t)ld & ~(uintptr_t)3);
+    int32_t cr = 0, cs = 0, cn = 0;
+    for (int64_t b = 16 * (int64_t)lane; b < e_lo; b += 1024) {
+      uint32_t rw[4], dw[5];
+#pragma unroll
+      for (int q = 0; q < 4; q++) rw[q] = la[(b >> 2) + q];
+#pragma unroll
+      for (int q = 0; q < 5; q++) dw[q] = da[(b >> 2) + q];
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        const bool in = b + q < e_lo;
+        const uint32_t rv = __builtin_amdgcn_ubfe(rw[q >> 2], 8 * (q & 3), 8);
+        const uint32_t dx = __builtin_amdgcn_alignbyte(dw[(q >> 2) + 1], dw[q >> 2], dsh);
+        const uint32_t dv = __builtin_amdgcn_ubfe(dx, 8 * (q & 3), 8);
+        cr += in && rv == 0;
+        cs += in && (int)dv >= c.rep_def;
+        cn += in && (int)dv == c.max_def;
+      }
+    }
+    row_run = wave_sum32(cr);
+    slot_run = wave_sum32(cs);
+    nn_run = wave_sum32(cn);
+    e0 = e_lo;
+    if (d.enc == ENC_RLE_DICT && keys.skip(nn_run) != E_OK) {
+      set_status(a.status, page, ST_REDO, 0);
+      return;
+    }
+  }
 
-  while (e0 < n) {
+  while (e0 < e_end) {
     const int cnt = (int)min<int64_t>(n - e0, flat ? 256 - ((slot_base + e0) & 255) : 256);
     uint32_t r[4] = {0, 0, 0, 0}, dl[4] = {0, 0, 0, 0};
     if (d.lvl_base >= 0) {  // decoded (and checked) by k_prepare's level walk
@@ -3173,7 +3229,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   // a later-found level error can outrank this one: k_level_check re-walks
   // the earlier level streams (the reference decodes all rep levels, then all
   // def levels, then the values, page_v1.go:37-52)
-  if (err) set_status(a.status, page, err_stage, err);
+  if (err) {
+    if (part && e_lo > 0) set_status(a.status, page, ST_REDO, 0);  // the redo launch finds the first error
+    else set_status(a.status, page, err_stage, err);
+  }
 }
 
 // Wave copy of up to MAXC KiB, in passes of 4 KiB with every load of a pass
@@ -4297,6 +4356,8 @@ struct pq_launch_args {
   const int32_t *walk, *seg_base;
   int64_t *segs;
   uint32_t *seg_flag;
+  const int32_t *parts;  // k_decode<3>: (page, first level, end level) triplets instead of `list`
+  int32_t redo;          // k_decode<3>: decode again (whole) the pages whose parts failed
 };
 
 static pq::KArgs to_k(const pq_launch_args *p) {
@@ -4344,6 +4405,8 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   k.epoch = p->epoch;
   k.tiles = (const pq::TileJob *)p->tiles;
   k.lgroups = (const pq::LdsGroup *)p->lgroups;
+  k.parts = p->parts;
+  k.redo = p->redo;
   return k;
 }
 

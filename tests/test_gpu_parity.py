@@ -314,6 +314,49 @@ def test_generated_lists():
     check_file(_pq_bytes(t, compression="snappy", row_group_size=25000, data_page_version="2.0"), "lists v2")
 
 
+@pytest.mark.parametrize("part", ["256", "768", "0"])
+def test_list_page_parts(part):
+    """k_decode<3> over parts of list pages (PQG_NEST_PART level entries a
+    wave; 0 = a wave per page): each part counts the rows / slots / values
+    before it from k_levels' bytes and seeks the key stream (HybS::skip,
+    trains of identical bit-packed headers 64 runs a step).  Dictionary and
+    PLAIN values, nulls at both levels, V1 and V2, bit-exact against the
+    oracle; then seeded corruptions of uncompressed list pages, where a part
+    after the first that fails leaves the page to the whole-page redo launch:
+    the GPU reports the oracle's first error."""
+    pa = pytest.importorskip("pyarrow")
+    pq = pytest.importorskip("pyarrow.parquet")
+    rng = np.random.default_rng(60)
+    n = 30000
+    lists = [None if rng.random() < 0.05 else [None if rng.random() < 0.05 else int(v)
+                                                for v in rng.integers(-3000, 3000, rng.poisson(4))] for _ in range(n)]
+    l64 = [None if x is None else [None if v is None else v * 977 for v in x] for x in lists]
+    t = pa.table({"d": pa.array(lists, pa.list_(pa.int32())), "p": pa.array(l64, pa.list_(pa.int64()))})
+    os.environ["PQG_NEST_PART"] = part
+    try:
+        for ver in ("1.0", "2.0"):
+            check_file(_pq_bytes(t, compression="snappy", row_group_size=15000, data_page_version=ver,
+                                 use_dictionary=["d"]), "list parts %s v%s" % (part, ver))
+        base = _pq_bytes(t.select(["d"]), compression="none", row_group_size=n, data_page_size=16 << 10)
+        cc = pq.ParquetFile(io.BytesIO(base)).metadata.row_group(0).column(0)
+        lo, hi = cc.data_page_offset, cc.dictionary_page_offset + cc.total_compressed_size
+        outcomes = set()
+        for trial in range(16):
+            data = bytearray(base)
+            for _ in range(int(rng.integers(1, 3))):
+                p = int(rng.integers(lo + 32, hi))
+                data[p] ^= int(rng.integers(1, 256))
+            check_file(bytes(data), "list parts %s corrupt %d" % (part, trial))
+            try:
+                oracle.File(bytes(data)).decode(0)
+                outcomes.add(0)
+            except oracle.OracleError as e:
+                outcomes.add(e.code)
+        assert len(outcomes) >= 2, outcomes
+    finally:
+        del os.environ["PQG_NEST_PART"]
+
+
 def _req_table(cols):
     pa = pytest.importorskip("pyarrow")
     return pa.table({k: pa.array(v) for k, v in cols.items()},
@@ -390,7 +433,16 @@ def test_c5_lineitem_large_string_dictionary(tmp_path):
     dictionary page holds ~30k strings (k_dict_prepare on a large string
     dictionary) before the PLAIN fallback; 16 leaves side by side."""
     pytest.importorskip("pyarrow")
-    check_file(_c5_bytes(tmp_path, 80000, 40000), "c5 default dict")
+    data = _c5_bytes(tmp_path, 80000, 40000)
+    check_file(data, "c5 default dict")
+    # the ~1 MiB string dictionary pages themselves cut into Snappy segments:
+    # k_dict_prepare must follow the segment chain (an early, side-stream
+    # k_dict_prepare read them undecoded: an illegal access on the full C5)
+    os.environ["PQG_SNAPPY_SEG_MIN"] = "65537"
+    try:
+        check_file(data, "c5 default dict, segmented dictionary pages")
+    finally:
+        del os.environ["PQG_SNAPPY_SEG_MIN"]
 
 
 @pytest.mark.parametrize("per,depth", [(1, 2), (2, 1), (3, 3)])

@@ -3,6 +3,8 @@ of a short `bench.py --child` run): per launch, its stream queue, start and
 end relative to the step's k_reset, and duration.
 
 usage: python tools/timeline.py CONFIG [extra bench args]   (on the GPU box)
+       python tools/timeline.py --csv KERNEL_TRACE.csv [NAME]  (a kept trace, e.g.
+       profiles/r03/*/rocprof_kernel_trace_c5.csv from bench.py's own child run)
 """
 import csv
 import glob
@@ -13,7 +15,11 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c5"
-with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+if cfg == "--csv":
+    rows = list(csv.DictReader(open(sys.argv[2])))
+    cfg = sys.argv[3] if len(sys.argv) > 3 else os.path.basename(sys.argv[2])
+else:
+  with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
     cmd = ["timeout", "-s", "KILL", "150", "rocprofv3", "--kernel-trace", "--output-format", "csv", "-d", td, "-o", "run",
            "--", sys.executable, os.path.join(ROOT, "bench.py"), "--child", "--steps", "3", "--warmup", "1",
            "--config", cfg] + sys.argv[2:]
