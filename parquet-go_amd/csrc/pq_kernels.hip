@@ -95,11 +95,25 @@ struct KArgs {
 };
 
 #ifdef PQ_STAMPS
-// per-wave s_memrealtime (100 MHz) stamps: slot (blockIdx * 4 + wave) * 8 + i
+// per-wave s_memrealtime (100 MHz) stamps, slot (blockIdx * 4 + wave) * 8:
+// [0] the kernel's start, [i] (1..5) time accumulated over the wave's jobs
+// from the previous stamp to stamp i, [6] the last stamp (the wave's end),
+// [7] jobs (counted at stamp 1)
 #define STAMP(i)                                                                              \
   do {                                                                                        \
-    if (a.dbg && lane_id() == 0)                                                              \
-      a.dbg[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    if (a.dbg && lane_id() == 0) {                                                            \
+      const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                                   \
+      uint64_t *sl_ = a.dbg + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8;              \
+      if ((i) == 0) {                                                                         \
+        sl_[0] = t_;                                                                          \
+        sl_[7] = 0;                                                                           \
+        for (int q_ = 1; q_ < 6; q_++) sl_[q_] = 0;                                           \
+      } else {                                                                                \
+        sl_[(i)] += t_ - sl_[6];                                                              \
+        if ((i) == 1) sl_[7] += 1;                                                            \
+      }                                                                                       \
+      sl_[6] = t_;                                                                            \
+    }                                                                                         \
   } while (0)
 #define PSTAMP(page, i, v)                              \
   do {                                                   \
@@ -4126,10 +4140,8 @@ __global__ __launch_bounds__(LD_WAVES_H * 64) void k_expand_mix(KArgs a) {
   if (g.dpage < 0) mix_global<WIDTH>(a, g, lds_dyn);
   else mix_lds<WIDTH>(a, g, lds_dyn);
 #ifdef PQ_STAMPS
-  if (a.dbg && lane_id() == 0) {  // block kind and the wave's end
-    a.dbg[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + 6] = g.dpage >= 0 ? 1 : 2;
-    a.dbg[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + 7] = __builtin_amdgcn_s_memrealtime();
-  }
+  if (a.dbg && lane_id() == 0)  // the wave's end
+    a.dbg[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + 6] = __builtin_amdgcn_s_memrealtime();
 #endif
 }
 
