@@ -150,7 +150,17 @@ __device__ __forceinline__ const uint8_t *body_ptr(const KArgs &a, const PageDes
 // ===========================================================================
 // K1: Snappy (vendor/github.com/golang/snappy/decode.go:55-75, decode_other.go:14-101)
 // ===========================================================================
-constexpr int RING = 4096;  // per-wave LDS history (bytes): 4 KB keeps six waves per SIMD resident (older bytes: HBM)
+#ifndef PQ_RING
+#define PQ_RING 4096
+#endif
+#ifndef PQ_SNAPPY_WPE
+#define PQ_SNAPPY_WPE 6
+#endif
+// per-wave LDS history (bytes): 4 KB keeps six waves per SIMD resident (older
+// bytes: HBM).  Measured (C3 / C5 step, ms): 4 KB at 6 waves 5.26 / 24.4;
+// 8 KB at 4 waves 6.24 / 28.7; 16 KB at 2 waves 8.40 / 39.7; 2 KB at 7 waves
+// 5.10 / 24.8, at 8 waves (10 VGPRs spilled) 5.17 / 25.7 — occupancy first.
+constexpr int RING = PQ_RING;
 constexpr int RING_MASK = RING - 1;
 constexpr int SNAPPY_WAVES = 4;
 
@@ -690,7 +700,7 @@ constexpr int64_t SNAP_SEG = 65536;
 enum { SNAP_ITEMS = 0, SNAP_FALLBACK = 1 };
 
 template <int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_snappy(KArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PQ_SNAPPY_WPE))) void k_snappy(KArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t ring_all[SNAPPY_WAVES][RING];
   __shared__ SnapLds sl_all[SNAPPY_WAVES];
   const int lane = lane_id();
