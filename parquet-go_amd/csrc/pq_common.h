@@ -62,7 +62,7 @@ struct PageDesc {
   uint8_t kind;          // PAGE_V1 / PAGE_V2 / PAGE_DICT
   uint8_t enc;           // value encoding (PLAIN_DICT already mapped to RLE_DICT)
   uint8_t body_src;      // BODY_*
-  uint8_t pad0;
+  uint8_t train;         // SNAPPY body that is only literals: copied by k_copy from the host plan
   int32_t v2_rep_len;    // V2: rep level bytes at src
   int32_t v2_def_len;    // V2: def level bytes at src + v2_rep_len
   int64_t level_base;    // first level entry of the page inside its column (flat slot base)

@@ -91,6 +91,9 @@ struct pq_launch_args {
   uint32_t *seg_flag;
   const int32_t *parts;  // k_decode<3>: (page, first level, end level) triplets instead of `list`
   int32_t redo;          // k_decode<3>: decode again (whole) the pages whose parts failed
+  const int64_t *hjobs;
+  int32_t nhjobs;
+  uint32_t *status_next;
 };
 int pq_launch(int which, const pq_launch_args *p, hipStream_t s);
 extern int pq_launch_fail_which, pq_launch_fail_err;
@@ -726,13 +729,20 @@ struct pqg_batch {
   std::vector<ChunkError> chunk_errors;
   int64_t input_bytes = 0, staged_bytes = 0, h2d_bytes = 0, host_inflated = 0, dict_entries = 0;
   int64_t literal_pages = 0;  // Snappy pages that are one literal, read in place (no k_snappy work)
+  // Snappy pages that are only literals (snappy_literal_train): copied by
+  // k_copy from the plan, (stream offset in d_in, offset in d_stage, length,
+  // 0) per literal; no k_snappy work
+  std::vector<int64_t> hjobs;
+  int64_t train_pages = 0;
+  int64_t *d_hjobs = nullptr;
   // device
   uint8_t *d_in = nullptr, *d_stage = nullptr;
   uint8_t *d_in_alloc = nullptr;  // the allocation d_in lives in (PQG_DEBUG_INPUT_HIGH_WORD shifts d_in inside it)
   size_t in_alloc = 0, stage_alloc = 0;  // bytes incl. pad
   PageDesc *d_pages = nullptr;
   PageInfo *d_info = nullptr;
-  uint32_t *d_status = nullptr;
+  uint32_t *d_status = nullptr;  // two arrays of npages (epoch parity)
+  bool st_ready[2] = {false, false};  // that array already holds the planned statuses
   uint32_t *d_status0 = nullptr;  // initial statuses (k_reset copies them in every decode)
   void *d_zr = nullptr;           // ZeroRange table of the validity bitmaps
   int32_t nzr = 0;
@@ -1233,6 +1243,11 @@ int pqg_file_last_error(const pqg_file *f, char *buf, size_t cap) {
 // a literal of that length and the stream ends with it.  *data = offset of
 // the literal's bytes.  Anything else (including a corrupt stream) is left to
 // k_snappy, which reports the reference's error.
+static bool getenv_flag(const char *name) {
+  const char *v = getenv(name);
+  return v && v[0] == '1';
+}
+
 static bool snappy_single_literal(const uint8_t *p, int64_t n, int64_t expect, int64_t *data) {
   uint64_t v = 0;
   int64_t i = 0;
@@ -1257,6 +1272,52 @@ static bool snappy_single_literal(const uint8_t *p, int64_t n, int64_t expect, i
   if (x + 1 != v || i + hs + (int64_t)v != n) return false;
   *data = i + hs;
   return true;
+}
+
+// Raw Snappy block that is only literals (an incompressible page longer than
+// one 64 KiB encoder block: a train of maximal literals) decoding to exactly
+// `expect` bytes and ending with the stream — valid by decode_other.go:16-99
+// (every literal inside src and dst, d == len(dst) at the end), and its output
+// is the literals' payloads back to back.  Fills `lits` with (stream offset,
+// output offset, length) per literal; the page is then copied by k_copy from
+// the plan, with no k_snappy work.  Literals must average >= 4 KiB (short
+// literal trains are not worth a copy item each); anything else answers false
+// and is left to k_snappy, which reports the reference's errors.
+static bool snappy_literal_train(const uint8_t *p, int64_t n, int64_t expect, std::vector<int64_t> &lits) {
+  lits.clear();
+  uint64_t v = 0;
+  int64_t i = 0;
+  for (int sh = 0;; sh += 7) {
+    if (i >= n || i >= 5) return false;
+    const uint8_t b = p[i++];
+    v |= (uint64_t)(b & 0x7f) << sh;
+    if (b < 0x80) break;
+  }
+  if (v == 0 || v != (uint64_t)expect || v > 0xffffffffull) return false;
+  const int64_t max_lits = expect / 4096 + 1;
+  int64_t d = 0;
+  while (i < n) {
+    const uint8_t tag = p[i];
+    if (tag & 3) return false;
+    uint64_t x = tag >> 2;
+    int64_t hs = 1;
+    if (x >= 60) {
+      const int extra = (int)x - 59;
+      hs = 1 + extra;
+      if (i + hs > n) return false;
+      x = 0;
+      for (int k = 0; k < extra; k++) x |= (uint64_t)p[i + 1 + k] << (8 * k);
+    }
+    const int64_t len = (int64_t)x + 1;
+    if (len > expect - d || len > n - i - hs) return false;
+    if ((int64_t)(lits.size() / 3) >= max_lits) return false;
+    lits.push_back(i + hs);
+    lits.push_back(d);
+    lits.push_back(len);
+    i += hs + len;
+    d += len;
+  }
+  return d == expect && !lits.empty();
 }
 
 static int supported_encoding(int ptype, int enc) {
@@ -1457,6 +1518,7 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
     };
     const int64_t avail = (int64_t)f->len - w.payload;
     bool needs_device_codec = false;
+    std::vector<int64_t> train;
     int64_t comp = 0, body = 0, lsize = 0;
     if (h.type == 2) {
       d.kind = PAGE_DICT;
@@ -1518,6 +1580,24 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
           d.body_src = BODY_RAW;
           d.body = d.src + (uint64_t)(lsize + lit);
           B->literal_pages++;
+        } else if (C.codec == PQG_CODEC_SNAPPY && !(h.type == 2 && L.physical_type == T_BYTE_ARRAY) &&
+                   !getenv_flag("PQG_NO_TRAIN") &&
+                   snappy_literal_train(f->data + w.payload + lsize, comp, body, train)) {
+          // a train of literals: staged by k_copy from the plan (a BYTE_ARRAY
+          // dictionary is read by k_dict_prepare before k_copy runs: k_snappy)
+          d.body_src = BODY_SNAPPY;
+          d.body = (uint64_t)stage_off;
+          d.train = 1;
+          for (size_t q = 0; q < train.size(); q += 3) {
+            B->hjobs.push_back((int64_t)d.src + lsize + train[q]);
+            B->hjobs.push_back((int64_t)stage_off + train[q + 1]);
+            B->hjobs.push_back(train[q + 2]);
+            B->hjobs.push_back(0);
+          }
+          stage_off += ((body + 15) & ~15) + 16;
+          B->staged_bytes += body;
+          B->train_pages++;
+          if (h.type != 2) B->data_may_defer = true;
         } else {
           needs_device_codec = true;
         }
@@ -2265,6 +2345,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     tab.put((void **)&B->d_copy_cnt, nullptr, 16);
     tab.put((void **)&B->d_job_base, job_base.data(), 4 * job_base.size());
     tab.put((void **)&B->d_job_owner, job_owner.data(), 4 * job_owner.size());
+    tab.put((void **)&B->d_hjobs, B->hjobs.data(), 8 * B->hjobs.size());
     // the image travels with the chunk bytes (the end of the input layout):
     // one pinned-ring upload, no separate copy
     B->tab_host = std::move(tab.h);
@@ -2292,7 +2373,9 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   rc |= alloc_dev((void **)&B->d_stage, (size_t)stage_off);
   B->in_alloc = in_bytes + kPad;
   B->stage_alloc = (size_t)stage_off + kPad;
-  rc |= alloc_dev((void **)&B->d_status, sizeof(uint32_t) * npages);
+  // two status arrays, by epoch parity: a decode's k_level_check leaves the
+  // next decode's array at the planned statuses (no k_reset launch for them)
+  rc |= alloc_dev((void **)&B->d_status, 2 * sizeof(uint32_t) * npages);
   // zero-initialised on the upload stream (not shipped as zeros): page infos
   // (failed pages count zero in the scans) and job records (stale: epoch 0)
   rc |= alloc_dev((void **)&B->d_info, sizeof(PageInfo) * npages);
@@ -2506,7 +2589,6 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.stage_end = B->d_stage + B->stage_alloc;
   a.pages = B->d_pages;
   a.info = B->d_info;
-  a.status = B->d_status;
   a.cols = B->d_cols;
   a.dict_ent = B->d_dict;
   a.ncols = (int32_t)B->cols.size();
@@ -2516,6 +2598,8 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.job_base = B->d_job_base;
   a.job_owner = B->d_job_owner;
   a.copy_cnt = B->d_copy_cnt;
+  a.hjobs = B->d_hjobs;
+  a.nhjobs = (int32_t)(B->hjobs.size() / 4);
   a.copy_idx = B->d_copy_idx;
   a.lens = B->d_lens;
   a.lvl = B->d_lvl;
@@ -2538,6 +2622,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   const bool resume = !upto_scan && B->counted;
   B->counted = upto_scan;
   a.epoch = resume ? B->epoch : ++B->epoch;
+  a.status = B->d_status + (a.epoch & 1) * npages;
   a.tiles = B->d_tiles;
   a.lgroups = B->d_lgroups;
   for (int i = 0; i < 6; i++) {
@@ -2547,8 +2632,12 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   const int32_t ns = (int32_t)B->snappy_list.size(), nd = (int32_t)B->dict_list.size(),
                 ndata = (int32_t)B->data_list.size(), ngen = (int32_t)B->general_list.size();
   int e = 0;
-  if (resume) {
-    if (a.nzr) {  // k_reset over the bitmaps only (the statuses stay the counting pass's)
+  // statuses: already planned when the previous decode's k_level_check set
+  // this epoch's array (k_reset then only zeroes the validity bitmaps)
+  const bool st_planned = resume || B->st_ready[a.epoch & 1];
+  B->st_ready[a.epoch & 1] = false;
+  if (st_planned) {
+    if (a.nzr) {  // k_reset over the bitmaps only
       pq_launch_args z = a;
       z.npages = 0;
       e |= pq_launch(13, &z, s);
@@ -2667,7 +2756,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   // except data pages with deferred literals: k_prepare runs beside the copies
   // in one launch and those pages after it (with string dictionaries, the
   // string pages would all wait: measured slower)
-  const bool fused = nd == 0 && B->max_jobs > 0 && !B->seg_times;
+  const bool fused = nd == 0 && (B->max_jobs > 0 || !B->hjobs.empty()) && !B->seg_times;
   if (lvl_early) hipStreamWaitEvent(s, B->ctx->join[2], 0);  // the levels and counts k_prepare reads
   const bool lvl_now = B->lvl_bytes && !lvl_early;
   if (fused) {
@@ -2778,7 +2867,12 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     mark(true);
     a.list = B->d_lists + ns + nd;
     a.nlist = ndata;
+    // k_level_check also plans the next epoch's statuses (grid-strided copy of
+    // the initial statuses into the other array)
+    const bool plan_next = ndata > 0 && !getenv_flag("PQG_NO_STATUS_PLAN");
+    a.status_next = plan_next ? B->d_status + ((a.epoch + 1) & 1) * npages : nullptr;
     e |= pq_launch(5, &a, s);
+    if (plan_next && !e) B->st_ready[(a.epoch + 1) & 1] = true;
     mark(false);
   }
   if (e) {
@@ -2815,7 +2909,9 @@ int pqg_batch_sync(pqg_batch *B) {
   HIPCHK(hipStreamSynchronize(B->ctx->stream));
   const size_t npages = B->pages.size();
   std::vector<uint32_t> st(npages);
-  if (npages) HIPCHK(hipMemcpy(st.data(), B->d_status, sizeof(uint32_t) * npages, hipMemcpyDeviceToHost));
+  if (npages)
+    HIPCHK(hipMemcpy(st.data(), B->d_status + (B->epoch & 1) * npages, sizeof(uint32_t) * npages,
+                     hipMemcpyDeviceToHost));
   // first error in the reference's order: row group, leaf, phase, page ordinal, stage
   struct Key {
     int rg, leaf, phase, ord;

@@ -74,6 +74,9 @@ struct KArgs {
   uint32_t epoch;         // this decode's record epoch
   uint32_t *copy_cnt;     // deferred literals registered this decode: [epoch & 1] (the other is reset)
   int32_t *copy_idx;      // their job slots, compact (k_snappy -> k_copy)
+  const int64_t *hjobs;   // literal-train pages' copies from the host plan: (d_in offset, d_stage offset, len, 0)
+  int32_t nhjobs;
+  uint32_t *status_next;  // k_level_check: the next decode's status array, set to status0 (null: k_reset does it)
   int32_t *lens;          // DELTA string pages: suffix lengths [0, nv), prefix lengths [nv, 2 nv)
   uint8_t *lvl;           // decoded levels of count-path pages (PageDesc::lvl_base), k_prepare -> k_decode
   const uint32_t *status0;  // k_reset: every page's initial status (host planning errors)
@@ -1351,17 +1354,28 @@ __device__ __forceinline__ void copy_items(const KArgs &a, uint32_t blk, uint32_
   // launch: read them with vector loads at device scope (a uniform plain load
   // becomes a scalar-cache load, which can return lines of an earlier decode
   // that used the same addresses)
+  // the host plan's literal copies (literal-train pages) first, then the
+  // deferred literals k_snappy registered
+  const uint32_t nh = (uint32_t)a.nhjobs;
   const uint32_t items =
-      __hip_atomic_load(&a.copy_cnt[a.epoch & 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * COPY_ITEMS;
+      (nh + __hip_atomic_load(&a.copy_cnt[a.epoch & 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) * COPY_ITEMS;
   for (uint32_t it = blk; it < items; it += nblk) {
     const uint32_t c = it % COPY_ITEMS;
-    const uint32_t ji =
-        (uint32_t)__hip_atomic_load(&a.copy_idx[it / COPY_ITEMS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t *jw = (const uint64_t *)&a.jobs[ji];
+    const uint32_t jn = it / COPY_ITEMS;
     CopyJob job;
-    job.src = (const uint8_t *)(uintptr_t)__hip_atomic_load(&jw[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    job.dst = (uint8_t *)(uintptr_t)__hip_atomic_load(&jw[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    job.len = (int64_t)__hip_atomic_load(&jw[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (jn < nh) {
+      const uint64_t *hw = (const uint64_t *)&a.hjobs[4 * (size_t)jn];
+      job.src = a.in + __hip_atomic_load(&hw[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      job.dst = a.stage + __hip_atomic_load(&hw[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      job.len = (int64_t)__hip_atomic_load(&hw[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      const uint32_t ji =
+          (uint32_t)__hip_atomic_load(&a.copy_idx[jn - nh], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t *jw = (const uint64_t *)&a.jobs[ji];
+      job.src = (const uint8_t *)(uintptr_t)__hip_atomic_load(&jw[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      job.dst = (uint8_t *)(uintptr_t)__hip_atomic_load(&jw[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      job.len = (int64_t)__hip_atomic_load(&jw[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     PQ_CHK(a.in_end && (job.src < a.in || job.src + job.len > a.in_end || job.dst < a.stage ||
                         job.dst + job.len > a.stage_end || job.len < 0),
            20, (uintptr_t)job.src, job.len, return);
@@ -2015,7 +2029,7 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
   const PageDesc d = a.pages[page];
   PageInfo *pi = &a.info[page];
   if (mode >= 0) {
-    const bool waits = d.sidx >= 0 && a.njobs[d.sidx] > 0;  // deferred literals of this body
+    const bool waits = d.train || (d.sidx >= 0 && a.njobs[d.sidx] > 0);  // deferred literals of this body
     if (waits != (mode == 1)) return;
   }
   if (page_status(a.status, page) != STATUS_OK) return;
@@ -2325,7 +2339,7 @@ __global__ __launch_bounds__(256) void k_levels(KArgs a) {
   const PageDesc d = a.pages[page];
   if (d.lvl_base < 0) return;
   if (MODE >= 0) {
-    const bool waits = d.sidx >= 0 && a.njobs[d.sidx] > 0;
+    const bool waits = d.train || (d.sidx >= 0 && a.njobs[d.sidx] > 0);
     if (waits != (MODE == 1)) return;
   }
   if (page_status(a.status, page) != STATUS_OK) return;
@@ -4286,6 +4300,8 @@ __global__ __launch_bounds__(256) void k_dba(KArgs a) {
 // values or def stage, finish decoding the earlier level streams to see if
 // the reference would have failed there first.
 __global__ __launch_bounds__(256) void k_level_check(KArgs a) {
+  if (a.status_next)
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < a.npages; i += gridDim.x * 256) a.status_next[i] = a.status0[i];
   const int gi = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
   if (gi >= a.nlist) return;
   const int page = ufirst(a.list[gi]);
@@ -4380,6 +4396,9 @@ struct pq_launch_args {
   uint32_t *seg_flag;
   const int32_t *parts;  // k_decode<3>: (page, first level, end level) triplets instead of `list`
   int32_t redo;          // k_decode<3>: decode again (whole) the pages whose parts failed
+  const int64_t *hjobs;
+  int32_t nhjobs;
+  uint32_t *status_next;
 };
 
 static pq::KArgs to_k(const pq_launch_args *p) {
@@ -4429,6 +4448,9 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   k.lgroups = (const pq::LdsGroup *)p->lgroups;
   k.parts = p->parts;
   k.redo = p->redo;
+  k.hjobs = p->hjobs;
+  k.status_next = p->status_next;
+  k.nhjobs = p->nhjobs;
   return k;
 }
 
@@ -4455,7 +4477,7 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     return launch_status(which);
   }
   if (which == 12) {  // k_prepare_copy: the prepare blocks, then the copy grid
-    const uint32_t items = k.max_jobs * pq::COPY_ITEMS;
+    const uint32_t items = (k.max_jobs + (uint32_t)k.nhjobs) * pq::COPY_ITEMS;
     const uint32_t cb = items < 1024 ? items : 1024;
     const uint32_t pb = ((uint32_t)(k.nlist > 0 ? k.nlist : 0) + 3) / 4;
     if (pb + cb == 0) return 0;
@@ -4463,8 +4485,8 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     return launch_status(which);
   }
   if (which == 6) {  // deferred literal copies: fixed grid, the job count lives on the device
-    if (k.max_jobs == 0) return 0;
-    const uint32_t items = k.max_jobs * pq::COPY_ITEMS;
+    if (k.max_jobs == 0 && k.nhjobs == 0) return 0;
+    const uint32_t items = (k.max_jobs + (uint32_t)k.nhjobs) * pq::COPY_ITEMS;
     hipLaunchKernelGGL(pq::k_copy, dim3(items < 4096 ? items : 4096), dim3(256), 0, s, k);
     return launch_status(which);
   }

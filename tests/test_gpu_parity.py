@@ -593,6 +593,37 @@ def test_tiled_corrupted_key_streams_match_oracle():
     assert len(outcomes) >= 2, outcomes  # the corruptions reach more than one outcome
 
 
+def test_snappy_literal_train_pages():
+    """Incompressible Snappy pages longer than one 64 KiB encoder block are a
+    train of literals: the host plan copies them with k_copy (no k_snappy).
+    Data pages (required, and nullable with their levels inside the V1 body),
+    big fixed-width dictionaries, and corrupted literal headers — which leave
+    the page to k_snappy and its error classes — against the oracle."""
+    pa = pytest.importorskip("pyarrow")
+    rng = np.random.default_rng(31)
+    rows = 300000
+    K = 1 << 17
+    dvals = rng.integers(-2**31, 2**31 - 1, K, dtype=np.int64).astype(np.int32)
+    t = pa.table({
+        "r": pa.array(rng.integers(-2**63, 2**63 - 1, rows, dtype=np.int64)),
+        "n": pa.array(rng.integers(-2**63, 2**63 - 1, rows, dtype=np.int64), mask=rng.random(rows) < 0.2),
+        "d": pa.array(dvals[rng.integers(0, K, rows)]),
+    }, schema=pa.schema([pa.field("r", pa.int64(), nullable=False), pa.field("n", pa.int64()),
+                         pa.field("d", pa.int32(), nullable=False)]))
+    for ver in ("1.0",):  # (pyarrow writes incompressible V2 pages uncompressed: D4)
+        base = _pq_bytes(t, compression="snappy", row_group_size=rows // 2, data_page_size=1 << 20,
+                         use_dictionary=["d"], dictionary_pagesize_limit=1 << 30, data_page_version=ver)
+        check_file(base, "train v" + ver)
+        # 64 KiB literal headers (tag 61, length 0xffff): corrupt the tag / length
+        hits = [m for m in range(len(base) - 3) if base[m:m + 3] == b"\xf4\xff\xff"]
+        assert len(hits) > 20, len(hits)
+        for trial in range(10):
+            data = bytearray(base)
+            m = hits[int(rng.integers(0, len(hits)))]
+            data[m + int(rng.integers(0, 3))] ^= int(rng.integers(1, 256))
+            check_file(bytes(data), "train v%s corrupt %d" % (ver, trial))
+
+
 def test_boolean_columns_generated():
     """BOOLEAN (type_boolean.go): PLAIN bit-packed and RLE pages, nullable,
     required and inside lists, V1 and V2."""
