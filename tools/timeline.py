@@ -1,6 +1,6 @@
 """Diagnostic: the kernel timeline of one decode step (rocprofv3 kernel trace
 of a short `bench.py --child` run): per launch, its stream queue, start and
-end relative to the step's k_reset, and duration.
+end relative to the step's first launch, and duration.
 
 usage: python tools/timeline.py CONFIG [extra bench args]   (on the GPU box)
        python tools/timeline.py --csv KERNEL_TRACE.csv [NAME]  (a kept trace, e.g.
@@ -29,13 +29,15 @@ else:
         rows += list(csv.DictReader(open(f)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 name = lambda r: r["Kernel_Name"].split("(")[0].replace("void ", "").replace("pq::", "").strip()
-resets = [i for i, r in enumerate(rows) if name(r) == "k_reset"]
-if len(resets) < 2:
+# a decode step ends with k_level_check (k_reset runs only when a step has
+# bitmaps to zero or its statuses were not planned by the previous step)
+ends = [i for i, r in enumerate(rows) if name(r) == "k_level_check"]
+if len(ends) < 2:
     sys.exit("fewer than two decode steps in the trace")
-step = rows[resets[-2]:resets[-1]]  # the last complete step
+step = rows[ends[-2] + 1:ends[-1] + 1]  # the last complete step
 t0 = int(step[0]["Start_Timestamp"])
 end = max(int(r["End_Timestamp"]) for r in step)
-print("%s: step %.3f ms (k_reset to last end), %d launches" % (cfg, (end - t0) / 1e6, len(step)))
+print("%s: step %.3f ms (first launch to last end), %d launches" % (cfg, (end - t0) / 1e6, len(step)))
 print("%-22s %6s %9s %9s %9s %7s" % ("kernel", "queue", "start us", "end us", "dur us", "grid"))
 for r in step:
     s, e = int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0
