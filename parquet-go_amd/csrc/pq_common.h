@@ -75,7 +75,7 @@ struct PageDesc {
   int64_t lens_base;     // BYTE_ARRAY page scratch, 2 x num_values int32 (-1: none): DELTA_(LENGTH_)BYTE_ARRAY
                          // suffix / prefix lengths; PLAIN (offset, length) per value from k_prepare's walk
   int32_t sidx;          // index in the Snappy page list (-1: not decoded by k_snappy)
-  int32_t pad2;
+  int32_t swalk;         // long PLAIN BYTE_ARRAY page: index in the region-parallel length walk (-1: none)
   int64_t lvl_base;      // page with levels on k_prepare's count path: byte offset of its decoded
                          // levels in the level scratch (rep bytes if max_rep > 0, then def bytes,
                          // num_values each); -1: k_decode reads the level streams itself
@@ -86,6 +86,35 @@ struct PageDesc {
 // workgroup takes 4 waves x EX_WAVE_VALUES consecutive values of one page.
 constexpr int RUN_TILE = 512;
 constexpr int EX_WAVE_VALUES = 2048;
+// Region-parallel length-prefix walk of long PLAIN BYTE_ARRAY pages
+// (type_bytearray.go:24-45): the values section is cut into SW_R-byte regions;
+// k_sw_regions walks every region from a candidate entry, k_sw_link confirms
+// the chain region by region (re-walking a region whose candidate was not on
+// it) and counts, k_sw_emit writes each value's (offset, length).
+constexpr int SW_R = 256;            // bytes per region (one lane)
+constexpr int SW_MIN = 64 * 1024;    // pages whose body is at least this long
+struct SwPage {
+  int32_t page;   // PageDesc index
+  int32_t reg0;   // first region record
+  int32_t nreg;   // regions (body_len / SW_R, rounded up)
+  int32_t kind;   // 0: data page (lens scratch), 1: dictionary page (entry table)
+};
+struct SwReg {     // one region: [start, start + SW_R) of the values section
+  int32_t c;       // k_sw_regions: candidate entry (values offset, -1: none); k_sw_link: the true entry
+  int32_t x;       // the chain's exit (first entry at or past the region end)
+  int32_t cnt;     // entries whose header starts in the region, before an error
+  uint32_t err;    // first error on the chain (0: none), after cnt entries
+  int64_t lsum;    // their string bytes
+  int32_t base;    // k_sw_link: value index of the region's first entry (-1: nothing to emit)
+  int32_t pad;
+};
+struct SwRes {     // per page, k_sw_link -> k_prepare / k_dict_prepare / k_sw_emit
+  uint32_t err;    // the walk's error (0: none)
+  int32_t n;       // entries read (the page's non-null values)
+  int64_t sbytes;  // their string bytes
+  int32_t treg;    // the region holding the n-th entry (k_sw_emit adds its part of sbytes)
+  int32_t pad;
+};
 // k_reset: a device buffer zeroed at the start of every decode
 struct ZeroRange {
   uint32_t *ptr;

@@ -94,6 +94,11 @@ struct pq_launch_args {
   const int64_t *hjobs;
   int32_t nhjobs;
   uint32_t *status_next;
+  const void *sw_pages;
+  void *sw_regs;
+  void *sw_res;
+  const void *sw_items;
+  int32_t n_sw_items, n_sw_pages;
 };
 int pq_launch(int which, const pq_launch_args *p, hipStream_t s);
 extern int pq_launch_fail_which, pq_launch_fail_err;
@@ -757,6 +762,14 @@ struct pqg_batch {
   uint32_t *d_copy_cnt = nullptr;  // deferred literals registered per decode (two, by epoch parity)
   int32_t *d_copy_idx = nullptr;   // their job slots, compact
   int32_t *d_lens = nullptr;       // DELTA string pages: length scratch
+  // long PLAIN BYTE_ARRAY pages: region-parallel length walk (k_sw_*)
+  std::vector<SwPage> sw_pages;
+  std::vector<int32_t> sw_items;  // (sw page, chunk of 64 regions) pairs
+  int64_t sw_nreg = 0;
+  SwPage *d_sw_pages = nullptr;
+  int32_t *d_sw_items = nullptr;
+  SwReg *d_sw_regs = nullptr;
+  SwRes *d_sw_res = nullptr;
   int64_t lens_entries = 0;
   int64_t lvl_bytes = 0;     // decoded-level scratch (PageDesc::lvl_base)
   // a level page whose streams sit in a compressed V1 body, or whose chunk has
@@ -1506,6 +1519,7 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
     d.lens_base = -1;
     d.lvl_base = -1;
     d.sidx = -1;
+    d.swalk = -1;
     d.col = ci;
     d.rg = rg;
     d.ord = w.ord;
@@ -1664,6 +1678,20 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
         // length here for k_decode (offsets, then lengths)
         B->pages.back().lens_base = B->lens_entries;
         B->lens_entries += 2 * (int64_t)std::max(d.num_values, 0);
+        // a long page: its walk split over SW_R-byte regions (k_sw_*), when
+        // its non-null count comes from k_levels (or every value is defined)
+        static const bool sw_off = getenv_flag("PQG_NO_SWALK");
+        if (!sw_off && body >= SW_MIN && d.num_values > 0 && (L.max_def == 0 || B->pages.back().lvl_base >= 0)) {
+          const int32_t nreg = (int32_t)((body + SW_R - 1) / SW_R);
+          B->pages.back().swalk = (int32_t)B->sw_pages.size();
+          for (int32_t k = 0; k * 64 < nreg; k++) {
+            B->sw_items.push_back((int32_t)B->sw_pages.size());
+            B->sw_items.push_back(k);
+          }
+          B->sw_pages.push_back(SwPage{my_index, (int32_t)B->sw_nreg, nreg, 0});
+          B->sw_nreg += nreg;
+          B->data_may_defer = true;  // k_prepare<1> takes them after the walk
+        }
       }
     }
     if (needs_device_codec) {
@@ -2346,6 +2374,8 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     tab.put((void **)&B->d_job_base, job_base.data(), 4 * job_base.size());
     tab.put((void **)&B->d_job_owner, job_owner.data(), 4 * job_owner.size());
     tab.put((void **)&B->d_hjobs, B->hjobs.data(), 8 * B->hjobs.size());
+    tab.put((void **)&B->d_sw_pages, B->sw_pages.data(), sizeof(SwPage) * B->sw_pages.size());
+    tab.put((void **)&B->d_sw_items, B->sw_items.data(), 4 * B->sw_items.size());
     // the image travels with the chunk bytes (the end of the input layout):
     // one pinned-ring upload, no separate copy
     B->tab_host = std::move(tab.h);
@@ -2389,6 +2419,8 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   rc |= alloc_dev((void **)&B->d_njobs, 4 * (B->snappy_list.size() + 1));
   rc |= alloc_dev((void **)&B->d_copy_idx, 4 * (job_owner.size() + 1));
   rc |= alloc_dev((void **)&B->d_lens, 4 * (size_t)(B->lens_entries + 1));
+  rc |= alloc_dev((void **)&B->d_sw_regs, sizeof(SwReg) * (size_t)(B->sw_nreg + 1));
+  rc |= alloc_dev((void **)&B->d_sw_res, sizeof(SwRes) * (B->sw_pages.size() + 1));
   rc |= alloc_dev((void **)&B->d_lvl, (size_t)B->lvl_bytes + 16);
   rc |= alloc_dev((void **)&B->d_segs, 8 * (size_t)(B->seg_base.back() + 1));
 #ifdef PQ_STAMPS
@@ -2599,6 +2631,12 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.job_owner = B->d_job_owner;
   a.copy_cnt = B->d_copy_cnt;
   a.hjobs = B->d_hjobs;
+  a.sw_pages = B->d_sw_pages;
+  a.sw_regs = B->d_sw_regs;
+  a.sw_res = B->d_sw_res;
+  a.sw_items = B->d_sw_items;
+  a.n_sw_items = (int32_t)(B->sw_items.size() / 2);
+  a.n_sw_pages = (int32_t)B->sw_pages.size();
   a.nhjobs = (int32_t)(B->hjobs.size() / 4);
   a.copy_idx = B->d_copy_idx;
   a.lens = B->d_lens;
@@ -2759,13 +2797,22 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   const bool fused = nd == 0 && (B->max_jobs > 0 || !B->hjobs.empty()) && !B->seg_times;
   if (lvl_early) hipStreamWaitEvent(s, B->ctx->join[2], 0);  // the levels and counts k_prepare reads
   const bool lvl_now = B->lvl_bytes && !lvl_early;
+  // long PLAIN string pages: the length walk region-parallel (after the
+  // copies and k_levels' non-null counts; k_prepare reads the result)
+  auto sw_walk = [&]() {
+    if (B->sw_pages.empty()) return;
+    e |= pq_launch(28, &a, s);  // k_sw_regions
+    e |= pq_launch(29, &a, s);  // k_sw_link
+    e |= pq_launch(30, &a, s);  // k_sw_emit
+  };
   if (fused) {
     a.list = B->d_lists + ns + nd;
     a.nlist = ndata;
     if (lvl_now) e |= pq_launch(lv_id + 1, &a, s);  // k_levels: pages that do not wait on k_copy
     e |= pq_launch(12, &a, s);  // k_prepare_copy (+ the run walk of tiled RLE_DICTIONARY pages)
-    if (B->data_may_defer) {    // pages that waited on k_copy
+    if (B->data_may_defer) {    // pages that waited on k_copy (or on the length walk)
       if (lvl_now) e |= pq_launch(lv_id + 2, &a, s);
+      sw_walk();
       e |= pq_launch(11, &a, s);
     }
   } else {
@@ -2780,6 +2827,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     a.list = B->d_lists + ns + nd;
     a.nlist = ndata;
     if (lvl_now) e |= pq_launch(lv_id, &a, s);  // k_levels
+    sw_walk();
     e |= pq_launch(2, &a, s);  // (+ the run walk of tiled RLE_DICTIONARY pages)
   }
   mark(false);
@@ -3092,6 +3140,8 @@ void pqg_batch_destroy(pqg_batch *B) {
   free_dev(B->d_zr);
   free_dev(B->d_copy_idx);
   free_dev(B->d_lens);
+  free_dev(B->d_sw_regs);
+  free_dev(B->d_sw_res);
   free_dev(B->d_lvl);
   free_dev(B->d_dbg);
   free_dev(B->d_dbg2);

@@ -77,6 +77,11 @@ struct KArgs {
   const int64_t *hjobs;   // literal-train pages' copies from the host plan: (d_in offset, d_stage offset, len, 0)
   int32_t nhjobs;
   uint32_t *status_next;  // k_level_check: the next decode's status array, set to status0 (null: k_reset does it)
+  const SwPage *sw_pages;  // region-parallel length walk: pages, region records, results, (page, chunk) items
+  SwReg *sw_regs;
+  SwRes *sw_res;
+  const int2 *sw_items;
+  int32_t n_sw_items, n_sw_pages;
   int32_t *lens;          // DELTA string pages: suffix lengths [0, nv), prefix lengths [nv, 2 nv)
   uint8_t *lvl;           // decoded levels of count-path pages (PageDesc::lvl_base), k_prepare -> k_decode
   const uint32_t *status0;  // k_reset: every page's initial status (host planning errors)
@@ -1643,6 +1648,353 @@ __device__ uint32_t layout(const KArgs &a, const PageDesc &d, int page, const Co
 __device__ __forceinline__ int bits_len(int v) { return v ? 32 - __clz(v) : 0; }
 
 // ===========================================================================
+// Region-parallel length-prefix walk of long PLAIN BYTE_ARRAY pages
+// (type_bytearray.go:24-45: [u32 len][bytes] ... for the page's non-null
+// values; a negative length is an error, a header or bytes past the stream
+// io.EOF).  ba_walk finds a page's chain 64 entries at a time in one wave,
+// which leaves a 1 MiB page of short strings with ~1,000 dependent steps.
+// Here every SW_R-byte region of the values section is walked by its own lane:
+//   k_sw_regions  lane = region: the first candidate entry whose chain stays
+//                 well-formed for SW_K hops (or to the region end), then the
+//                 chain from it through the region: entries, string bytes,
+//                 exit, first error;
+//   k_sw_link     wave per page, 64 regions a step: a region is on the true
+//                 chain when its candidate is the exit of the previous region
+//                 on it (a region the chain jumps over has no candidate);
+//                 the first region that is not is walked again from the true
+//                 entry (global loads).  Exclusive counts give every region's
+//                 first value index; the walk ends at the page's n-th value
+//                 or at the first error before it (ba_walk's result);
+//   k_sw_emit     lane = region on the chain: (offset, length) per value.
+// Wrong candidates only cost a re-walk of their region: the result is the
+// serial walk's, whatever the bytes.
+// ===========================================================================
+constexpr int SW_K = 4;                              // hops a candidate must survive
+constexpr int SW_STAGE_W = (64 * SW_R + 64) / 4;     // staged dwords: 64 regions + header lookahead + skew
+
+// the page's values section (data page: after the V1 level streams)
+__device__ __forceinline__ bool sw_values(const KArgs &a, const SwPage &sp, const uint8_t *&vp, int64_t &vlen) {
+  const PageDesc d = a.pages[sp.page];
+  if (sp.kind == 1) {
+    vp = body_ptr(a, d, sp.page);
+    vlen = d.body_len;
+    return true;
+  }
+  const ColDesc c = a.cols[d.col];
+  PageStreams ps;
+  uint32_t stage = 0;
+  if (layout(a, d, sp.page, c, ps, stage)) return false;  // k_prepare reports it
+  vp = ps.body + ps.val_off;
+  vlen = ps.val_len;
+  return true;
+}
+
+// values bytes [lo, lo + 64 SW_R + 4) into LDS (dword aligned: byte p at
+// p - lo + sh); nothing at or past the section end is loaded
+__device__ __forceinline__ int sw_stage(uint32_t *st, const uint8_t *vp, int64_t vlen, int64_t lo) {
+  const uintptr_t a0 = (uintptr_t)(vp + lo), ab = a0 & ~(uintptr_t)3, lim = (uintptr_t)(vp + vlen);
+  const __attribute__((address_space(1))) uint32_t *g = (const __attribute__((address_space(1))) uint32_t *)ab;
+  const int lane = lane_id();
+  constexpr int NQ = (SW_STAGE_W + 63) / 64;
+  constexpr int G = 13;
+  static_assert(NQ % G == 0, "groups of loads");
+#pragma unroll
+  for (int q0 = 0; q0 < NQ; q0 += G) {
+    uint32_t v[G];
+#pragma unroll
+    for (int q = 0; q < G; q++) {
+      const int i = lane + 64 * (q0 + q);
+      v[q] = (i < SW_STAGE_W && ab + 4 * (uintptr_t)i < lim) ? g[i] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < G; q++) {
+      const int i = lane + 64 * (q0 + q);
+      if (i < SW_STAGE_W) st[i] = v[q];
+    }
+  }
+  return (int)(a0 & 3);
+}
+
+__device__ __forceinline__ int32_t sw_rd(const uint32_t *st, int64_t p, int64_t lo, int sh) {
+  const int q = (int)(p - lo) + sh;
+  return (int32_t)__builtin_amdgcn_alignbyte(st[(q >> 2) + 1], st[q >> 2], q & 3);
+}
+
+__global__ __launch_bounds__(64) void k_sw_regions(KArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t st[SW_STAGE_W];
+  const int2 it = a.sw_items[blockIdx.x];
+  const int spi = ufirst(it.x), chunk = ufirst(it.y);
+  const SwPage sp = a.sw_pages[spi];
+  if (page_status(a.status, sp.page) != STATUS_OK) return;
+  const uint8_t *vp;
+  int64_t vlen;
+  if (!sw_values(a, sp, vp, vlen)) return;
+  const int lane = lane_id();
+  const int64_t lo = (int64_t)chunk * 64 * SW_R;
+  const int32_t r = chunk * 64 + lane;
+  if (lo >= vlen) return;  // past the values section (body_len counted the levels too)
+  const int sh = sw_stage(st, vp, vlen, lo);
+  wave_lds_sync();
+  const int64_t rs = lo + (int64_t)lane * SW_R;
+  SwReg out;
+  out.c = -1;
+  out.x = (int32_t)rs;
+  out.cnt = 0;
+  out.err = 0;
+  out.lsum = 0;
+  out.base = -1;
+  out.pad = 0;
+  if (rs < vlen) {
+    const int64_t re = min(rs + (int64_t)SW_R, vlen);
+    int64_t cand = -1;
+    for (int64_t s0 = rs; s0 < re && cand < 0; s0++) {
+      int64_t p = s0;
+      bool ok = true;
+      for (int h = 0; h < SW_K && p < re; h++) {
+        const int32_t l = p + 4 <= vlen ? sw_rd(st, p, lo, sh) : -1;
+        if (l < 0 || p + 4 + (int64_t)l > vlen) {
+          ok = false;
+          break;
+        }
+        p += 4 + (int64_t)l;
+      }
+      if (ok) cand = s0;
+    }
+    if (cand >= 0) {
+      int64_t p = cand, ls = 0;
+      int32_t cnt = 0;
+      uint32_t err = E_OK;
+      while (p < re) {
+        if (p + 4 > vlen) {
+          err = E_EOF;
+          break;
+        }
+        const int32_t l = sw_rd(st, p, lo, sh);
+        if (l < 0) {
+          err = E_BYTE_ARRAY;
+          break;
+        }
+        if (p + 4 + (int64_t)l > vlen) {
+          err = E_EOF;
+          break;
+        }
+        cnt++;
+        ls += l;
+        p += 4 + (int64_t)l;
+      }
+      out.c = (int32_t)cand;
+      out.x = (int32_t)p;
+      out.cnt = cnt;
+      out.err = err;
+      out.lsum = ls;
+    }
+  }
+  if (r < sp.nreg) a.sw_regs[sp.reg0 + r] = out;
+}
+
+// the values the length walk reads: the page's non-null values (k_levels'
+// count, read at device scope) or the dictionary's entries
+__device__ __forceinline__ int64_t sw_count(const KArgs &a, const SwPage &sp) {
+  const PageDesc d = a.pages[sp.page];
+  if (sp.kind == 0 && d.lvl_base >= 0)
+    return __hip_atomic_load(&a.info[sp.page].non_null, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return max(d.num_values, 0);
+}
+
+__global__ __launch_bounds__(256) void k_sw_link(KArgs a) {
+  const int wi = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
+  if (wi >= a.n_sw_pages) return;
+  const SwPage sp = a.sw_pages[wi];
+  const int lane = lane_id();
+  if (page_status(a.status, sp.page) != STATUS_OK) return;
+  const uint8_t *vp;
+  int64_t vlen;
+  if (!sw_values(a, sp, vp, vlen)) return;
+  const int64_t n = sw_count(a, sp);
+  const int64_t nregs = (vlen + SW_R - 1) / SW_R;
+  int64_t E = 0;     // the true chain's next entry (values offset)
+  int64_t done = 0;  // values before it
+  int64_t sb = 0;    // their string bytes
+  uint32_t err = E_OK;
+  int32_t treg = -1;  // the region holding the n-th value (k_sw_emit adds its bytes)
+  bool fin = done >= n;
+  // one region of the true chain walked again from its entry (global loads):
+  // up to the region end, the n-th value or an error
+  auto rewalk = [&](int64_t p, int64_t re, int64_t want, int32_t &cnt, int64_t &ls, uint32_t &e) {
+    cnt = 0;
+    ls = 0;
+    e = E_OK;
+    while (p < re && cnt < want) {
+      if (p + 4 > vlen) {
+        e = E_EOF;
+        break;
+      }
+      const int32_t l = (int32_t)load_u32_unaligned(vp + p);
+      if (l < 0) {
+        e = E_BYTE_ARRAY;
+        break;
+      }
+      if (p + 4 + (int64_t)l > vlen) {
+        e = E_EOF;
+        break;
+      }
+      cnt++;
+      ls += l;
+      p += 4 + (int64_t)l;
+    }
+    return p;
+  };
+  for (int64_t c0 = 0; c0 < nregs && !fin; c0 += 64) {
+    const int64_t r = c0 + lane;
+    SwReg g;
+    g.c = -1;
+    g.x = 0;
+    g.cnt = 0;
+    g.err = 0;
+    g.lsum = 0;
+    if (r < nregs) g = a.sw_regs[sp.reg0 + r];
+    const int64_t re = min((r + 1) * (int64_t)SW_R, vlen);
+    int32_t my_base = -1, my_c = -1;
+    int l0 = 0;
+    while (l0 < 64 && !fin) {
+      const bool in = lane >= l0 && r < nregs;
+      if (!ballot(in)) break;
+      const bool has = in && g.c >= 0;
+      // entry into this lane's region if every region in [l0, lane) is on the
+      // chain: the exit of the last of them with an entry, else E
+      const uint64_t below = ballot(has) & ((1ull << lane) - 1ull);
+      const int src = below ? 63 - __clzll(below) : -1;
+      const int32_t xs = (int32_t)shfl32((uint32_t)g.x, src < 0 ? 0 : src);
+      const int64_t entry = src < 0 ? E : (int64_t)xs;
+      const bool cons = !in || (has ? entry == (int64_t)g.c : entry >= re);
+      const uint64_t badm = ballot(!cons);
+      const int m = badm ? (int)__builtin_ctzll(badm) : 64;
+      const bool conf = in && has && lane < m;  // on the chain, with entries
+      int32_t tot = 0;
+      const int32_t ex = wave_excl_scan32(conf ? g.cnt : 0, &tot);
+      const int64_t b = done + ex;
+      const bool term = conf && (b + g.cnt >= n || (g.err != E_OK && b + g.cnt < n));
+      const uint64_t tm = ballot(term);
+      const int t = tm ? (int)__builtin_ctzll(tm) : 64;
+      const int64_t lsx = wave_incl_scan64(conf && lane < t ? g.lsum : 0);
+      const int64_t ls_before = (int64_t)ufirst64((int64_t)shfl64((uint64_t)lsx, 63));
+      if (conf && lane <= t) {
+        my_base = (int32_t)b;
+        my_c = g.c;
+      }
+      if (tm) {
+        const uint32_t te = (uint32_t)__builtin_amdgcn_readlane((int)g.err, t);
+        const int64_t tb = (int64_t)ufirst64((int64_t)shfl64((uint64_t)b, t));
+        const int32_t tc = (int32_t)__builtin_amdgcn_readlane(g.cnt, t);
+        if (te != E_OK && tb + tc < n) {
+          err = te;  // ba_walk: the first failing entry in order
+        } else {
+          treg = (int32_t)(c0 + t);
+          done = n;
+        }
+        sb += ls_before;
+        fin = true;
+        break;
+      }
+      done += tot;
+      sb += ls_before;
+      const uint64_t cm = ballot(conf);
+      if (cm) E = (int64_t)(int32_t)shfl32((uint32_t)g.x, 63 - __clzll(cm));
+      if (m == 64) break;
+      // region c0 + m is not entered where its walk started: walk it from E
+      const int64_t rm = c0 + m, rem = min((rm + 1) * (int64_t)SW_R, vlen);
+      if (E < rem) {
+        int32_t cnt;
+        int64_t ls;
+        uint32_t e;
+        const int64_t x = rewalk(E, rem, n - done, cnt, ls, e);
+        if (lane == m) {
+          my_base = (int32_t)done;
+          my_c = (int32_t)E;
+        }
+        if (e != E_OK && done + cnt < n) {
+          err = e;
+          fin = true;
+          break;
+        }
+        if (done + cnt >= n) {
+          treg = (int32_t)rm;  // k_sw_emit adds the bytes of its values before the n-th
+          done = n;
+          fin = true;
+          break;
+        }
+        done += cnt;
+        sb += ls;
+        E = x;
+      }
+      l0 = m + 1;
+    }
+    if (r < nregs) {
+      a.sw_regs[sp.reg0 + r].base = my_base;
+      a.sw_regs[sp.reg0 + r].c = my_c;
+    }
+  }
+  // the chain ended (at the section end) before n values: the next header is past it
+  if (err == E_OK && done < n) err = E_EOF;
+  if (lane == 0) {
+    SwRes res;
+    res.err = err;
+    res.n = (int32_t)n;
+    res.sbytes = err == E_OK ? sb : 0;
+    res.treg = treg;
+    res.pad = 0;
+    a.sw_res[wi] = res;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_sw_emit(KArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t st[SW_STAGE_W];
+  const int2 it = a.sw_items[blockIdx.x];
+  const int spi = ufirst(it.x), chunk = ufirst(it.y);
+  const SwPage sp = a.sw_pages[spi];
+  if (page_status(a.status, sp.page) != STATUS_OK) return;
+  // written by k_sw_link in the previous launch: device scope
+  const uint32_t rerr = __hip_atomic_load(&a.sw_res[spi].err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int64_t n = __hip_atomic_load(&a.sw_res[spi].n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int32_t treg = __hip_atomic_load(&a.sw_res[spi].treg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (rerr != E_OK || n <= 0) return;
+  const int lane = lane_id();
+  const int32_t r = chunk * 64 + lane;
+  SwReg g;
+  g.base = -1;
+  g.c = -1;
+  if (r < sp.nreg) g = a.sw_regs[sp.reg0 + r];
+  if (!ballot(g.base >= 0)) return;
+  const uint8_t *vp;
+  int64_t vlen;
+  if (!sw_values(a, sp, vp, vlen)) return;
+  const int64_t lo = (int64_t)chunk * 64 * SW_R;
+  const int sh = sw_stage(st, vp, vlen, lo);
+  wave_lds_sync();
+  if (g.base < 0) return;
+  const PageDesc d = a.pages[sp.page];
+  const int64_t re = min(lo + (int64_t)(lane + 1) * SW_R, vlen);
+  const int32_t nvp = max(d.num_values, 0);
+  int32_t *SO = sp.kind == 0 ? a.lens + d.lens_base : nullptr;
+  int64_t p = g.c, idx = g.base, ls = 0;
+  while (p < re && idx < n) {
+    const int32_t l = sw_rd(st, p, lo, sh);
+    if (sp.kind == 0) {
+      if (idx < nvp) {
+        SO[idx] = (int32_t)(p + 4);
+        SO[nvp + idx] = l;
+      }
+    } else {
+      a.dict_ent[d.dict_base + idx] = ((uint64_t)(p + 4) << 32) | (uint32_t)l;
+    }
+    ls += l;
+    idx++;
+    p += 4 + (int64_t)l;
+  }
+  if (r == treg) atomicAdd((unsigned long long *)&a.sw_res[spi].sbytes, (unsigned long long)ls);
+}
+
+// ===========================================================================
 // Run walk for the tiled decode of flat, required, fixed-width RLE_DICTIONARY
 // pages (called by k_prepare, consumed by k_expand).
 //
@@ -2029,7 +2381,8 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
   const PageDesc d = a.pages[page];
   PageInfo *pi = &a.info[page];
   if (mode >= 0) {
-    const bool waits = d.train || (d.sidx >= 0 && a.njobs[d.sidx] > 0);  // deferred literals of this body
+    // deferred literals of this body, or a length walk done by the k_sw_* launches between
+    const bool waits = d.train || (d.sidx >= 0 && a.njobs[d.sidx] > 0) || d.swalk >= 0;
     if (waits != (mode == 1)) return;
   }
   if (page_status(a.status, page) != STATUS_OK) return;
@@ -2208,7 +2561,13 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
           SO[nvp + first + ln] = l;
         }
       };
-      const uint32_t e2 = ba_walk<960>(ps.body + ps.val_off, ps.val_len, nn, (uint32_t *)lbytes, lnx, lnx + 968, put);
+      uint32_t e2;
+      if (d.swalk >= 0) {  // walked region-parallel by k_sw_regions / _link / _emit (previous launches)
+        e2 = __hip_atomic_load(&a.sw_res[d.swalk].err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        acc = __hip_atomic_load(&a.sw_res[d.swalk].sbytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        e2 = ba_walk<960>(ps.body + ps.val_off, ps.val_len, nn, (uint32_t *)lbytes, lnx, lnx + 968, put);
+      }
       if (e2) {
         set_status(a.status, page, ST_VALUES, e2);
         return;
@@ -4399,6 +4758,11 @@ struct pq_launch_args {
   const int64_t *hjobs;
   int32_t nhjobs;
   uint32_t *status_next;
+  const void *sw_pages;
+  void *sw_regs;
+  void *sw_res;
+  const void *sw_items;
+  int32_t n_sw_items, n_sw_pages;
 };
 
 static pq::KArgs to_k(const pq_launch_args *p) {
@@ -4450,6 +4814,12 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   k.redo = p->redo;
   k.hjobs = p->hjobs;
   k.status_next = p->status_next;
+  k.sw_pages = (const pq::SwPage *)p->sw_pages;
+  k.sw_regs = (pq::SwReg *)p->sw_regs;
+  k.sw_res = (pq::SwRes *)p->sw_res;
+  k.sw_items = (const int2 *)p->sw_items;
+  k.n_sw_items = p->n_sw_items;
+  k.n_sw_pages = p->n_sw_pages;
   k.nhjobs = p->nhjobs;
   return k;
 }
@@ -4542,6 +4912,17 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
       k.recs = (pq::ExRec *)p->recs + (size_t)p->ldn[0] * pq::LD_WAVES_H;           // are launch-relative
       hipLaunchKernelGGL(pq::k_expand_mix<8>, dim3(p->ldn[1]), blk, (size_t)p->ldl[1], s, k);
     }
+    return launch_status(which);
+  }
+  if (which == 28 || which == 30) {  // k_sw_regions / k_sw_emit: one wave per 64 regions
+    if (k.n_sw_items <= 0) return 0;
+    if (which == 28) hipLaunchKernelGGL(pq::k_sw_regions, dim3(k.n_sw_items), dim3(64), 0, s, k);
+    else hipLaunchKernelGGL(pq::k_sw_emit, dim3(k.n_sw_items), dim3(64), 0, s, k);
+    return launch_status(which);
+  }
+  if (which == 29) {  // k_sw_link: one wave per page
+    if (k.n_sw_pages <= 0) return 0;
+    hipLaunchKernelGGL(pq::k_sw_link, dim3((k.n_sw_pages + 3) / 4), dim3(256), 0, s, k);
     return launch_status(which);
   }
   if (which == 0) {  // k_snappy over work items (pages, or segments of long pages)

@@ -750,6 +750,64 @@ def test_plain_strings_corrupted_match_oracle(shape):
     assert len(outcomes) >= 2, outcomes
 
 
+def _plain_string_cases(rng):
+    """Long PLAIN BYTE_ARRAY pages (>= 64 KiB: the region-parallel length walk,
+    k_sw_regions / k_sw_link / k_sw_emit)."""
+    pa = pytest.importorskip("pyarrow")
+    letters = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz     ", np.uint8)
+    n = 60000
+    # l_comment-like text
+    lens = rng.integers(10, 44, n)
+    offs = np.zeros(n + 1, np.int32)
+    offs[1:] = np.cumsum(lens)
+    text = pa.StringArray.from_buffers(n, pa.py_buffer(offs.tobytes()),
+                                       pa.py_buffer(letters[rng.integers(0, len(letters), int(offs[-1]))].tobytes()))
+    # binary values: short, empty, longer than a region, longer than a 64-region chunk
+    lens = rng.integers(0, 20, n)
+    lens[rng.random(n) < 0.02] = rng.integers(300, 3000, int((rng.random(n) < 0.02).sum()) or 1)[0]
+    lens[rng.integers(0, n, 3)] = 20000
+    offs = np.zeros(n + 1, np.int32)
+    offs[1:] = np.cumsum(lens)
+    blob = pa.BinaryArray.from_buffers(pa.binary(), n, [None, pa.py_buffer(offs.tobytes()),
+                                       pa.py_buffer(rng.integers(0, 256, int(offs[-1]), dtype=np.uint8).tobytes())])
+    # values that hold well-formed length prefixes themselves: candidates inside
+    # values survive, so regions are walked again from the true entry
+    fake = b"\x04\x00\x00\x00abcd\x00\x00\x00\x00"
+    adv = pa.array([fake * int(k) for k in rng.integers(0, 6, n)], pa.binary())
+    mask = rng.random(n) < 0.15
+    return {
+        "text": pa.table({"s": text}, schema=pa.schema([pa.field("s", pa.string(), nullable=False)])),
+        "blob_nullable": pa.table({"s": pa.array(blob.to_pylist(), pa.binary(), mask=mask)}),
+        "adversarial": pa.table({"s": adv}, schema=pa.schema([pa.field("s", pa.binary(), nullable=False)])),
+    }
+
+
+@pytest.mark.parametrize("case", ["text", "blob_nullable", "adversarial"])
+def test_plain_strings_region_walk(case):
+    """Long PLAIN string pages walked region by region: V1 and V2, Snappy and
+    uncompressed, required and nullable, values longer than a region and than
+    a chunk of regions, values holding fake length prefixes; then seeded
+    corruptions of the uncompressed pages (errors or other chains) — every
+    outcome the oracle's."""
+    pq = pytest.importorskip("pyarrow.parquet")
+    rng = np.random.default_rng(61)
+    t = _plain_string_cases(rng)[case]
+    for ver in ("1.0", "2.0"):
+        for comp in ("none", "snappy"):
+            data = _pq_bytes(t, compression=comp, use_dictionary=False, data_page_size=1 << 20,
+                             data_page_version=ver, row_group_size=40000)
+            check_file(data, "%s v%s %s" % (case, ver, comp))
+    base = _pq_bytes(t, compression="none", use_dictionary=False, data_page_size=1 << 20, row_group_size=40000)
+    cc = pq.ParquetFile(io.BytesIO(base)).metadata.row_group(0).column(0)
+    lo, hi = cc.data_page_offset, cc.data_page_offset + cc.total_compressed_size
+    for trial in range(8):
+        data = bytearray(base)
+        for _ in range(int(rng.integers(1, 3))):
+            p = int(rng.integers(lo + 64, hi))
+            data[p] ^= int(rng.integers(1, 256))
+        check_file(bytes(data), "%s corrupt %d" % (case, trial))
+
+
 # ---------------------------------------------------------------------------
 # the reference's own vectors (tests/golden/make_ref_vectors.py)
 # ---------------------------------------------------------------------------
