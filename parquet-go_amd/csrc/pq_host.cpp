@@ -98,7 +98,7 @@ struct pq_launch_args {
   void *sw_regs;
   void *sw_res;
   const void *sw_items;
-  int32_t n_sw_items, n_sw_pages;
+  int32_t n_sw_items, n_sw_pages, sw_page0;
 };
 int pq_launch(int which, const pq_launch_args *p, hipStream_t s);
 extern int pq_launch_fail_which, pq_launch_fail_err;
@@ -763,8 +763,10 @@ struct pqg_batch {
   int32_t *d_copy_idx = nullptr;   // their job slots, compact
   int32_t *d_lens = nullptr;       // DELTA string pages: length scratch
   // long PLAIN BYTE_ARRAY pages: region-parallel length walk (k_sw_*)
-  std::vector<SwPage> sw_pages;
-  std::vector<int32_t> sw_items;  // (sw page, chunk of 64 regions) pairs
+  std::vector<SwPage> sw_dict, sw_data;  // while planning: dictionary pages, data pages
+  std::vector<SwPage> sw_pages;           // dictionary pages first, then data pages
+  std::vector<int32_t> sw_items;  // (sw page, chunk of 64 regions) pairs, the dictionary pages' first
+  int32_t sw_ndict = 0, sw_dict_items = 0;
   int64_t sw_nreg = 0;
   SwPage *d_sw_pages = nullptr;
   int32_t *d_sw_items = nullptr;
@@ -1651,6 +1653,12 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
       dict_idx = my_index;
       if (L.physical_type == T_BYTE_ARRAY) {
         B->dict_list.push_back(my_index);  // k_dict_prepare: the length-prefix walk
+        static const bool swd_off = getenv_flag("PQG_NO_SWALK");
+        if (!swd_off && body >= SW_MIN && d.num_values > 0) {  // region-parallel (k_sw_*) before it
+          const int32_t nreg = (int32_t)((body + SW_R - 1) / SW_R);
+          B->pages.back().swalk = (int32_t)B->sw_dict.size();
+          B->sw_dict.push_back(SwPage{my_index, 0, nreg, 1});
+        }
       } else if (L.physical_type == T_BOOLEAN) {
         if (B->status0.back() == STATUS_OK) B->status0.back() = make_status(ST_DICT_VALUES, (uint32_t)PQG_ERR_UNSUPPORTED);
       } else if ((int64_t)std::max(d.num_values, 0) * L.value_width > (int64_t)d.body_len &&
@@ -1683,13 +1691,8 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
         static const bool sw_off = getenv_flag("PQG_NO_SWALK");
         if (!sw_off && body >= SW_MIN && d.num_values > 0 && (L.max_def == 0 || B->pages.back().lvl_base >= 0)) {
           const int32_t nreg = (int32_t)((body + SW_R - 1) / SW_R);
-          B->pages.back().swalk = (int32_t)B->sw_pages.size();
-          for (int32_t k = 0; k * 64 < nreg; k++) {
-            B->sw_items.push_back((int32_t)B->sw_pages.size());
-            B->sw_items.push_back(k);
-          }
-          B->sw_pages.push_back(SwPage{my_index, (int32_t)B->sw_nreg, nreg, 0});
-          B->sw_nreg += nreg;
+          B->pages.back().swalk = (int32_t)B->sw_data.size();
+          B->sw_data.push_back(SwPage{my_index, 0, nreg, 0});
           B->data_may_defer = true;  // k_prepare<1> takes them after the walk
         }
       }
@@ -2278,6 +2281,24 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
       if (pt == 1) B->n_dict_items++;
     }
   }
+  {  // region-parallel length walks: dictionary pages' first (a launch on the
+     // dictionary chain), then data pages' (after k_levels); region records
+    B->sw_ndict = (int32_t)B->sw_dict.size();
+    B->sw_pages = B->sw_dict;
+    B->sw_pages.insert(B->sw_pages.end(), B->sw_data.begin(), B->sw_data.end());
+    for (auto &pg : B->pages)
+      if (pg.swalk >= 0 && pg.kind != PAGE_DICT) pg.swalk += B->sw_ndict;
+    for (size_t i = 0; i < B->sw_pages.size(); i++) {
+      SwPage &sp = B->sw_pages[i];
+      sp.reg0 = (int32_t)B->sw_nreg;
+      B->sw_nreg += sp.nreg;
+      for (int32_t k = 0; k * 64 < sp.nreg; k++) {
+        B->sw_items.push_back((int32_t)i);
+        B->sw_items.push_back(k);
+      }
+      if ((int32_t)i + 1 == B->sw_ndict) B->sw_dict_items = (int32_t)(B->sw_items.size() / 2);
+    }
+  }
   phase("plan");
   // tables
   std::vector<std::pair<void **, size_t>> tab_fix;
@@ -2635,8 +2656,10 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.sw_regs = B->d_sw_regs;
   a.sw_res = B->d_sw_res;
   a.sw_items = B->d_sw_items;
-  a.n_sw_items = (int32_t)(B->sw_items.size() / 2);
-  a.n_sw_pages = (int32_t)B->sw_pages.size();
+  // (the dictionary pages' part: launches before k_dict_prepare)
+  a.n_sw_items = B->sw_dict_items;
+  a.sw_page0 = 0;
+  a.n_sw_pages = B->sw_ndict;
   a.nhjobs = (int32_t)(B->hjobs.size() / 4);
   a.copy_idx = B->d_copy_idx;
   a.lens = B->d_lens;
@@ -2779,6 +2802,9 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
       aw = a;
       aw.list = B->d_lists + ns;
       aw.nlist = nd;
+      e |= pq_launch(28, &aw, ss);  // long dictionary pages: region-parallel length walk
+      e |= pq_launch(29, &aw, ss);
+      e |= pq_launch(30, &aw, ss);
       e |= pq_launch(1, &aw, ss);  // k_dict_prepare (its pages are all decoded on this stream)
     }
     if (walk_side && !one) {
@@ -2800,10 +2826,15 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   // long PLAIN string pages: the length walk region-parallel (after the
   // copies and k_levels' non-null counts; k_prepare reads the result)
   auto sw_walk = [&]() {
-    if (B->sw_pages.empty()) return;
-    e |= pq_launch(28, &a, s);  // k_sw_regions
-    e |= pq_launch(29, &a, s);  // k_sw_link
-    e |= pq_launch(30, &a, s);  // k_sw_emit
+    if ((int32_t)B->sw_pages.size() == B->sw_ndict) return;
+    pq_launch_args w = a;
+    w.sw_items = B->d_sw_items + 2 * (size_t)B->sw_dict_items;
+    w.n_sw_items = (int32_t)(B->sw_items.size() / 2) - B->sw_dict_items;
+    w.sw_page0 = B->sw_ndict;
+    w.n_sw_pages = (int32_t)B->sw_pages.size() - B->sw_ndict;
+    e |= pq_launch(28, &w, s);  // k_sw_regions
+    e |= pq_launch(29, &w, s);  // k_sw_link
+    e |= pq_launch(30, &w, s);  // k_sw_emit
   };
   if (fused) {
     a.list = B->d_lists + ns + nd;
@@ -2821,6 +2852,9 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     if (B->seg_times) {  // phase timing: k_dict_prepare here (not on the side stream)
       a.list = B->d_lists + ns;
       a.nlist = nd;
+      e |= pq_launch(28, &a, s);
+      e |= pq_launch(29, &a, s);
+      e |= pq_launch(30, &a, s);
       e |= pq_launch(1, &a, s);
     }
     mark(false);

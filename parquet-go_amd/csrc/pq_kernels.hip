@@ -81,7 +81,7 @@ struct KArgs {
   SwReg *sw_regs;
   SwRes *sw_res;
   const int2 *sw_items;
-  int32_t n_sw_items, n_sw_pages;
+  int32_t n_sw_items, n_sw_pages, sw_page0;  // (a launch's part: pages [sw_page0, + n_sw_pages))
   int32_t *lens;          // DELTA string pages: suffix lengths [0, nv), prefix lengths [nv, 2 nv)
   uint8_t *lvl;           // decoded levels of count-path pages (PageDesc::lvl_base), k_prepare -> k_decode
   const uint32_t *status0;  // k_reset: every page's initial status (host planning errors)
@@ -1580,6 +1580,11 @@ __global__ __launch_bounds__(256) void k_dict_prepare(KArgs a) {
     return;
   }
   // length-prefix walk (type_bytearray.go:24-45): entry table (offset << 32 | length)
+  if (d.swalk >= 0) {  // a long page: walked region-parallel by the k_sw_* launches before this one
+    const uint32_t e = __hip_atomic_load(&a.sw_res[d.swalk].err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (e) set_status(a.status, page, ST_DICT_VALUES, e);
+    return;
+  }
   __shared__ __attribute__((aligned(16))) BaLdsT<BA_WIN_DICT> ba_all[4];
   BaLdsT<BA_WIN_DICT> &bl = ba_all[threadIdx.x >> 6];
   auto put = [&](int64_t first, int ln, int64_t voff, int32_t l, int cnt) {
@@ -1802,8 +1807,9 @@ __device__ __forceinline__ int64_t sw_count(const KArgs &a, const SwPage &sp) {
 }
 
 __global__ __launch_bounds__(256) void k_sw_link(KArgs a) {
-  const int wi = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
-  if (wi >= a.n_sw_pages) return;
+  const int wl = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
+  if (wl >= a.n_sw_pages) return;
+  const int wi = a.sw_page0 + wl;
   const SwPage sp = a.sw_pages[wi];
   const int lane = lane_id();
   if (page_status(a.status, sp.page) != STATUS_OK) return;
@@ -4762,7 +4768,7 @@ struct pq_launch_args {
   void *sw_regs;
   void *sw_res;
   const void *sw_items;
-  int32_t n_sw_items, n_sw_pages;
+  int32_t n_sw_items, n_sw_pages, sw_page0;
 };
 
 static pq::KArgs to_k(const pq_launch_args *p) {
@@ -4820,6 +4826,7 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   k.sw_items = (const int2 *)p->sw_items;
   k.n_sw_items = p->n_sw_items;
   k.n_sw_pages = p->n_sw_pages;
+  k.sw_page0 = p->sw_page0;
   k.nhjobs = p->nhjobs;
   return k;
 }

@@ -806,6 +806,22 @@ def test_plain_strings_region_walk(case):
             p = int(rng.integers(lo + 64, hi))
             data[p] ^= int(rng.integers(1, 256))
         check_file(bytes(data), "%s corrupt %d" % (case, trial))
+    # one dictionary page per row group holding every distinct value (>= 64 KiB:
+    # walked region-parallel before k_dict_prepare), Snappy and uncompressed,
+    # and corruptions inside the dictionary page
+    for comp in ("none", "snappy"):
+        data = _pq_bytes(t, compression=comp, use_dictionary=True, dictionary_pagesize_limit=1 << 30,
+                         data_page_size=1 << 20, row_group_size=40000)
+        check_file(data, "%s dictionary %s" % (case, comp))
+    base = _pq_bytes(t, compression="none", use_dictionary=True, dictionary_pagesize_limit=1 << 30,
+                     data_page_size=1 << 20, row_group_size=40000)
+    cc = pq.ParquetFile(io.BytesIO(base)).metadata.row_group(0).column(0)
+    lo, hi = cc.dictionary_page_offset, cc.data_page_offset
+    for trial in range(6 if hi - lo > 64 << 10 else 0):  # (the fake-prefix values have 6 distinct)
+        data = bytearray(base)
+        p = int(rng.integers(lo + 64, hi))
+        data[p] ^= int(rng.integers(1, 256))
+        check_file(bytes(data), "%s dictionary corrupt %d" % (case, trial))
 
 
 # ---------------------------------------------------------------------------
