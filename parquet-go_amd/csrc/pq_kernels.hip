@@ -1675,6 +1675,7 @@ __device__ __forceinline__ int bits_len(int v) { return v ? 32 - __clz(v) : 0; }
 // serial walk's, whatever the bytes.
 // ===========================================================================
 constexpr int SW_K = 4;                              // hops a candidate must survive
+constexpr int SW_MAX_REWALK = 16;                    // k_sw_link: then ba_walk for the rest of the page
 constexpr int SW_STAGE_W = (64 * SW_R + 64) / 4;     // staged dwords: 64 regions + header lookahead + skew
 
 // the page's values section (data page: after the V1 level streams)
@@ -1737,9 +1738,6 @@ __global__ __launch_bounds__(64) void k_sw_regions(KArgs a) {
   const int lane = lane_id();
   const int64_t lo = (int64_t)chunk * 64 * SW_R;
   const int32_t r = chunk * 64 + lane;
-  if (lo >= vlen) return;  // past the values section (body_len counted the levels too)
-  const int sh = sw_stage(st, vp, vlen, lo);
-  wave_lds_sync();
   const int64_t rs = lo + (int64_t)lane * SW_R;
   SwReg out;
   out.c = -1;
@@ -1749,13 +1747,23 @@ __global__ __launch_bounds__(64) void k_sw_regions(KArgs a) {
   out.lsum = 0;
   out.base = -1;
   out.pad = 0;
+  // (regions past the values section — body_len counted the V1 levels too —
+  // keep an empty record: k_sw_emit never takes them)
+  const int sh = lo < vlen ? sw_stage(st, vp, vlen, lo) : 0;
+  wave_lds_sync();
   if (rs < vlen) {
     const int64_t re = min(rs + (int64_t)SW_R, vlen);
-    int64_t cand = -1;
+    // a strong candidate makes at least two hops inside the region (or ends
+    // the section): a stray small "length" — the last byte of a string and
+    // the low bytes of the next header, ~7 KB for text — jumps out in one.
+    // The first weak one is taken only when the region has no strong one
+    // (an entry spanning the region end)
+    int64_t cand = -1, weak = -1;
     for (int64_t s0 = rs; s0 < re && cand < 0; s0++) {
       int64_t p = s0;
       bool ok = true;
-      for (int h = 0; h < SW_K && p < re; h++) {
+      int h = 0;
+      for (; h < SW_K && p < re; h++) {
         const int32_t l = p + 4 <= vlen ? sw_rd(st, p, lo, sh) : -1;
         if (l < 0 || p + 4 + (int64_t)l > vlen) {
           ok = false;
@@ -1763,8 +1771,11 @@ __global__ __launch_bounds__(64) void k_sw_regions(KArgs a) {
         }
         p += 4 + (int64_t)l;
       }
-      if (ok) cand = s0;
+      if (!ok) continue;
+      if (h >= 2 || p == vlen) cand = s0;
+      else if (weak < 0) weak = s0;
     }
+    if (cand < 0) cand = weak;
     if (cand >= 0) {
       int64_t p = cand, ls = 0;
       int32_t cnt = 0;
@@ -1824,6 +1835,7 @@ __global__ __launch_bounds__(256) void k_sw_link(KArgs a) {
   uint32_t err = E_OK;
   int32_t treg = -1;  // the region holding the n-th value (k_sw_emit adds its bytes)
   bool fin = done >= n;
+  int rewalks = 0;
   // one region of the true chain walked again from its entry (global loads):
   // up to the region end, the n-th value or an error
   auto rewalk = [&](int64_t p, int64_t re, int64_t want, int32_t &cnt, int64_t &ls, uint32_t &e) {
@@ -1909,6 +1921,40 @@ __global__ __launch_bounds__(256) void k_sw_link(KArgs a) {
       if (m == 64) break;
       // region c0 + m is not entered where its walk started: walk it from E
       const int64_t rm = c0 + m, rem = min((rm + 1) * (int64_t)SW_R, vlen);
+      if (E < rem && ++rewalks > SW_MAX_REWALK) {
+        // values that hold well-formed length prefixes themselves mislead the
+        // candidates region after region: the rest of the page by ba_walk
+        // (regions from here on emit nothing)
+        __shared__ __attribute__((aligned(16))) BaLds swb_all[4];
+        BaLds &bl = swb_all[threadIdx.x >> 6];
+        const PageDesc d = a.pages[sp.page];
+        const int32_t nvp = max(d.num_values, 0);
+        int32_t *SO = sp.kind == 0 ? a.lens + d.lens_base : nullptr;
+        const int64_t d0 = done, E0 = E;
+        int64_t acc = 0;
+        auto put = [&](int64_t first, int ln, int64_t voff, int32_t l, int cnt) {
+          const int64_t t2 = wave_incl_scan64(ln < cnt ? (int64_t)l : 0);
+          acc += (int64_t)ufirst64((int64_t)shfl64((uint64_t)t2, 63));
+          const int64_t idx = d0 + first + ln;
+          if (ln < cnt) {
+            if (SO) {
+              if (idx < nvp) {
+                SO[idx] = (int32_t)(E0 + voff);
+                SO[nvp + idx] = l;
+              }
+            } else {
+              a.dict_ent[d.dict_base + idx] = ((uint64_t)(E0 + voff) << 32) | (uint32_t)l;
+            }
+          }
+        };
+        err = ba_walk<BA_WIN>(vp + E0, vlen - E0, n - d0, bl.win, bl.jt[0], bl.jt[1], put);
+        if (err == E_OK) {
+          done = n;
+          sb += acc;
+        }
+        fin = true;
+        break;
+      }
       if (E < rem) {
         int32_t cnt;
         int64_t ls;
@@ -1966,15 +2012,15 @@ __global__ __launch_bounds__(64) void k_sw_emit(KArgs a) {
   if (rerr != E_OK || n <= 0) return;
   const int lane = lane_id();
   const int32_t r = chunk * 64 + lane;
-  SwReg g;
-  g.base = -1;
-  g.c = -1;
-  if (r < sp.nreg) g = a.sw_regs[sp.reg0 + r];
-  if (!ballot(g.base >= 0)) return;
   const uint8_t *vp;
   int64_t vlen;
   if (!sw_values(a, sp, vp, vlen)) return;
   const int64_t lo = (int64_t)chunk * 64 * SW_R;
+  SwReg g;
+  g.base = -1;
+  g.c = -1;
+  if (r < sp.nreg && lo + (int64_t)lane * SW_R < vlen) g = a.sw_regs[sp.reg0 + r];
+  if (!ballot(g.base >= 0)) return;
   const int sh = sw_stage(st, vp, vlen, lo);
   wave_lds_sync();
   if (g.base < 0) return;
