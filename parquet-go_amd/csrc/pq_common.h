@@ -71,7 +71,8 @@ struct PageDesc {
   int32_t run_cap;       // run-table entries reserved for the page (runs + sentinel)
   int32_t tile_base;     // tiled page: first entry of its tile -> first-run index table
   int32_t job_base;      // tiled page: first entry of its job -> position table (page_jobs)
-  int32_t alias_any;     // dictionary page: k_snappy may alias it at any alignment (LDS-group chunks)
+  int16_t alias_any;     // dictionary page: k_snappy may alias it at any alignment (LDS-group chunks)
+  int16_t srec;          // tiled PLAIN page whose k_expand records the host wrote (no k_prepare work)
   int64_t lens_base;     // BYTE_ARRAY page scratch, 2 x num_values int32 (-1: none): DELTA_(LENGTH_)BYTE_ARRAY
                          // suffix / prefix lengths; PLAIN (offset, length) per value from k_prepare's walk
   int32_t sidx;          // index in the Snappy page list (-1: not decoded by k_snappy)
@@ -172,6 +173,12 @@ struct ExRec {
   int32_t val_len;       // values section bytes
 };
 static_assert(sizeof(ExRec) == 64, "one scalar load");
+// ExRec::epoch of a record the host wrote once (a tiled PLAIN page: nothing
+// about it depends on the data), current in every decode
+constexpr uint32_t EPOCH_STATIC = 0xFFFFFFFFu;
+__host__ __device__ inline bool rec_live(uint32_t rec_epoch, uint32_t epoch) {
+  return rec_epoch == epoch || rec_epoch == EPOCH_STATIC;
+}
 
 // One RLE/bit-packed run of a key stream (hybrid_decoder.go:143-166), as
 // written by k_runs: x = first value (page-relative) | RUN_RLE for an RLE run;

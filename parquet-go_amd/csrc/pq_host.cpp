@@ -809,6 +809,8 @@ struct pqg_batch {
   hipEvent_t ready = nullptr;  // recorded on the context's upload stream after the chunk bytes' H2D
   bool ready_final = false;    // `ready` recorded after every set-up copy (else copies may be in flight)
   bool counted = false;        // the last launch was the counting pass (the next decode resumes from it)
+  bool all_srec = false;  // every data page has host-written records: no k_prepare work
+  std::vector<ExRec> recs_host;  // tiled PLAIN pages' static k_expand records (upload source)
   std::vector<uint8_t> tab_host;  // the small tables (d_pages, d_info, d_lists, ...): host image, uploaded at
                                   // the end of d_in
   std::vector<ColDesc> hcols0;    // column descriptors as first uploaded (before the counting pass)
@@ -1908,6 +1910,13 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     }
     const int32_t n = std::max(d.num_values, 0);
     const int32_t nt = (n + RUN_TILE - 1) / RUN_TILE;
+    // a PLAIN page's k_expand records depend only on its header (flat and
+    // required: the values section is the whole body): written by the host
+    // once; a page too short for its values is left to k_prepare's check
+    static const bool srec_off = getenv_flag("PQG_NO_STATIC_RECORDS");
+    if (d.enc == ENC_PLAIN && !srec_off && B->status0[(size_t)pi] == STATUS_OK &&
+        (int64_t)n * L.value_width <= (int64_t)d.body_len)
+      d.srec = 1;
     d.job_base = (int32_t)B->page_job_entries;
     B->page_job_entries += (n + EX_WAVE_VALUES - 1) / EX_WAVE_VALUES;
     d.tile_base = (int32_t)B->tile_entries;
@@ -2299,6 +2308,8 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
       if ((int32_t)i + 1 == B->sw_ndict) B->sw_dict_items = (int32_t)(B->sw_items.size() / 2);
     }
   }
+  B->all_srec = !B->data_list.empty();
+  for (int32_t pi : B->data_list) B->all_srec &= B->pages[(size_t)pi].srec != 0;
   phase("plan");
   // tables
   std::vector<std::pair<void **, size_t>> tab_fix;
@@ -2462,7 +2473,29 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     B->h2d_bytes += (int64_t)in_bytes;
     for (auto &f : tab_fix) *f.first = B->d_in + tab_off + f.second;
     hipMemsetAsync(B->d_info, 0, sizeof(PageInfo) * npages, ctx->upload);
-    hipMemsetAsync(B->d_recs, 0, sizeof(ExRec) * (B->tiles.size() + 1), ctx->upload);
+    // job records: stale (epoch 0), and the host's records of tiled PLAIN
+    // pages (EPOCH_STATIC) at their launch positions
+    bool any_srec = false;
+    for (const TileJob &tj : B->tiles) any_srec |= tj.page >= 0 && B->pages[(size_t)tj.page].srec;
+    if (!any_srec) {
+      hipMemsetAsync(B->d_recs, 0, sizeof(ExRec) * (B->tiles.size() + 1), ctx->upload);
+    } else {
+      B->recs_host.assign(B->tiles.size() + 1, ExRec{});
+      for (size_t p = 0; p < B->tiles.size(); p++) {
+        const TileJob &tj = B->tiles[p];
+        if (tj.page < 0 || !B->pages[(size_t)tj.page].srec) continue;
+        const PageDesc &d = B->pages[(size_t)tj.page];
+        ExRec &rc = B->recs_host[p];
+        rc.vals = (d.body_src == BODY_RAW ? B->d_in : B->d_stage) + d.body;
+        rc.v0 = tj.v0;
+        rc.lim = std::min(tj.v0 + EX_WAVE_VALUES, std::max(d.num_values, 0));
+        rc.bw = -1;
+        rc.epoch = EPOCH_STATIC;
+        rc.val_len = d.body_len;
+      }
+      hipMemcpyAsync(B->d_recs, B->recs_host.data(), sizeof(ExRec) * B->recs_host.size(), hipMemcpyHostToDevice,
+                     ctx->upload);
+    }
     if (hipEventCreateWithFlags(&B->ready, hipEventDisableTiming) != hipSuccess) {
       set_err("hipEventCreate failed");
       return PQG_ERR_DEVICE;
@@ -2840,8 +2873,12 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     a.list = B->d_lists + ns + nd;
     a.nlist = ndata;
     if (lvl_now) e |= pq_launch(lv_id + 1, &a, s);  // k_levels: pages that do not wait on k_copy
-    e |= pq_launch(12, &a, s);  // k_prepare_copy (+ the run walk of tiled RLE_DICTIONARY pages)
-    if (B->data_may_defer) {    // pages that waited on k_copy (or on the length walk)
+    {
+      pq_launch_args pc = a;
+      if (B->all_srec) pc.nlist = 0;  // the copies only
+      e |= pq_launch(12, &pc, s);  // k_prepare_copy (+ the run walk of tiled RLE_DICTIONARY pages)
+    }
+    if (B->data_may_defer && !B->all_srec) {  // pages that waited on k_copy (or on the length walk)
       if (lvl_now) e |= pq_launch(lv_id + 2, &a, s);
       sw_walk();
       e |= pq_launch(11, &a, s);
@@ -2862,7 +2899,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     a.nlist = ndata;
     if (lvl_now) e |= pq_launch(lv_id, &a, s);  // k_levels
     sw_walk();
-    e |= pq_launch(2, &a, s);  // (+ the run walk of tiled RLE_DICTIONARY pages)
+    if (!B->all_srec) e |= pq_launch(2, &a, s);  // (+ the run walk of tiled RLE_DICTIONARY pages)
   }
   mark(false);
   }  // !resume

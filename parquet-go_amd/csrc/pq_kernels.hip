@@ -2431,6 +2431,7 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
   const int page = ufirst(a.list[gi]);
   PSTAMP(page, 0, __builtin_amdgcn_s_memrealtime());
   const PageDesc d = a.pages[page];
+  if (d.srec) return;  // tiled PLAIN page: its k_expand records were written by the host
   PageInfo *pi = &a.info[page];
   if (mode >= 0) {
     // deferred literals of this body, or a length walk done by the k_sw_* launches between
@@ -4354,7 +4355,7 @@ __global__ __launch_bounds__(NW * 64) void k_expand_pass(KArgs a) {
   if (wv < g.njobs) {
     tj = sload(a.tiles + j);
     rc = sload(a.recs + j);
-    if (rc.epoch == a.epoch && rc.v0 < rc.lim) {
+    if (rec_live(rc.epoch, a.epoch) && rc.v0 < rc.lim) {
       if (rc.bw < 0) {  // PLAIN (a dictionary chunk's fallback page): a copy of the job's bytes
         copy_tile<EX_WAVE * 8 / 1024>(rc.vals + (int64_t)rc.v0 * WIDTH, tj.out + (int64_t)rc.v0 * WIDTH,
                                       (int64_t)(rc.lim - rc.v0) * WIDTH, lane);
@@ -4387,7 +4388,7 @@ __global__ __launch_bounds__(NW * 64) void k_expand_pass(KArgs a) {
   const ExRec r0 = sload(a.recs + g.job0);
   const uint8_t *dict;
   uint32_t dn;
-  if (r0.epoch == a.epoch && r0.dict) {
+  if (rec_live(r0.epoch, a.epoch) && r0.dict) {
     dict = r0.dict;
     dn = r0.dict_n;
   } else {  // a failed or PLAIN first page: the dictionary page itself (its size checked on the host)
@@ -4501,7 +4502,7 @@ __device__ __forceinline__ void mix_global(const KArgs &a, const LdsGroup &g, ui
   const int j = (int)blockIdx.x * LD_WAVES + wv;
   const TileJob tj = sload(a.tiles + j);
   const ExRec rc = sload(a.recs + j);
-  if (rc.epoch != a.epoch) return;  // an unused slot, or the page failed before k_prepare finished it
+  if (!rec_live(rc.epoch, a.epoch)) return;  // an unused slot, or the page failed before k_prepare finished it
   expand_job<WIDTH, false>(a, tj, rc, lds_dyn + wv * (g.kspan / 4), g.kspan, nullptr);
 }
 
@@ -4521,7 +4522,7 @@ __device__ __forceinline__ void mix_lds(const KArgs &a, const LdsGroup &g, uint3
   }
   const uint8_t *dict;
   uint32_t dn;
-  if (r0.epoch == a.epoch && r0.dict) {
+  if (rec_live(r0.epoch, a.epoch) && r0.dict) {
     dict = r0.dict;
     dn = r0.dict_n;
   } else {  // a failed or PLAIN first page: the dictionary page itself
@@ -4562,7 +4563,7 @@ __device__ __forceinline__ void mix_lds(const KArgs &a, const LdsGroup &g, uint3
       tj = sload(a.tiles + j);
       rc = sload(a.recs + j);
     }
-    if (rc.epoch != a.epoch) continue;  // the page failed before k_prepare finished it
+    if (!rec_live(rc.epoch, a.epoch)) continue;  // the page failed before k_prepare finished it
     expand_job<WIDTH, true>(a, tj, rc, kspan, g.kspan, lds_dyn);
   }
 }
