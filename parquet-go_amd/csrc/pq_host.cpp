@@ -93,6 +93,7 @@ struct pq_launch_args {
   int32_t redo;          // k_decode<3>: decode again (whole) the pages whose parts failed
   const int64_t *hjobs;
   int32_t nhjobs;
+  int32_t grid_cap;  // k_levels<-1>: at most this many workgroups (grid-stride loop)
   uint32_t *status_next;
   const void *sw_pages;
   void *sw_regs;
@@ -2769,6 +2770,12 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     al.nlist = ndata;
     hipEventRecord(B->ctx->fork, s);
     hipStreamWaitEvent(B->ctx->side[2], B->ctx->fork, 0);
+    // PQG_LEVELS_CAP=k: k workgroups per CU looping over the pages, resident
+    // from the start beside k_snappy's.  Measured on C3 (ms a step): full
+    // grid 5.38, k = 1 6.52, 2 5.91, 4 5.43, 8 5.37 — resident waves beside
+    // k_snappy's get too little issue; the full grid stays
+    static const int lv_cap = getenv("PQG_LEVELS_CAP") ? atoi(getenv("PQG_LEVELS_CAP")) : 0;
+    al.grid_cap = lv_cap > 0 ? lv_cap * B->ctx->cus : 0;
     e |= pq_launch(lv_id, &al, B->ctx->side[2]);  // k_levels<-1>: every level page
     hipEventRecord(B->ctx->join[2], B->ctx->side[2]);
   }

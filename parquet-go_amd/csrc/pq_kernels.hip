@@ -2735,17 +2735,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
 // k_prepare and k_decode then read the counts and levels instead of the
 // streams.  MODE as k_prepare (-1 every page, 0 / 1 pages that do not / do
 // wait on k_copy).
-template <int MODE, bool SPLIT>
-__global__ __launch_bounds__(256) void k_levels(KArgs a) {
-  // SPLIT (batches with repeated columns): two waves per page — the
-  // repetition and the definition streams are independent (each its own run
-  // chain) and are decoded side by side; errors meet in the page status
-  // (atomicMin: ST_REP before ST_DEF, the reference's order).  Otherwise one
-  // wave per page decodes both in turn.
-  const int wv = (int)ufirst(threadIdx.x >> 6);
-  const int gi = SPLIT ? blockIdx.x * 2 + (wv >> 1) : blockIdx.x * 4 + wv;
-  const int part = SPLIT ? (wv & 1) : 2;  // 0: repetition levels, 1: definition levels, 2: both
-  if (gi >= a.nlist) return;
+template <int MODE>
+__device__ __forceinline__ void levels_page(const KArgs &a, int gi, int part) {
   const int lane = lane_id();
   const int page = ufirst(a.list[gi]);
   const PageDesc d = a.pages[page];
@@ -2793,6 +2784,25 @@ __global__ __launch_bounds__(256) void k_levels(KArgs a) {
     a.info[page].non_null = nn;
   }
 }
+
+// SPLIT (batches with repeated columns): two waves per page — the repetition
+// and the definition streams are independent (each its own run chain) and are
+// decoded side by side; errors meet in the page status (atomicMin: ST_REP
+// before ST_DEF, the reference's order).  Otherwise one wave per page decodes
+// both in turn.  Workgroups loop over the pages with a grid stride
+// (PQG_LEVELS_CAP: a capped grid for the launch beside the Snappy phase;
+// measured slower, so the full grid is the default)
+template <int MODE, bool SPLIT>
+__global__ __launch_bounds__(256) void k_levels(KArgs a) {
+  const int wv = (int)ufirst(threadIdx.x >> 6);
+  const int part = SPLIT ? (wv & 1) : 2;  // 0: repetition levels, 1: definition levels, 2: both
+  for (uint32_t b = blockIdx.x;; b += gridDim.x) {
+    const int gi = SPLIT ? (int)b * 2 + (wv >> 1) : (int)b * 4 + wv;
+    if (gi >= a.nlist) break;
+    levels_page<MODE>(a, gi, part);
+  }
+}
+
 
 // k_prepare beside k_copy in one launch (batches without BYTE_ARRAY
 // dictionaries): the first blocks prepare every page whose body does not wait
@@ -4810,6 +4820,7 @@ struct pq_launch_args {
   int32_t redo;          // k_decode<3>: decode again (whole) the pages whose parts failed
   const int64_t *hjobs;
   int32_t nhjobs;
+  int32_t grid_cap;  // k_levels<-1>: at most this many workgroups (grid-stride loop)
   uint32_t *status_next;
   const void *sw_pages;
   void *sw_regs;
@@ -4996,11 +5007,15 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     case 1: hipLaunchKernelGGL(pq::k_dict_prepare, grid, block, 0, s, k); break;
     case 2: hipLaunchKernelGGL(pq::k_prepare<-1>, grid, block, 0, s, k); break;
     case 11: hipLaunchKernelGGL(pq::k_prepare<1>, grid, block, 0, s, k); break;
-    case 19: hipLaunchKernelGGL((pq::k_levels<-1, false>), grid, block, 0, s, k); break;
+    case 19: hipLaunchKernelGGL((pq::k_levels<-1, false>), p->grid_cap > 0 && (int)grid.x > p->grid_cap ? dim3(p->grid_cap) : grid, block, 0, s, k); break;
     case 20: hipLaunchKernelGGL((pq::k_levels<0, false>), grid, block, 0, s, k); break;
     case 21: hipLaunchKernelGGL((pq::k_levels<1, false>), grid, block, 0, s, k); break;
     // two waves a page (batches with repeated columns)
-    case 24: hipLaunchKernelGGL((pq::k_levels<-1, true>), dim3((k.nlist + 1) / 2), block, 0, s, k); break;
+    case 24: {
+      const int g24 = (k.nlist + 1) / 2;
+      hipLaunchKernelGGL((pq::k_levels<-1, true>), dim3(p->grid_cap > 0 && g24 > p->grid_cap ? p->grid_cap : g24), block, 0, s, k);
+      break;
+    }
     case 25: hipLaunchKernelGGL((pq::k_levels<0, true>), dim3((k.nlist + 1) / 2), block, 0, s, k); break;
     case 26: hipLaunchKernelGGL((pq::k_levels<1, true>), dim3((k.nlist + 1) / 2), block, 0, s, k); break;
     case 3: hipLaunchKernelGGL(pq::k_decode<0>, grid, block, 0, s, k); break;
