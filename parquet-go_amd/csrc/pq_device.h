@@ -408,6 +408,31 @@ struct HybT {
     return inwin ? wv : unpack_u32(p, len, bitpos, bw);
   }
 
+  // values rel .. rel + 3 of the table (the caller masks those past its end):
+  // one binary search, then the next runs' starts checked value by value
+  __device__ __forceinline__ void table_value4(int32_t rel, uint32_t (&out)[4]) const {
+    int r = 0;
+#pragma unroll
+    for (int st = 32; st >= 1; st >>= 1) {
+      const int32_t s2 = (int32_t)shfl32((uint32_t)tr_s, r + st < 64 ? r + st : 63);
+      if (r + st < t_n && s2 <= rel) r += st;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      // runs hold >= 1 value: at most one step per value
+      const int32_t sn = (int32_t)shfl32((uint32_t)tr_s, r + 1 < 64 ? r + 1 : 63);
+      if (i > 0 && r + 1 < t_n && sn <= rel + i) r++;
+      const int32_t s0 = (int32_t)shfl32((uint32_t)tr_s, r);
+      const uint32_t v = shfl32(tr_v, r);
+      const int32_t k = (int32_t)shfl32((uint32_t)tr_k, r);
+      const int64_t bitpos = (int64_t)v * 8 + (int64_t)(rel + i - s0) * bw;
+      const uint64_t o = (uint64_t)(p + (bitpos >> 3) - W.ab);
+      const bool inwin = o + 8 <= 256;
+      const uint32_t wv = win_unpack(inwin ? bitpos : (int64_t)(W.ab - p) * 8);
+      out[i] = k ? v : inwin ? wv : unpack_u32(p, len, bitpos, bw);
+    }
+  }
+
   // Bit-packed values of the current run from the register window: the bytes
   // [lo, hi) of the stream are made resident (one refill, a 256-byte load)
   // when they fit; false when they do not (wide values: the caller reads
@@ -541,6 +566,14 @@ struct HybT {
     for (int64_t j = lo + lane_id(); j < hi; j += 64) dst[j] = (uint8_t)v;
   }
 
+  // analysis builds (-DPQ_LEVELS_SERIAL_FILL): the run-at-a-time fill
+  __device__ __forceinline__ static bool lvl_serial_fill() {
+#ifdef PQ_LEVELS_SERIAL_FILL
+    return true;
+#else
+    return false;
+#endif
+  }
   // Consume the next n values (any n), counting those == A (cA) and >= B
   // (cB): the count path of k_prepare, no value leaves the run table (RLE
   // runs count whole).  Errors as next4 would report reading them.  With
@@ -565,6 +598,27 @@ struct HybT {
           const int32_t nxt = (int32_t)shfl32((uint32_t)tr_s, lane + 1 < 64 ? lane + 1 : 63);
           const int32_t e = lane + 1 < t_n ? nxt : (int32_t)(t_end - t_base);
           const bool mine = lane < t_n;
+          if (dst && !lvl_serial_fill()) {
+            // every value of the table's part by its own lane (run found by
+            // a binary search over the lanes' run starts, table_value), one
+            // coalesced byte store per 64 values — instead of a fill or
+            // unpack loop per run, one run at a time (C4's definition
+            // streams: ~15 values a run)
+            int32_t la = 0, lb = 0;
+            for (int32_t q0 = rel0; q0 < rel1; q0 += 64) {
+              const int32_t q = q0 + lane;
+              const bool in = q < rel1;
+              const uint32_t v = table_value(in ? q : rel0);  // every lane takes part in the shuffles
+              if (in) dst[t_base + q] = (uint8_t)v;
+              la += in && v == A;
+              lb += in && v >= B;
+            }
+            cA += wave_sum32(la);
+            cB += wave_sum32(lb);
+            vdone += take;
+            left -= take;
+            continue;
+          }
           const int32_t lo = max(tr_s, rel0), hi = min(e, rel1);
           const int64_t c = mine && hi > lo ? (int64_t)(hi - lo) : 0;
           // RLE runs: whole counts, summed over the wave
