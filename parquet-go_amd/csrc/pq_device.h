@@ -605,6 +605,7 @@ struct HybT {
             // unpack loop per run, one run at a time (C4's definition
             // streams: ~15 values a run)
             int32_t la = 0, lb = 0;
+#ifndef PQ_LEVELS_LANE4
             for (int32_t q0 = rel0; q0 < rel1; q0 += 64) {
               const int32_t q = q0 + lane;
               const bool in = q < rel1;
@@ -613,6 +614,35 @@ struct HybT {
               la += in && v == A;
               lb += in && v >= B;
             }
+#else
+            // 4 values a lane, 4-aligned in memory (whole dword stores)
+            const int32_t a0 = rel0 - (int32_t)((uintptr_t)(dst + t_base + rel0) & 3);
+            for (int32_t q0 = a0; q0 < rel1; q0 += 256) {
+              const int32_t q = q0 + 4 * lane;
+              uint32_t v4[4];
+              table_value4(q < rel0 ? rel0 : (q < rel1 ? q : rel0), v4);  // every lane takes part
+              uint32_t word = 0;
+              bool all = true;
+#pragma unroll
+              for (int i = 0; i < 4; i++) {
+                const bool in = q + i >= rel0 && q + i < rel1;
+                all &= in;
+                // (a lane that starts below rel0 searched from rel0: value q + i is v4[q + i - rel0])
+                const int k = q < rel0 ? q + i - rel0 : i;
+                const uint32_t v = k >= 0 && k < 4 ? v4[k] : 0u;
+                word |= (v & 0xffu) << (8 * i);
+                la += in && v == A;
+                lb += in && v >= B;
+              }
+              if (all) {
+                *(uint32_t *)(dst + t_base + q) = word;
+              } else {
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                  if (q + i >= rel0 && q + i < rel1) dst[t_base + q + i] = (uint8_t)(word >> (8 * i));
+              }
+            }
+#endif
             cA += wave_sum32(la);
             cB += wave_sum32(lb);
             vdone += take;
