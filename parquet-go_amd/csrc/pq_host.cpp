@@ -568,13 +568,23 @@ struct pqg_ctx {
   hipStream_t stream = nullptr;
   hipStream_t side[3] = {nullptr, nullptr, nullptr};  // concurrent size-class decode launches
   hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr};
+  std::mutex launch_mu;  // (lane 0: the fields above)
+  // a second decode lane (stream, side streams, fork / join events): a
+  // pqg_stream puts consecutive slices on alternate lanes, so the next slice's
+  // decode runs beside the tail of the current one
+  struct Lane {
+    hipStream_t stream = nullptr;
+    hipStream_t side[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr};
+    std::mutex mu;
+  } lane1;
   // batch set-up stream: the H2D copies of chunk bytes run here, and a batch's
   // decodes wait on its `ready` event, so a pqg_stream worker can upload the
   // next slice while the context stream decodes the current one
   hipStream_t upload = nullptr;
-  // launch sequences (which share the fork/join events) from several host
-  // threads — a pqg_stream's worker runs counting passes beside the caller's decodes
-  std::mutex launch_mu;
+  // (launch_mu: launch sequences, which share a lane's fork / join events,
+  // from several host threads — a pqg_stream's worker runs counting passes
+  // beside the caller's decodes)
   // pinned upload ring (allocated on first use): chunk bytes are copied into
   // one buffer while the DMA of the previous one runs
   static constexpr int kRingBufs = 4;
@@ -811,6 +821,7 @@ struct pqg_batch {
   bool ready_final = false;    // `ready` recorded after every set-up copy (else copies may be in flight)
   bool counted = false;        // the last launch was the counting pass (the next decode resumes from it)
   bool all_srec = false;  // every data page has host-written records: no k_prepare work
+  int lane = 0;  // decode lane of the context (pqg_stream: alternate slices)
   std::vector<ExRec> recs_host;  // tiled PLAIN pages' static k_expand records (upload source)
   std::vector<uint8_t> tab_host;  // the small tables (d_pages, d_info, d_lists, ...): host image, uploaded at
                                   // the end of d_in
@@ -877,6 +888,18 @@ int pqg_ctx_create(int device, pqg_ctx **out) {
     }
   }
   hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
+  if (hipStreamCreateWithFlags(&c->lane1.stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->lane1.fork, hipEventDisableTiming) != hipSuccess) {
+    set_err("hipStreamCreate failed");
+    return PQG_ERR_DEVICE;
+  }
+  for (int i = 0; i < 3; i++) {
+    if (hipStreamCreateWithFlags(&c->lane1.side[i], hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->lane1.join[i], hipEventDisableTiming) != hipSuccess) {
+      set_err("hipStreamCreate failed");
+      return PQG_ERR_DEVICE;
+    }
+  }
   if (hipStreamCreateWithFlags(&c->upload, hipStreamNonBlocking) != hipSuccess) {
     set_err("hipStreamCreate failed");
     return PQG_ERR_DEVICE;
@@ -894,6 +917,12 @@ void pqg_ctx_destroy(pqg_ctx *ctx) {
     if (ctx->join[i]) hipEventDestroy(ctx->join[i]);
   }
   if (ctx->fork) hipEventDestroy(ctx->fork);
+  if (ctx->lane1.stream) hipStreamDestroy(ctx->lane1.stream);
+  for (int i = 0; i < 3; i++) {
+    if (ctx->lane1.side[i]) hipStreamDestroy(ctx->lane1.side[i]);
+    if (ctx->lane1.join[i]) hipEventDestroy(ctx->lane1.join[i]);
+  }
+  if (ctx->lane1.fork) hipEventDestroy(ctx->lane1.fork);
   if (ctx->upload) {
     hipStreamSynchronize(ctx->upload);
     hipStreamDestroy(ctx->upload);
@@ -1820,6 +1849,16 @@ static void free_dev(void *p) {
 
 static int launch_all(pqg_batch *B, bool upto_scan, bool timed);
 
+struct LaneRef {
+  hipStream_t stream;
+  hipStream_t *side;
+  hipEvent_t fork;
+  hipEvent_t *join;
+  std::mutex *mu;
+};
+static LaneRef lane_of(pqg_batch *B);
+static hipStream_t bstream(pqg_batch *B);
+
 // Everything after the batch object exists: any failure returns a status and
 // pqg_batch_create releases the partial batch (device buffers, pinned status)
 static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const int *leaves,
@@ -2462,7 +2501,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
 #endif
   if (rc) return PQG_ERR_DEVICE;
   phase("alloc");
-  hipStream_t s = ctx->stream;
+  hipStream_t s = bstream(B);  // the batch's decode lane (its counting pass)
   // one upload of all chunk bytes through the context's pinned ring, queued on
   // the upload stream (decodes wait on `ready`; the host goes on planning)
   {
@@ -2638,8 +2677,16 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   return PQG_OK;
 }
 
+static int batch_create_lane(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const int *leaves, int nleaves,
+                             int flags, int lane, pqg_batch **out);
+
 int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const int *leaves, int nleaves, int flags,
                      pqg_batch **out) {
+  return batch_create_lane(ctx, f, rg_begin, rg_end, leaves, nleaves, flags, 0, out);
+}
+
+static int batch_create_lane(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const int *leaves, int nleaves,
+                             int flags, int lane, pqg_batch **out) {
   *out = nullptr;
   if (!ctx || !f || rg_begin < 0 || rg_end > (int)f->rgs.size() || rg_begin > rg_end || nleaves < 0) {
     set_err("bad batch arguments");
@@ -2648,6 +2695,7 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
   HIPCHK(hipSetDevice(ctx->device));
   pqg_batch *B = new pqg_batch();
   B->ctx = ctx;
+  B->lane = lane;
   B->file = f;
   B->rg_begin = rg_begin;
   B->rg_end = rg_end;
@@ -2662,10 +2710,11 @@ int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const 
 }
 
 static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
-  hipStream_t s = B->ctx->stream;
+  const LaneRef LN = lane_of(B);
+  hipStream_t s = LN.stream;
   const size_t npages = B->pages.size();
-  // one launch sequence at a time per context (shared fork/join events)
-  std::lock_guard<std::mutex> launch_lock(B->ctx->launch_mu);
+  // one launch sequence at a time per lane (shared fork/join events)
+  std::lock_guard<std::mutex> launch_lock(*LN.mu);
   if (B->ready) hipStreamWaitEvent(s, B->ready, 0);  // the chunk bytes are on the device
   if (timed && !B->ev[B->ring_head][0])  // timing events of this ring slot, made on first use
     for (int i = 0; i < 8; i++) hipEventCreate(&B->ev[B->ring_head][i]);
@@ -2768,16 +2817,16 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     pq_launch_args al = a;
     al.list = B->d_lists + ns + nd;
     al.nlist = ndata;
-    hipEventRecord(B->ctx->fork, s);
-    hipStreamWaitEvent(B->ctx->side[2], B->ctx->fork, 0);
+    hipEventRecord(LN.fork, s);
+    hipStreamWaitEvent(LN.side[2], LN.fork, 0);
     // PQG_LEVELS_CAP=k: k workgroups per CU looping over the pages, resident
     // from the start beside k_snappy's.  Measured on C3 (ms a step): full
     // grid 5.38, k = 1 6.52, 2 5.91, 4 5.43, 8 5.37 — resident waves beside
     // k_snappy's get too little issue; the full grid stays
     static const int lv_cap = getenv("PQG_LEVELS_CAP") ? atoi(getenv("PQG_LEVELS_CAP")) : 0;
     al.grid_cap = lv_cap > 0 ? lv_cap * B->ctx->cus : 0;
-    e |= pq_launch(lv_id, &al, B->ctx->side[2]);  // k_levels<-1>: every level page
-    hipEventRecord(B->ctx->join[2], B->ctx->side[2]);
+    e |= pq_launch(lv_id, &al, LN.side[2]);  // k_levels<-1>: every level page
+    hipEventRecord(LN.join[2], LN.side[2]);
   }
   a.list = B->d_lists;
   a.nlist = ns;
@@ -2810,14 +2859,14 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
       const char *v = getenv("PQG_WALK_SIDE");
       return v && v[0] == '1';
     }();
-    hipStream_t ss = side && walk_side ? ctx->side[0] : s;   // the serial chain
-    hipStream_t sw = side && !walk_side ? ctx->side[0] : s;  // whole data pages
+    hipStream_t ss = side && walk_side ? LN.side[0] : s;   // the serial chain
+    hipStream_t sw = side && !walk_side ? LN.side[0] : s;  // whole data pages
     // (the whole dictionary pages and k_dict_prepare stay on the chain: a
     // BYTE_ARRAY dictionary page may itself be segmented — C5's l_comment
     // dictionaries — and k_dict_prepare reads what its segments write)
     if (side) {
-      hipEventRecord(ctx->fork, s);
-      hipStreamWaitEvent(ctx->side[0], ctx->fork, 0);
+      hipEventRecord(LN.fork, s);
+      hipStreamWaitEvent(LN.side[0], LN.fork, 0);
     }
     if (one) {
       a.nitems = nwhole + ndict;
@@ -2852,8 +2901,8 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
       e |= pq_launch(0, &a, sw);  // k_snappy: whole data pages
     }
     if (side) {
-      hipEventRecord(ctx->join[0], ctx->side[0]);
-      hipStreamWaitEvent(s, ctx->join[0], 0);
+      hipEventRecord(LN.join[0], LN.side[0]);
+      hipStreamWaitEvent(s, LN.join[0], 0);
     }
   }
   // without BYTE_ARRAY dictionaries nothing k_prepare reads waits on k_copy
@@ -2861,7 +2910,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   // in one launch and those pages after it (with string dictionaries, the
   // string pages would all wait: measured slower)
   const bool fused = nd == 0 && (B->max_jobs > 0 || !B->hjobs.empty()) && !B->seg_times;
-  if (lvl_early) hipStreamWaitEvent(s, B->ctx->join[2], 0);  // the levels and counts k_prepare reads
+  if (lvl_early) hipStreamWaitEvent(s, LN.join[2], 0);  // the levels and counts k_prepare reads
   const bool lvl_now = B->lvl_bytes && !lvl_early;
   // long PLAIN string pages: the length walk region-parallel (after the
   // copies and k_levels' non-null counts; k_prepare reads the result)
@@ -2922,28 +2971,28 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     const int32_t npstr = (int32_t)(B->pstr_items.size() / 2);
     const bool str_side = B->ngen_str > 0 || npstr > 0;
     const bool fork = B->ngen_flat > 0 || str_side || B->ngen_nest > 0;
-    if (fork) hipEventRecord(ctx->fork, s);
+    if (fork) hipEventRecord(LN.fork, s);
     if (B->ngen_flat > 0) {
-      hipStreamWaitEvent(ctx->side[0], ctx->fork, 0);
+      hipStreamWaitEvent(LN.side[0], LN.fork, 0);
       a.list = B->d_lists + ns + nd + ndata + ng0;
       a.nlist = B->ngen_flat;
-      e |= pq_launch(14, &a, ctx->side[0]);  // k_decode<1>: flat fixed-width pages
-      hipEventRecord(ctx->join[0], ctx->side[0]);
+      e |= pq_launch(14, &a, LN.side[0]);  // k_decode<1>: flat fixed-width pages
+      hipEventRecord(LN.join[0], LN.side[0]);
     }
     if (str_side) {
-      hipStreamWaitEvent(ctx->side[1], ctx->fork, 0);
+      hipStreamWaitEvent(LN.side[1], LN.fork, 0);
       if (npstr > 0) {  // k_plain_str: flat required PLAIN string pages, items of PLAIN_STR_ITEM values
         a.list = B->d_lists + ns + nd + ndata + ngen + (int32_t)B->dba_list.size();
         a.nlist = npstr;
-        e |= pq_launch(23, &a, ctx->side[1]);
+        e |= pq_launch(23, &a, LN.side[1]);
       }
       a.list = B->d_lists + ns + nd + ndata + ng0 + B->ngen_flat;
       a.nlist = B->ngen_str;
-      e |= pq_launch(15, &a, ctx->side[1]);  // k_decode<2>: flat BYTE_ARRAY pages
-      hipEventRecord(ctx->join[1], ctx->side[1]);
+      e |= pq_launch(15, &a, LN.side[1]);  // k_decode<2>: flat BYTE_ARRAY pages
+      hipEventRecord(LN.join[1], LN.side[1]);
     }
     if (B->ngen_nest > 0) {
-      hipStreamWaitEvent(ctx->side[2], ctx->fork, 0);
+      hipStreamWaitEvent(LN.side[2], LN.fork, 0);
       a.list = B->d_lists + ns + nd + ndata + ng0 + B->ngen_flat + B->ngen_str;
       a.nlist = B->ngen_nest;
       const int32_t nparts = (int32_t)(B->nest_parts.size() / 3);
@@ -2951,14 +3000,14 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
         pq_launch_args ap = a;
         ap.parts = B->d_parts;
         ap.nlist = nparts;
-        e |= pq_launch(16, &ap, ctx->side[2]);  // k_decode<3>: parts of list pages of fixed-width values
+        e |= pq_launch(16, &ap, LN.side[2]);  // k_decode<3>: parts of list pages of fixed-width values
         ap = a;
         ap.redo = 1;
-        e |= pq_launch(16, &ap, ctx->side[2]);  // k_decode<3>: pages whose later parts failed, whole
+        e |= pq_launch(16, &ap, LN.side[2]);  // k_decode<3>: pages whose later parts failed, whole
       } else {
-        e |= pq_launch(16, &a, ctx->side[2]);  // k_decode<3>: lists of fixed-width values
+        e |= pq_launch(16, &a, LN.side[2]);  // k_decode<3>: lists of fixed-width values
       }
-      hipEventRecord(ctx->join[2], ctx->side[2]);
+      hipEventRecord(LN.join[2], LN.side[2]);
     }
     a.list = B->d_lists + ns + nd + ndata;
     a.nlist = ng0;
@@ -2966,7 +3015,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     // (k_plain_str beside k_decode<2> on another side stream, and the tiled
     // expand beside both, were measured on C5: 24.50 vs 24.28 ms — the three
     // are throughput-bound and only slowed each other)
-    if (str_side) hipStreamWaitEvent(s, ctx->join[1], 0);
+    if (str_side) hipStreamWaitEvent(s, LN.join[1], 0);
     if (!B->dba_list.empty()) {  // DELTA_BYTE_ARRAY value bytes (after k_decode's offsets)
       a.list = B->d_lists + ns + nd + ndata + ngen;
       a.nlist = (int32_t)B->dba_list.size();
@@ -2978,18 +3027,18 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     static const int big_order = getenv("PQG_BIG_ORDER") ? atoi(getenv("PQG_BIG_ORDER")) : 0;
     const bool big = B->ldn[2] + B->ldn[3] > 0;
     if (big && big_order == 2) {
-      hipEventRecord(ctx->fork, s);
-      hipStreamWaitEvent(ctx->side[1], ctx->fork, 0);
-      e |= pq_launch(22, &a, ctx->side[1]);
-      hipEventRecord(ctx->join[1], ctx->side[1]);
+      hipEventRecord(LN.fork, s);
+      hipStreamWaitEvent(LN.side[1], LN.fork, 0);
+      e |= pq_launch(22, &a, LN.side[1]);
+      hipEventRecord(LN.join[1], LN.side[1]);
     }
     if (big && big_order == 1) e |= pq_launch(22, &a, s);
     e |= pq_launch(9, &a, s);  // k_expand_mix (tiled pages)
     if (big && big_order == 0) e |= pq_launch(22, &a, s);
-    if (big && big_order == 2) hipStreamWaitEvent(s, ctx->join[1], 0);
+    if (big && big_order == 2) hipStreamWaitEvent(s, LN.join[1], 0);
     if (B->ldn[4] + B->ldn[5] > 0) e |= pq_launch(27, &a, s);  // k_expand_pass (wide dictionaries)
-    if (B->ngen_flat > 0) hipStreamWaitEvent(s, ctx->join[0], 0);
-    if (B->ngen_nest > 0) hipStreamWaitEvent(s, ctx->join[2], 0);
+    if (B->ngen_flat > 0) hipStreamWaitEvent(s, LN.join[0], 0);
+    if (B->ngen_nest > 0) hipStreamWaitEvent(s, LN.join[2], 0);
     mark(true);
     a.list = B->d_lists + ns + nd;
     a.nlist = ndata;
@@ -3012,6 +3061,13 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   return PQG_OK;
 }
 
+static LaneRef lane_of(pqg_batch *B) {
+  pqg_ctx *c = B->ctx;
+  if (B->lane == 1) return {c->lane1.stream, c->lane1.side, c->lane1.fork, c->lane1.join, &c->lane1.mu};
+  return {c->stream, c->side, c->fork, c->join, &c->launch_mu};
+}
+static hipStream_t bstream(pqg_batch *B) { return B->lane == 1 ? B->ctx->lane1.stream : B->ctx->stream; }
+
 int pqg_batch_decode(pqg_batch *B) {
   if (!B) return PQG_ERR_ARG;
   HIPCHK(hipSetDevice(B->ctx->device));
@@ -3032,7 +3088,7 @@ int pqg_batch_set_timing(pqg_batch *B, int every) {
 int pqg_batch_sync(pqg_batch *B) {
   if (!B) return PQG_ERR_ARG;
   HIPCHK(hipSetDevice(B->ctx->device));
-  HIPCHK(hipStreamSynchronize(B->ctx->stream));
+  HIPCHK(hipStreamSynchronize(bstream(B)));
   const size_t npages = B->pages.size();
   std::vector<uint32_t> st(npages);
   if (npages)
@@ -3123,7 +3179,7 @@ int pqg_batch_copy(pqg_batch *B, int i, int buf, void *dst, size_t cap, size_t *
     return PQG_ERR_ARG;
   }
   if (n) {
-    HIPCHK(hipStreamSynchronize(B->ctx->stream));
+    HIPCHK(hipStreamSynchronize(bstream(B)));
     HIPCHK(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost));
   }
   return PQG_OK;
@@ -3168,7 +3224,7 @@ int pqg_batch_kernel_times(pqg_batch *B, const char **names, float *ms, int cap)
   int n = B->nev > 0 ? B->nev - 1 : 0;
   if (hipSetDevice(B->ctx->device) != hipSuccess) return 0;
   if (B->ring_count > 0) {
-    hipStreamSynchronize(B->ctx->stream);
+    hipStreamSynchronize(bstream(B));
     for (int i = 0; i < 8; i++) B->kms_sum[i] = 0;
     B->kms_n = 0;
     for (int k = 0; k < B->ring_count; k++) {
@@ -3196,7 +3252,7 @@ void pqg_batch_destroy(pqg_batch *B) {
   // failed part-way may have copies queued after its last `ready` record
   if (B->ready_final) hipEventSynchronize(B->ready);
   else hipStreamSynchronize(B->ctx->upload);
-  hipStreamSynchronize(B->ctx->stream);
+  hipStreamSynchronize(bstream(B));
   for (auto &cp : B->cols) {
     free_dev(cp.values);
     free_dev(cp.validity);
@@ -3247,6 +3303,9 @@ struct pqg_stream {
   std::vector<int> rcs;
   std::vector<std::string> errs;
   std::vector<char> done;     // per slice: built (or failed)
+  std::vector<char> launched;  // per slice: its decode already launched (ahead of its turn)
+  std::vector<int> lrc;        // that launch's status
+  int lanes = 2;              // decode lanes: slice k on lane k % 2 (PQG_STREAM_LANES=1: one)
   size_t next_build = 0;      // next slice a worker takes
   size_t ntaken = 0;
   bool stop = false, failed = false;
@@ -3273,8 +3332,9 @@ static void stream_worker(pqg_stream *S) {
       k = S->next_build++;
     }
     pqg_batch *B = nullptr;
-    const int rc = pqg_batch_create(S->ctx, S->f, S->slices[k].first, S->slices[k].second,
-                                    S->leaves.empty() ? nullptr : S->leaves.data(), (int)S->leaves.size(), S->flags, &B);
+    const int rc = batch_create_lane(S->ctx, S->f, S->slices[k].first, S->slices[k].second,
+                                     S->leaves.empty() ? nullptr : S->leaves.data(), (int)S->leaves.size(), S->flags,
+                                     S->lanes > 1 ? (int)(k & 1) : 0, &B);
     std::lock_guard<std::mutex> lk(S->mu);
     S->built[k] = B;
     S->rcs[k] = rc;
@@ -3311,6 +3371,9 @@ int pqg_stream_open(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const i
   S->rcs.assign(S->slices.size(), 0);
   S->errs.assign(S->slices.size(), std::string());
   S->done.assign(S->slices.size(), 0);
+  S->launched.assign(S->slices.size(), 0);
+  S->lrc.assign(S->slices.size(), 0);
+  if (getenv("PQG_STREAM_LANES") && atoi(getenv("PQG_STREAM_LANES")) == 1) S->lanes = 1;
   const char *w = getenv("PQG_STREAM_WORKERS");
   const int nw = std::max(1, std::min({w ? atoi(w) : 3, depth, (int)std::max<size_t>(1, S->slices.size())}));
   for (int i = 0; i < nw; i++) S->workers.emplace_back(stream_worker, S);
@@ -3346,9 +3409,23 @@ int pqg_stream_next(pqg_stream *S, pqg_batch **out, int *rg_first) {
   }
   pqg_batch *B = S->built[k];
   S->built[k] = nullptr;
-  const int rc = pqg_batch_decode(B);
+  const int rc = S->launched[k] ? S->lrc[k] : pqg_batch_decode(B);
   S->cur = B;
   if (rc) return rc;
+  // decode-ahead: the next slice, if built, starts on the other lane now — it
+  // runs beside this one's tail (a slice's decode lasts at least its longest
+  // page chain) and while the caller consumes this one
+  if (S->lanes > 1 && k + 1 < S->slices.size()) {
+    pqg_batch *N = nullptr;
+    {
+      std::lock_guard<std::mutex> lk(S->mu);
+      if (S->done[k + 1] && !S->rcs[k + 1] && S->built[k + 1]) N = S->built[k + 1];
+    }
+    if (N) {
+      S->lrc[k + 1] = pqg_batch_decode(N);
+      S->launched[k + 1] = 1;
+    }
+  }
   *out = B;
   if (rg_first) *rg_first = S->slices[k].first;
   return PQG_OK;
@@ -3517,7 +3594,7 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
 // diagnostic build only (not part of include/pqgpu.h): copy the stamp buffer
 // diagnostic: zero the stamp buffers (before the decode a tool reads back)
 extern "C" int pqg_diag_reset(pqg_batch *B) {
-  hipStreamSynchronize(B->ctx->stream);
+  hipStreamSynchronize(bstream(B));
   const size_t n1 = std::max(8 * 4 * (B->tiles.size() + 1), 4 * (B->pages.size() + 1));
   const size_t n2 = 16 * (B->pages.size() + 1) + 256;
   if (B->d_dbg) hipMemset(B->d_dbg, 0, 8 * n1);
@@ -3531,13 +3608,13 @@ extern "C" int pqg_diag_page_cols(pqg_batch *B, int32_t *out, size_t n) {
   return (int)k;
 }
 extern "C" int pqg_diag_stamps(pqg_batch *B, uint64_t *out, size_t n) {
-  hipStreamSynchronize(B->ctx->stream);
+  hipStreamSynchronize(bstream(B));
   size_t cap = std::max(8 * 4 * (B->tiles.size() + 1), 4 * (B->pages.size() + 1));
   if (n > cap) n = cap;
   return hipMemcpy(out, B->d_dbg, n * 8, hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
 }
 extern "C" int pqg_diag_stamps2(pqg_batch *B, uint64_t *out, size_t n) {
-  hipStreamSynchronize(B->ctx->stream);
+  hipStreamSynchronize(bstream(B));
   size_t cap = 16 * (B->pages.size() + 1) + 256;
   if (n > cap) n = cap;
   return hipMemcpy(out, B->d_dbg2, n * 8, hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
