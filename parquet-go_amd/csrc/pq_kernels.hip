@@ -1758,9 +1758,11 @@ __global__ __launch_bounds__(64) void k_sw_regions(KArgs a) {
     // the low bytes of the next header, ~7 KB for text — jumps out in one.
     // The first weak one is taken only when the region has no strong one
     // (an entry spanning the region end)
-    int64_t cand = -1, weak = -1;
+    // (the strong candidate's hops are the start of its walk below)
+    int64_t cand = -1, weak = -1, cp = 0, cls = 0;
+    int32_t ccnt = 0;
     for (int64_t s0 = rs; s0 < re && cand < 0; s0++) {
-      int64_t p = s0;
+      int64_t p = s0, ls = 0;
       bool ok = true;
       int h = 0;
       for (; h < SW_K && p < re; h++) {
@@ -1769,16 +1771,27 @@ __global__ __launch_bounds__(64) void k_sw_regions(KArgs a) {
           ok = false;
           break;
         }
+        ls += l;
         p += 4 + (int64_t)l;
       }
       if (!ok) continue;
-      if (h >= 2 || p == vlen) cand = s0;
-      else if (weak < 0) weak = s0;
+      if (h >= 2 || p == vlen) {
+        cand = s0;
+        cp = p;
+        ccnt = h;
+        cls = ls;
+      } else if (weak < 0) {
+        weak = s0;
+      }
     }
-    if (cand < 0) cand = weak;
+    if (cand < 0 && weak >= 0) {
+      cand = cp = weak;
+      ccnt = 0;
+      cls = 0;
+    }
     if (cand >= 0) {
-      int64_t p = cand, ls = 0;
-      int32_t cnt = 0;
+      int64_t p = cp, ls = cls;
+      int32_t cnt = ccnt;
       uint32_t err = E_OK;
       while (p < re) {
         if (p + 4 > vlen) {
@@ -4913,7 +4926,9 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
   }
   if (which == 12) {  // k_prepare_copy: the prepare blocks, then the copy grid
     const uint32_t items = (k.max_jobs + (uint32_t)k.nhjobs) * pq::COPY_ITEMS;
-    const uint32_t cb = items < 1024 ? items : 1024;
+    // PQG_COPY_BLOCKS: the copy grid's cap (analysis)
+    static const uint32_t cap = getenv("PQG_COPY_BLOCKS") ? (uint32_t)atoi(getenv("PQG_COPY_BLOCKS")) : 1024u;
+    const uint32_t cb = items < cap ? items : cap;
     const uint32_t pb = ((uint32_t)(k.nlist > 0 ? k.nlist : 0) + 3) / 4;
     if (pb + cb == 0) return 0;
     hipLaunchKernelGGL(pq::k_prepare_copy, dim3(pb + (cb ? cb : 1)), dim3(256), 0, s, k);
