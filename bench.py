@@ -313,7 +313,7 @@ def segment_times(reader, rg0, rg1, decodes=6):
         b.close()
 
 
-def e2e_rates(reader, rg0, rg1, stats, slice_counts=(4, 8, 24), depth=8):
+def e2e_rates(reader, rg0, rg1, stats, slice_counts=(2, 4, 8, 24), depth=8):
     """PCIe-inclusive rates (never `value`): the whole shard read through
     pqg_stream — the host worker plans and uploads slice k + 1 (pinned ring,
     PQG_UPLOAD_THREADS gather threads) while the GPU decodes slice k — timed
