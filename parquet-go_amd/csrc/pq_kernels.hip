@@ -1758,11 +1758,9 @@ __global__ __launch_bounds__(64) void k_sw_regions(KArgs a) {
     // the low bytes of the next header, ~7 KB for text — jumps out in one.
     // The first weak one is taken only when the region has no strong one
     // (an entry spanning the region end)
-    // (the strong candidate's hops are the start of its walk below)
-    int64_t cand = -1, weak = -1, cp = 0, cls = 0;
-    int32_t ccnt = 0;
+    int64_t cand = -1, weak = -1;
     for (int64_t s0 = rs; s0 < re && cand < 0; s0++) {
-      int64_t p = s0, ls = 0;
+      int64_t p = s0;
       bool ok = true;
       int h = 0;
       for (; h < SW_K && p < re; h++) {
@@ -1771,27 +1769,16 @@ __global__ __launch_bounds__(64) void k_sw_regions(KArgs a) {
           ok = false;
           break;
         }
-        ls += l;
         p += 4 + (int64_t)l;
       }
       if (!ok) continue;
-      if (h >= 2 || p == vlen) {
-        cand = s0;
-        cp = p;
-        ccnt = h;
-        cls = ls;
-      } else if (weak < 0) {
-        weak = s0;
-      }
+      if (h >= 2 || p == vlen) cand = s0;
+      else if (weak < 0) weak = s0;
     }
-    if (cand < 0 && weak >= 0) {
-      cand = cp = weak;
-      ccnt = 0;
-      cls = 0;
-    }
+    if (cand < 0) cand = weak;
     if (cand >= 0) {
-      int64_t p = cp, ls = cls;
-      int32_t cnt = ccnt;
+      int64_t p = cand, ls = 0;
+      int32_t cnt = 0;
       uint32_t err = E_OK;
       while (p < re) {
         if (p + 4 > vlen) {
