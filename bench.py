@@ -30,8 +30,10 @@ Besides the timed loop (rank 0, N = 1), outside the timed region:
     its kernels' traced time per step) and two `--pmc` child runs give
     FETCH_SIZE / WRITE_SIZE per kernel per step (`roofline.traffic`: every
     dispatch of the phase's kernels in a step);
-  * every row group of the shard is decoded again and compared bit-exactly
-    with the oracle;
+  * on every rank, the timed batch's own buffers (the whole shard, every
+    leaf) are compared bit-exactly with the oracle's decode of the shard, and
+    every row group is decoded again in a batch of its own and compared too
+    (N > 1: a mismatch flag is all-reduced);
   * the CPU oracle (and pyarrow, when importable) decodes a bounded sample of
     the same file (cpu_baseline).
 
@@ -420,12 +422,58 @@ def parity_check(reader, rg0, rg1, threads):
                         if not np.array_equal(got[k], ref[i][k]):
                             for f in pending.values():
                                 f.cancel()
-                            return "MISMATCH in row group %d leaf %s buffer %s" % (rg, info["name"], k)
+                            return False, "MISMATCH in row group %d leaf %s buffer %s" % (rg, info["name"], k)
             finally:
                 b.close()
             ok += 1
-    return "bit-exact vs oracle: %d/%d row groups of the shard, %d leaves, every buffer (%.1f s)" % (
+    return True, "per-RG batches bit-exact vs oracle: %d/%d row groups, %d leaves, every buffer (%.1f s)" % (
         ok, rg1 - rg0, len(cols), time.perf_counter() - t0)
+
+
+def timed_batch_parity(batch, reader, rg0, rg1, threads):
+    """The timed batch itself — the buffers its last timed decode left on the
+    device, every selected leaf over the whole shard [rg0, rg1) — copied back
+    and compared bit-exactly with the oracle's decode of the same row-group
+    range (oracle/pqref.c; type_dict.go:39-59, chunk_reader.go:380-402).  The
+    per-row-group batches of parity_check take other kernel routes (a lone
+    row group's big dictionary runs k_expand_big, the XCD dealing differs),
+    so this is the check that pins the headline's own bytes.  Oracle decodes
+    run on `threads` host threads, a few leaves ahead of the GPU copies.
+    Returns (ok, text)."""
+    import concurrent.futures as cf
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    cols = reader.Columns()
+    o = oracle.File(open(reader.path, "rb").read())
+    keys = ("values", "validity", "list_offsets", "list_validity", "str_offsets")
+    leaves = list(batch.leaves)
+    t0 = time.perf_counter()
+    window = max(1, min(len(leaves), threads, 4))
+    with cf.ThreadPoolExecutor(window) as ex:
+        pending = {}
+        for i, leaf in enumerate(leaves):
+            for j in range(i, min(len(leaves), i + window)):
+                if j not in pending:
+                    pending[j] = ex.submit(o.decode, leaves[j], rg0, rg1)
+            ref = pending.pop(i).result()
+            got = batch.column(i)
+            info = cols[leaf]
+            for k in keys:
+                if k == "validity" and info["max_def"] == 0:
+                    continue
+                if k in ("list_offsets", "list_validity") and info["max_rep"] != 1:
+                    continue
+                if got[k].size != ref[k].size or not np.array_equal(got[k], ref[k]):
+                    for f in pending.values():
+                        f.cancel()
+                    return False, "MISMATCH in the timed batch: leaf %s buffer %s (%d vs %d bytes)" % (
+                        info["name"], k, got[k].size, ref[k].size)
+            for k in ("slots", "str_bytes"):
+                if got[k] != ref[k]:
+                    return False, "MISMATCH in the timed batch: leaf %s count %s" % (info["name"], k)
+            del got, ref
+    return True, "timed batch bit-exact vs oracle (%d RGs, %d leaves, every buffer, %.1f s)" % (
+        rg1 - rg0, len(leaves), time.perf_counter() - t0)
 
 
 def pyarrow_baseline(path, cores, out_bytes, total_rows, budget_s=4.0):
@@ -595,6 +643,22 @@ def main():
         ta = time.perf_counter() - ta
         gb = sum(v.numel() * v.element_size() for v in col.values() if hasattr(v, "numel")) / 1e9
         allgather = {"leaf": 0, "GB_per_rank": round(gb, 4), "ms": round(ta * 1e3, 3), "GBps_per_rank": round(gb / ta, 1)}
+    parity = None
+    if not (args.child or args.no_parity):
+        # the timed batch's own output, on every rank, before it is closed
+        ok, txt = timed_batch_parity(batch, reader, rg0, rg1, cpu_cores()[0])
+        if ok:
+            ok2, txt2 = parity_check(reader, rg0, rg1, cpu_cores()[0])
+            ok, txt = ok and ok2, txt + " + " + txt2
+        if dist is not None:
+            import torch
+            dev = torch.device("cuda", device) if args.dist_backend == "nccl" else torch.device("cpu")
+            f = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(f, op=dist.ReduceOp.MIN)  # every rank's shard must be bit-exact
+            ranks_ok = int(f.item()) == 1
+            txt = ("all %d ranks: " % world if ranks_ok else "MISMATCH on some rank; rank %d: " % rank) + txt
+            ok = ok and ranks_ok
+        parity = {"ok": ok, "text": txt}
     batch.close()
     if args.child:
         if dist is not None:
@@ -630,6 +694,9 @@ def main():
     }
     if allgather:
         line["config"]["allgather"] = allgather
+    if parity is not None:
+        line["config"]["parity"] = parity["text"]
+        line["config"]["parity_ok"] = parity["ok"]
     if rank == 0 and world == 1:
         seg = segment_times(reader, rg0, rg1)
         line["config"]["phase_ms"] = {k: round(v, 4) for k, v in seg.items()}
@@ -673,8 +740,6 @@ def main():
                     line["roofline"]["traffic_unit"] = ("MB per decode step, summed over every dispatch of the "
                                                         "phase's kernels (FETCH_SIZE x 2 + WRITE_SIZE)")
                     line["roofline"]["traffic_vs_algorithmic"] = round(tr / phase_bytes(dom, stats), 3)
-        if not args.no_parity:
-            line["config"]["parity"] = parity_check(reader, rg0, rg1, cpu_cores()[0])
         line["config"]["e2e"].update(e2e_rates(reader, rg0, rg1, stats))
     if "roofline" not in line:
         # N > 1: the decode phase, HIP events over the timed steps (per rank)

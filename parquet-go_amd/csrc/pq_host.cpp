@@ -1295,16 +1295,29 @@ static bool getenv_flag(const char *name) {
   return v && v[0] == '1';
 }
 
+// decodedLen's binary.Uvarint (decode.go:38-46), with k_snappy's rules exactly:
+// up to 10 bytes, the 10th at most 1, over-long (non-minimal) encodings
+// accepted.  Returns the header length, 0 when the varint is malformed.
+static int64_t snappy_uvarint(const uint8_t *p, int64_t n, uint64_t *v) {
+  uint64_t x = 0;
+  uint32_t sh = 0;
+  for (int64_t i = 0; i < n; i++) {
+    const uint8_t b = p[i];
+    if (b < 0x80) {
+      if (i > 9 || (i == 9 && b > 1)) return 0;
+      *v = x | ((uint64_t)b << (sh & 63));
+      return i + 1;
+    }
+    if (sh < 64) x |= (uint64_t)(b & 0x7f) << sh;
+    sh += 7;
+  }
+  return 0;
+}
+
 static bool snappy_single_literal(const uint8_t *p, int64_t n, int64_t expect, int64_t *data) {
   uint64_t v = 0;
-  int64_t i = 0;
-  for (int sh = 0;; sh += 7) {
-    if (i >= n || i >= 5) return false;
-    const uint8_t b = p[i++];
-    v |= (uint64_t)(b & 0x7f) << sh;
-    if (b < 0x80) break;
-  }
-  if (v == 0 || v != (uint64_t)expect || v > 0xffffffffull || i >= n) return false;
+  int64_t i = snappy_uvarint(p, n, &v);
+  if (i == 0 || v == 0 || v != (uint64_t)expect || v > 0xffffffffull || i >= n) return false;
   const uint8_t tag = p[i];
   if (tag & 3) return false;
   uint64_t x = tag >> 2;
@@ -1333,14 +1346,8 @@ static bool snappy_single_literal(const uint8_t *p, int64_t n, int64_t expect, i
 static bool snappy_literal_train(const uint8_t *p, int64_t n, int64_t expect, std::vector<int64_t> &lits) {
   lits.clear();
   uint64_t v = 0;
-  int64_t i = 0;
-  for (int sh = 0;; sh += 7) {
-    if (i >= n || i >= 5) return false;
-    const uint8_t b = p[i++];
-    v |= (uint64_t)(b & 0x7f) << sh;
-    if (b < 0x80) break;
-  }
-  if (v == 0 || v != (uint64_t)expect || v > 0xffffffffull) return false;
+  int64_t i = snappy_uvarint(p, n, &v);
+  if (i == 0 || v == 0 || v != (uint64_t)expect || v > 0xffffffffull) return false;
   const int64_t max_lits = expect / 4096 + 1;
   int64_t d = 0;
   while (i < n) {

@@ -807,7 +807,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PQ_SNAPPY_W
             for (int k = 0; k < extra; k++) x |= W.byte_at(src + s + 1 + k) << (8 * k);
           }
         }
-        if (ok && (int64_t)x + 1 == dl && s + hs + dl == slen &&
+        // (never for a page whose k_expand records the host wrote: they read
+        // staging, so the block must be staged)
+        if (ok && (int64_t)x + 1 == dl && s + hs + dl == slen && !d.srec &&
             (d.kind != PAGE_DICT || d.alias_any || ((d.src + lsize + s + hs) & 7) == 0)) {
           if (lane == 0) a.info[page].alias1 = 1 + (int64_t)(d.src + lsize + s + hs);
           return;
@@ -1107,7 +1109,7 @@ __global__ __launch_bounds__(64) void k_snappy_walk(KArgs a) {
             for (int k = 0; k < extra; k++) x |= W.byte_at(src + s + 1 + k) << (8 * k);
           }
         }
-        if (lok && (int64_t)x + 1 == expect && s + hs + expect == slen &&
+        if (lok && (int64_t)x + 1 == expect && s + hs + expect == slen && !d.srec &&
             (d.kind != PAGE_DICT || d.alias_any || ((d.src + lsize + s + hs) & 7) == 0)) {
           if (lane == 0) a.info[page].alias1 = 1 + (int64_t)(d.src + lsize + s + hs);
           flag = 2;

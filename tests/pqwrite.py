@@ -162,12 +162,15 @@ def write(schema, columns):
     return bytes(out)
 
 
-def write_column(pages, ptype=1, encoding=5, optional=False, type_length=0, dict_page=None, dict_count=0):
+def write_column(pages, ptype=1, encoding=5, optional=False, type_length=0, dict_page=None, dict_count=0,
+                 codec=0, compress=None):
     """One leaf `v` (parquet.Type `ptype`, REQUIRED or OPTIONAL), one row group,
-    V1 uncompressed data pages whose values sections are given as bytes:
+    V1 data pages whose values sections are given as bytes:
     pages = [(num_values, def_levels or None, values_section_bytes)].  With
     `optional`, def levels go in front of each values section as one
-    bit-packed hybrid run (bit width 1).  Returns the file bytes."""
+    bit-packed hybrid run (bit width 1).  `codec` (parquet.CompressionCodec)
+    names the chunk's codec and `compress(page_body) -> bytes` writes each data
+    page's stored bytes (default: uncompressed).  Returns the file bytes."""
     elems = [_S().str(4, "schema").i32(5, 1)]
     leaf = _S().i32(1, ptype)
     if type_length:
@@ -191,10 +194,11 @@ def write_column(pages, ptype=1, encoding=5, optional=False, type_length=0, dict
             b += struct.pack("<I", len(s)) + s
         b += body
         dph = _S().i32(1, n).i32(2, encoding).i32(3, 3).i32(4, 3)
-        out += _S().i32(1, 0).i32(2, len(b)).i32(3, len(b)).struct(5, dph).done() + b
+        stored = compress(bytes(b)) if compress else bytes(b)
+        out += _S().i32(1, 0).i32(2, len(b)).i32(3, len(stored)).struct(5, dph).done() + stored
         n_total += n
     size = len(out) - first
-    meta = (_S().i32(1, ptype).list(2, T_I32, [0, 3, encoding]).list(3, T_BINARY, ["v"]).i32(4, 0).i64(5, n_total)
+    meta = (_S().i32(1, ptype).list(2, T_I32, [0, 3, encoding]).list(3, T_BINARY, ["v"]).i32(4, codec).i64(5, n_total)
             .i64(6, size).i64(7, size).i64(9, data_off))
     if dict_off is not None:
         meta.i64(11, dict_off)

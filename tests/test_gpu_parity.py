@@ -624,6 +624,44 @@ def test_snappy_literal_train_pages():
             check_file(bytes(data), "train v%s corrupt %d" % (ver, trial))
 
 
+def _snappy_one_literal(body, varint_len):
+    """A raw Snappy block that is one literal holding `body`, its decoded-length
+    uvarint padded to `varint_len` bytes (binary.Uvarint accepts non-minimal
+    encodings, decode.go:38-46)."""
+    n, vb = len(body), bytearray()
+    for i in range(varint_len):
+        b = (n >> (7 * i)) & 0x7F
+        vb.append(b | (0x80 if i < varint_len - 1 else 0))
+    assert n >> (7 * varint_len) == 0
+    x = n - 1
+    extra = (x.bit_length() + 7) // 8
+    tag = bytes([x << 2]) if x < 60 else bytes([(59 + extra) << 2]) + x.to_bytes(extra, "little")
+    return bytes(vb) + tag + body
+
+
+def test_snappy_single_literal_padded_varint():
+    """Flat required PLAIN INT64 / INT32 Snappy pages written as one literal
+    whose length uvarint is non-minimal (3..10 bytes): the host plan and
+    k_snappy must read the varint by the same rules, or a page the host left to
+    k_snappy but planned records for (tiled PLAIN) reads unstaged bytes."""
+    import pqwrite
+    rng = np.random.default_rng(77)
+    for ptype, width in ((2, 8), (1, 4)):
+        for vlen in (3, 5, 6, 7, 9, 10):
+            pages = []
+            for n in (8000, 3, 20000):
+                vals = rng.integers(-2**62, 2**62, n, dtype=np.int64)
+                body = (vals if width == 8 else vals.astype(np.int32)).tobytes()
+                pages.append((n, None, body))
+            data = pqwrite.write_column(pages, ptype=ptype, encoding=0, codec=1,
+                                        compress=lambda b, v=vlen: _snappy_one_literal(b, v))
+            check_file(data, "padded varint %d type %d" % (vlen, ptype))
+    # an 11-byte (over-long) varint is ErrCorrupt in both
+    data = pqwrite.write_column([(100, None, bytes(800))], ptype=2, encoding=0, codec=1,
+                                compress=lambda b: b"\x80" * 10 + b"\x00" + _snappy_one_literal(b, 2)[2:])
+    check_file(data, "varint 11 bytes")
+
+
 def test_boolean_columns_generated():
     """BOOLEAN (type_boolean.go): PLAIN bit-packed and RLE pages, nullable,
     required and inside lists, V1 and V2."""

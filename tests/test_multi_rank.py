@@ -206,15 +206,15 @@ def test_gpu_shards_allgather(tmp_path, name, leaf, world):
         assert np.array_equal(got[k].view(np.uint8).ravel(), whole[k]), k
 
 
-def _bench_line(tmp_path, gpus, path):
+def _bench_line(tmp_path, gpus, path, config="c1", parity=False):
     import json
     import subprocess
     env = dict(os.environ, TMPDIR=str(tmp_path))
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--config", "c1",
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--config", config,
                           "--rows", "300000", "--rg-rows", "50000", "--steps", "3", "--warmup", "1", "--file", path,
-                          "--no-prof", "--no-cpu", "--no-parity", "--dist-backend", "gloo"],
+                          "--no-prof", "--no-cpu", "--dist-backend", "gloo"] + ([] if parity else ["--no-parity"]),
                          env=env, capture_output=True, text=True, timeout=240, check=True)
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out.stdout + out.stderr
@@ -236,6 +236,23 @@ def test_bench_gpus_2_spawns_two_ranks(tmp_path):
     assert two["config"]["job_B_out"] == one["config"]["job_B_out"] == one["config"]["B_out"]
     assert 0 < two["config"]["B_out"] < one["config"]["B_out"]  # rank 0 decoded its shard only
     assert two["value"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("config", ["c2", "c4"])
+def test_bench_timed_batch_parity_every_rank(tmp_path, config):
+    """bench.py compares the timed batch's own buffers (whole shard, every
+    leaf) with the oracle on every rank and all-reduces the verdict."""
+    pytest.importorskip("pyarrow")
+    pytest.importorskip("torch")
+    path = str(tmp_path / ("%s_small.parquet" % config))
+    for gpus in (2, 1):
+        line = _bench_line(tmp_path, gpus, path, config, parity=True)
+        assert line["config"]["parity_ok"] is True, line["config"]["parity"]
+        assert "timed batch bit-exact" in line["config"]["parity"]
+        if gpus == 2:
+            assert line["config"]["parity"].startswith("all 2 ranks")
 
 
 def _gpu_rccl_main(rank, world, port, path, leaf, out_dir):
@@ -271,7 +288,10 @@ def test_gpu_allgather_rccl_device_tensors(tmp_path, name, leaf):
     import torch
     import torch.multiprocessing as mp
     import oracle
-    world = max(1, torch.cuda.device_count())
+    world = torch.cuda.device_count()
+    if world < 2:
+        pytest.skip("an RCCL all-gather needs >= 2 GPUs (a 1-rank 'collective' proves nothing); "
+                    "the gloo tests cover the re-packing")
     path = os.path.join(GOLDEN, name + ".parquet")
     mp.spawn(_gpu_rccl_main, args=(world, _free_port(), path, leaf, str(tmp_path)), nprocs=world, join=True)
     got = np.load(str(tmp_path / "gathered.npz"))
