@@ -12,8 +12,9 @@ uploaded to HBM once; the timed region is the whole GPU decode pipeline
 pipeline (analysis lines; tools/synth.py describes their files).
 
 A "step" decodes every page of the rank's shard once.  For N > 1 the file holds
-N x 100M rows and each rank decodes a contiguous, byte-balanced slice of its
-row groups (pqgpu.plan_row_group_shards) on its own GPU: weak scaling, no
+N x 100M rows and each rank decodes a contiguous slice of its row groups,
+balanced by estimated decode cost (pqgpu.plan_row_group_shards over
+FileReader.RowGroupCost) on its own GPU: weak scaling, no
 collective on the data path; value = decoded bytes of all ranks / max-over-ranks
 time.  `--gpus N` without WORLD_SIZE in the environment starts the N rank
 processes itself (spawn_ranks); under torch.distributed.run WORLD_SIZE must
@@ -586,7 +587,7 @@ def main():
     ctx = pqgpu.Context(device)
     reader = pqgpu.FileReader(path, ctx=ctx)
     reader.path = path
-    sizes = [reader.RowGroupByteSize(i) for i in range(reader.RowGroupCount())]
+    sizes = [reader.RowGroupCost(i) for i in range(reader.RowGroupCount())]  # balanced by decode cost
     rg0, rg1 = pqgpu.plan_row_group_shards(sizes, world)[rank]
     reader.batch(rg0, rg1).close()  # first use: HIP runtime and pinned ring set-up
     t_create = time.perf_counter()

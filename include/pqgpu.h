@@ -140,6 +140,12 @@ int64_t pqg_file_num_rows(const pqg_file *f);
 int pqg_file_row_group_count(const pqg_file *f);
 int64_t pqg_file_row_group_num_rows(const pqg_file *f, int rg);
 int64_t pqg_file_row_group_byte_size(const pqg_file *f, int rg); /* Σ chunk total_uncompressed_size */
+/* Estimated decode cost of a row group on one GPU (relative units, ~ns) from
+ * the footer and the dictionary page headers: uncompressed bytes, Snappy
+ * input, and dictionary gathers priced by the index bit width.  The weight the
+ * multi-GPU shard planner balances (no reference counterpart: the reader
+ * decodes row groups one after another, file_reader.go:101-116). */
+double pqg_file_row_group_cost(const pqg_file *f, int rg);
 int pqg_file_column_count(const pqg_file *f);
 int pqg_file_column_info(const pqg_file *f, int leaf, pqg_column_info *out);
 int pqg_file_find_column(const pqg_file *f, const char *flat_name); /* leaf index or -1 */
@@ -183,8 +189,13 @@ typedef struct {
 
 int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const int *leaves, int nleaves, int flags,
                      pqg_batch **out);
-/* Launch the whole decode pipeline on the context stream (asynchronous). */
+/* Launch the whole decode pipeline (asynchronous) on the batch's stream:
+ * the context stream, except for slices of a pqg_stream, which may decode on a
+ * second internal lane.  Order other device work after a decode with
+ * pqg_batch_sync, or on pqg_batch_stream(b) — not on pqg_ctx_stream. */
 int pqg_batch_decode(pqg_batch *b);
+/* HIP stream (hipStream_t as void*) the batch's decodes are launched on. */
+void *pqg_batch_stream(const pqg_batch *b);
 /* Wait for the last decode and reduce the per-page status words: returns the
  * reference's first error (row group, leaf, page order) or PQG_OK. */
 int pqg_batch_sync(pqg_batch *b);

@@ -1249,6 +1249,37 @@ int64_t pqg_file_row_group_byte_size(const pqg_file *f, int rg) {
   for (auto &c : f->rgs[(size_t)rg].cols) s += c.total_uncompressed;
   return s;
 }
+// Estimated GPU decode cost of row group rg for shard balancing (relative
+// units: ~ns on one MI355X), from the footer and the dictionary page headers
+// alone (no page walk).  Per chunk: its uncompressed bytes at ~2 TB/s
+// (output writes + staged reads), Snappy input at the measured k_snappy rate
+// (~0.5 GB/s a page-wave, ~400 GB/s over the chip), and for a dictionary
+// chunk its values at the gather rate of the dictionary's index bit width
+// (LDS groups ~780 Gvalues/s up to 2^12 entries, L1/L2 ~350 at
+// 2^13..2^15 and ~280 past, bit width 1 ~360).  A row group's chunks of one
+// bit width decode at about that rate whatever its neighbours are, so byte
+// sizes alone (dictionary pages count, keys do not) misjudge C2's row groups
+// by up to ~2x.
+double pqg_file_row_group_cost(const pqg_file *f, int rg) {
+  if (rg < 0 || rg >= (int)f->rgs.size()) return -1.0;
+  double ns = 0.0;
+  for (size_t li = 0; li < f->rgs[(size_t)rg].cols.size(); li++) {
+    const ColumnChunkMeta &c = f->rgs[(size_t)rg].cols[li];
+    ns += (double)std::max<int64_t>(c.total_uncompressed, 0) / 2000.0;  // bytes / (2 TB/s) in ns
+    if (c.codec == PQG_CODEC_SNAPPY) ns += (double)std::max<int64_t>(c.total_compressed, 0) / 400.0;
+    if (!c.has_dict_off || c.dict_page_offset <= 0 || c.dict_page_offset >= c.data_page_offset) continue;
+    if ((uint64_t)c.dict_page_offset >= f->len) continue;
+    TReader t(f->data + c.dict_page_offset, f->len - (size_t)c.dict_page_offset);
+    PageHeader h;
+    read_page_header(t, h);
+    if (t.err || h.type != 2 || !h.has_dict || h.dict_num_values <= 0) continue;
+    int bw = 0;
+    while (bw < 32 && ((int64_t)1 << bw) < (int64_t)h.dict_num_values) bw++;
+    const double gvals = bw <= 1 ? 360.0 : bw <= 12 ? 780.0 : bw <= 15 ? 350.0 : 280.0;
+    ns += (double)std::max<int64_t>(c.num_values, 0) / gvals;
+  }
+  return ns;
+}
 int pqg_file_column_count(const pqg_file *f) { return (int)f->leaves.size(); }
 int pqg_file_column_info(const pqg_file *f, int leaf, pqg_column_info *out) {
   if (leaf < 0 || leaf >= (int)f->leaves.size()) return PQG_ERR_ARG;
@@ -3074,6 +3105,9 @@ static LaneRef lane_of(pqg_batch *B) {
   return {c->stream, c->side, c->fork, c->join, &c->launch_mu};
 }
 static hipStream_t bstream(pqg_batch *B) { return B->lane == 1 ? B->ctx->lane1.stream : B->ctx->stream; }
+void *pqg_batch_stream(const pqg_batch *b) {
+  return b ? (void *)bstream(const_cast<pqg_batch *>(b)) : nullptr;
+}
 
 int pqg_batch_decode(pqg_batch *B) {
   if (!B) return PQG_ERR_ARG;

@@ -52,6 +52,7 @@ EXPORTS = [
     "pqg_register_block_compressor", "pqg_get_registered_codecs", "pqg_decompress_block",
     "pqg_file_open_path", "pqg_file_open_buffer", "pqg_file_close", "pqg_file_num_rows",
     "pqg_file_row_group_count", "pqg_file_row_group_num_rows", "pqg_file_row_group_byte_size",
+    "pqg_file_row_group_cost", "pqg_batch_stream",
     "pqg_file_column_count", "pqg_file_column_info", "pqg_file_find_column", "pqg_file_select_columns",
     "pqg_file_last_error", "pqg_batch_create", "pqg_batch_decode", "pqg_batch_sync",
     "pqg_batch_error_location", "pqg_batch_column", "pqg_batch_copy", "pqg_batch_stats_get",
@@ -119,6 +120,8 @@ def lib():
                 "pqg_file_close": (None, [vp]), "pqg_file_num_rows": (i64, [vp]),
                 "pqg_file_row_group_count": (i32, [vp]), "pqg_file_row_group_num_rows": (i64, [vp, i32]),
                 "pqg_file_row_group_byte_size": (i64, [vp, i32]),
+                "pqg_file_row_group_cost": (ctypes.c_double, [vp, i32]),
+                "pqg_batch_stream": (vp, [vp]),
                 "pqg_file_column_count": (i32, [vp]), "pqg_file_column_info": (i32, [vp, i32, P(ColumnInfo)]),
                 "pqg_file_find_column": (i32, [vp, ctypes.c_char_p]),
                 "pqg_file_select_columns": (i32, [vp, P(ctypes.c_char_p), i32, P(ctypes.c_int), i32]),
@@ -430,6 +433,11 @@ class FileReader:
         """Σ total_uncompressed_size of the row group's chunks (the shard balancing weight)."""
         return lib().pqg_file_row_group_byte_size(self._h, rg)
 
+    def RowGroupCost(self, rg):
+        """Estimated GPU decode cost of row group rg (pqg_file_row_group_cost):
+        the weight plan_row_group_shards balances for multi-GPU shards."""
+        return lib().pqg_file_row_group_cost(self._h, rg)
+
     def CurrentRowGroup(self):
         return self.row_group_position
 
@@ -517,7 +525,8 @@ def OpenFiles(paths, *columns, threads=0, **kw):
 
 def plan_row_group_shards(sizes, world):
     """Contiguous row-group ranges [(rg0, rg1)] for `world` ranks, balanced by
-    the byte sizes `sizes` (one per row group).  Row groups are independent
+    the weights `sizes` (one per row group: FileReader.RowGroupCost, the
+    estimated decode cost, or byte sizes).  Row groups are independent
     (one dictionary per chunk, chunk_reader.go:221), so a shard needs nothing
     from its neighbours and the decode path has no collective."""
     n = len(sizes)

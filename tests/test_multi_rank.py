@@ -43,6 +43,37 @@ def test_plan_row_group_shards_tiles_and_balances():
     assert [b - a for a, b in sh] == [12] * 8
 
 
+def test_cost_balanced_shards_c2_shape(tmp_path):
+    """plan_row_group_shards over FileReader.RowGroupCost: C2's row groups
+    (dictionary bit width 1 + i % 20) cost by their bit width, not by their
+    bytes (a bit-width-20 row group carries a 4 MiB dictionary page but its
+    gathers, not its bytes, are the cost).  The cost estimate grows with the
+    bit width past the LDS-resident sizes, and the cost-balanced plan's
+    heaviest shard is no heavier (in cost) than the byte-balanced plan's."""
+    pytest.importorskip("pyarrow")
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import synth
+    import pqgpu
+    path = str(tmp_path / "c2_cost.parquet")
+    synth.make("c2", path, 40 * 20000, 20000)  # 40 row groups: bit widths 1..20 twice
+    r = pqgpu.FileReader(path)
+    n = r.RowGroupCount()
+    assert n == 40
+    cost = [r.RowGroupCost(i) for i in range(n)]
+    size = [r.RowGroupByteSize(i) for i in range(n)]
+    assert all(c > 0 for c in cost)
+    assert r.RowGroupCost(n) < 0 and r.RowGroupCost(-1) < 0
+    # bit width b + 1 at row group b: big dictionaries cost more per row
+    assert cost[19] > cost[11] * 1.5 and cost[15] > cost[5] * 1.5
+    assert abs(cost[3] - cost[23]) < 0.05 * cost[3]  # same width, same cost
+    for world in (2, 3, 4, 8):
+        by_cost = pqgpu.plan_row_group_shards(cost, world)
+        by_size = pqgpu.plan_row_group_shards(size, world)
+        worst = lambda plan: max(sum(cost[a:b]) for a, b in plan)
+        assert worst(by_cost) <= worst(by_size) * 1.0001, (world, by_cost, by_size)
+        assert by_cost[0][0] == 0 and by_cost[-1][1] == n
+
+
 def _rank_main(rank, world, port, path, out_dir):
     import torch
     import torch.distributed as dist
@@ -52,7 +83,7 @@ def _rank_main(rank, world, port, path, out_dir):
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
     data = open(path, "rb").read()
     r = pqgpu.FileReader(data)  # host-side metadata only: no GPU needed
-    sizes = [r.RowGroupByteSize(i) for i in range(r.RowGroupCount())]
+    sizes = [r.RowGroupCost(i) for i in range(r.RowGroupCount())]
     rg0, rg1 = pqgpu.plan_row_group_shards(sizes, world)[rank]
     import time
     t0 = time.perf_counter()
