@@ -1428,6 +1428,490 @@ __device__ __forceinline__ void copy_items(const KArgs &a, uint32_t blk, uint32_
 __global__ __launch_bounds__(256) void k_copy(KArgs a) { copy_items(a, blockIdx.x, gridDim.x); }
 
 // ===========================================================================
+// K1w: k_snappy_wg — Snappy (decode_other.go:14-101) by one 256-thread
+// workgroup per work item (a whole page, or a 64 KiB segment of a long one),
+// with the whole Snappy block window (64 KiB: the encoders' block size, so the
+// reach of every copy they write) as history in LDS.  A copy never reads HBM:
+// the decode reads the compressed bytes once and writes the uncompressed ones
+// once.  72 KiB of LDS, two workgroups per CU.  Per batch (at most UZ_POS
+// compressed bytes, UZ_TOK tokens, UZ_OUT output bytes):
+//  1. the batch's compressed bytes in LDS (loaded into registers while the
+//     previous batch resolved);
+//  2. the token chain by pointer jumping: J_0(p) = p + size of the token at
+//     window position p, J_b+1 = J_b o J_b; thread t applies J_b for the set
+//     bits b of t (and of t + 256), so after 9 rounds it holds the positions
+//     of tokens t and t + 256;
+//  3. each thread decodes and checks its two tokens (the reference's checks:
+//     header inside src, length <= remaining dst, 0 < offset <= d); workgroup
+//     scans give their output offsets and cut the batch;
+//  4. token table + output-start bitmap with per-word token counts (token m
+//     writes count m + 1 into the words starting inside it);
+//  5. every output byte resolved by a thread, 4 bytes a thread per pass of
+//     UZ_PASS bytes: a literal byte from the window, a copy byte from the
+//     history (byte r of a copy of offset o is byte d - o + r mod o), chased
+//     to its source when that is a byte of the same pass;
+//  6. whole 16-byte chunks from the history to HBM.
+// Long literals (tag >= 60 << 2) are copied by the workgroup straight to HBM,
+// their last 64 KiB into the history.  A source older than the history (an
+// offset past 64 KiB - UZ_OUT, which block-structured encoders never write)
+// is read back from the staged output.
+// ===========================================================================
+constexpr int UZ_T = 256;                         // threads
+constexpr int UZ_HIST = 65536;                    // history (ring) bytes
+constexpr uint32_t UZ_HMASK = UZ_HIST - 1;
+constexpr int UZ_POS = 1024;                      // window positions parsed per batch
+constexpr int UZ_STOP = UZ_POS;                   // the chain's end in the jump tables
+constexpr int UZ_WIN_DW = (UZ_POS + 64 + 8) / 4;  // staged dwords: skew, positions, a short literal's payload
+constexpr int UZ_TOK = 2 * UZ_T;                  // tokens per batch (two per thread)
+constexpr int UZ_OUT = 4096;                      // output bytes per batch
+constexpr int UZ_ROUNDS = 9;                      // 2^9 = UZ_TOK
+static_assert((1 << UZ_ROUNDS) == UZ_TOK && UZ_WIN_DW > UZ_T && UZ_WIN_DW <= 2 * UZ_T, "k_snappy_wg shapes");
+
+struct UzLds {
+  uint8_t hist[UZ_HIST];
+  uint32_t win[UZ_WIN_DW + 2];
+  union {
+    uint16_t jt[2][UZ_POS + 4];  // J_b ping-pong; entry UZ_STOP = UZ_STOP
+    uint2 tok[UZ_TOK];           // {out_rel | len << 16 | literal << 31, literal: window position / copy: offset}
+  };
+  uint2 bmc[UZ_OUT / 32];        // output-start bits, tokens starting before the word
+  int32_t red[16];               // per wave: output bytes of tokens A, B; valid tokens A, B
+  int32_t last[8][4];            // per wave and token half: {last accepted token + 1, its end, stream bytes}
+  uint32_t flags;                // 1: a bad token, 2: a source older than the history
+  uint32_t go;
+};
+
+// Output byte j of the batch; `base`: the first byte of the current pass
+// (earlier bytes of the batch are already in the history).
+__device__ __forceinline__ uint32_t uz_byte(const UzLds &U, const uint8_t *wb, int j, int base, int64_t dpos,
+                                            int64_t near_lo, const uint8_t *dst) {
+  int q = j;
+  for (;;) {
+    const uint2 e = U.bmc[q >> 5];
+    const int k = (int)e.y + __builtin_popcount(e.x & (0xffffffffu >> (31 - (q & 31)))) - 1;
+    const uint2 t = U.tok[k];
+    const int out_rel = (int)(t.x & 0xffffu), len = (int)((t.x >> 16) & 0x7fu);
+    const uint32_t r = (uint32_t)(q - out_rel);
+    if (t.x >> 31) return wb[t.y + r];
+    const uint32_t off = t.y;
+    const int64_t q2 = (int64_t)out_rel - (int64_t)off + (int64_t)(off >= (uint32_t)len ? r : r % off);
+    if (q2 >= 0) {
+      if (q2 < base) return U.hist[(uint32_t)(dpos + q2) & UZ_HMASK];
+      q = (int)q2;  // a byte of this pass: resolve its own source
+      continue;
+    }
+    const int64_t p = dpos + q2;
+    if (p >= near_lo) return U.hist[(uint32_t)p & UZ_HMASK];
+    const uintptr_t from = (uintptr_t)(dst + p);  // older than the history: the staged output
+    const uint32_t w = __hip_atomic_load((const uint32_t *)(from & ~(uintptr_t)3), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    return (w >> ((from & 3) * 8)) & 0xffu;
+  }
+}
+
+// Decode the short token at window position pos (its tag is not a long
+// literal): output length, literal payload position or copy offset, header
+// bytes, and whether its header / payload lies past the block end.
+__device__ __forceinline__ void uz_token(const UzLds &U, int sh, int pos, int64_t sabs, int64_t slen, uint32_t &len,
+                                         uint32_t &x, bool &lit, bool &bad, int &adv) {
+  const int b = sh + pos;
+  const uint32_t w0 = U.win[b >> 2], w1 = U.win[(b >> 2) + 1], w2 = U.win[(b >> 2) + 2];
+  const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)b & 3);
+  const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, (uint32_t)b & 3);
+  const uint32_t tag = lo & 0xff;
+  if ((tag & 3) == 0) {
+    lit = true;
+    len = (tag >> 2) + 1;
+    x = (uint32_t)pos + 1;
+    adv = 1 + (int)len;
+    bad = sabs + 1 + (int64_t)len > slen;
+    return;
+  }
+  lit = false;
+  if ((tag & 3) == 1) {
+    adv = 2;
+    len = 4 + ((tag >> 2) & 7);
+    x = ((tag & 0xe0) << 3) | ((lo >> 8) & 0xff);
+  } else if ((tag & 3) == 2) {
+    adv = 3;
+    len = 1 + (tag >> 2);
+    x = (lo >> 8) & 0xffff;
+  } else {
+    adv = 5;
+    len = 1 + (tag >> 2);
+    x = (lo >> 8) | (hi << 24);
+  }
+  bad = sabs + adv > slen;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(UZ_T) void k_snappy_wg(KArgs a) {
+  __shared__ __attribute__((aligned(16))) UzLds U;
+  const int tid = threadIdx.x;
+  const int lane = lane_id();
+  const int wv = (int)ufirst((uint32_t)tid >> 6);
+  const int wi = blockIdx.x;
+  if (MODE == SNAP_ITEMS && wi == 0 && tid == 0) a.copy_cnt[(a.epoch + 1) & 1] = 0;  // the next decode's list
+  int gi, seg_k = 0;
+  bool seg = false;
+  if (MODE == SNAP_FALLBACK) {
+    if (wi >= a.nwalk) return;
+    gi = a.walk[wi];
+  } else {
+    if (wi >= a.nitems) return;
+    const int2 it = a.sitems[wi];
+    gi = it.x;
+    seg_k = it.y;
+    seg = a.seg_base[gi + 1] - a.seg_base[gi] > 1;
+  }
+  const int page = a.list[gi];
+  // words that other launches write are read by one thread (block-uniform decision)
+  if (tid == 0) {
+    bool go = page_status(a.status, page) >= make_status(ST_DECOMPRESS, 0);
+    if (MODE == SNAP_FALLBACK)
+      go = go && __hip_atomic_load(&a.seg_flag[gi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u;
+    else if (seg)
+      go = go && __hip_atomic_load(&a.seg_flag[gi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+    U.go = go ? 1u : 0u;
+    if (!seg && a.max_jobs > 0) a.njobs[gi] = 0u;  // nothing deferred to k_copy
+  }
+  __syncthreads();
+  if (!U.go) return;
+  const PageDesc d = a.pages[page];
+  const int64_t lsize = d.kind == PAGE_V2 ? (int64_t)d.v2_rep_len + d.v2_def_len : 0;
+  const uint8_t *src = a.in + d.src + lsize;
+  const int64_t slen = d.comp_len;
+  uint8_t *dst = a.stage + d.body;
+  const int64_t expect = d.body_len;
+  PQ_CHK(a.in_end && (src < a.in || src + slen > a.in_end), 13, (uintptr_t)src, slen, return);
+  PQ_CHK(a.stage_end && (dst < a.stage || dst + expect > a.stage_end), 14, (uintptr_t)dst, expect, return);
+
+  int64_t s = 0, seg_lo = 0, dl;
+  bool write;
+  if (seg) {
+    // k_snappy_walk checked the preamble and found the segment's first token
+    s = (int64_t)__hip_atomic_load(&a.segs[a.seg_base[gi] + seg_k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s = (int64_t)ufirst64((uint64_t)s);
+    seg_lo = (int64_t)seg_k * SNAP_SEG;
+    dl = min(seg_lo + SNAP_SEG, expect);
+    write = true;
+  } else {
+    // decodedLen: binary.Uvarint (n <= 0 or > 0xffffffff -> ErrCorrupt)
+    uint64_t dlen = 0;
+    bool ok = false;
+    for (int i = 0, sh = 0; s < slen; i++, sh += 7) {
+      const uint32_t b = src[s];
+      s++;
+      if (b < 0x80) {
+        ok = !(i > 9 || (i == 9 && b > 1));
+        dlen |= (uint64_t)b << (sh & 63);
+        break;
+      }
+      if (sh < 64) dlen |= (uint64_t)(b & 0x7f) << sh;
+    }
+    if (!ok || dlen > 0xffffffffull) {
+      if (tid == 0) atomicMin(&a.status[page], make_status(ST_DECOMPRESS, E_SNAPPY));
+      return;
+    }
+    write = dlen == (uint64_t)expect;
+    dl = (int64_t)dlen;
+    if (write && tid == 0) a.info[page].alias1 = 0;
+    // a block that is exactly one literal is its own content: left in place (a
+    // dictionary page only when 8-byte aligned, as k_snappy; never a page whose
+    // k_expand records the host wrote)
+    if (write && dl > 0 && s < slen) {
+      const uint32_t tag = src[s];
+      if ((tag & 3) == 0) {
+        uint32_t x = tag >> 2;
+        int64_t hs = 1;
+        bool ok1 = true;
+        if (x >= 60) {
+          const int extra = (int)x - 59;
+          hs = 1 + extra;
+          if (s + hs > slen) ok1 = false;
+          else {
+            x = 0;
+            for (int k = 0; k < extra; k++) x |= (uint32_t)src[s + 1 + k] << (8 * k);
+          }
+        }
+        if (ok1 && (int64_t)x + 1 == dl && s + hs + dl == slen && !d.srec &&
+            (d.kind != PAGE_DICT || d.alias_any || ((d.src + lsize + s + hs) & 7) == 0)) {
+          if (tid == 0) a.info[page].alias1 = 1 + (int64_t)(d.src + lsize + s + hs);
+          return;
+        }
+      }
+    }
+  }
+
+  int64_t dpos = seg_lo;
+  int64_t F = seg_lo;  // output below F is in HBM; [F, dpos) only in the history
+  uint32_t err = E_OK;
+  int64_t pf_s = -1;   // stream position of the window prefetched into pw0 / pw1
+  uint32_t pw0 = 0, pw1 = 0;
+  while (s < slen && (!seg || dpos < dl)) {
+    // ---- 1. the window: stream bytes [s, s + UZ_POS + 64) at win byte sh
+    const uintptr_t abase = (uintptr_t)(src + s) & ~(uintptr_t)3;
+    const int sh = (int)((uintptr_t)(src + s) & 3);
+    PQ_CHK(a.in_end && abase + 4 * UZ_WIN_DW > (uintptr_t)a.in_end, 10, abase, a.in_end, err = E_SNAPPY; break);
+    if (pf_s != s) {
+      pw0 = gld32(abase + 4 * (uintptr_t)tid);
+      pw1 = tid < UZ_WIN_DW - UZ_T ? gld32(abase + 4 * (uintptr_t)(UZ_T + tid)) : 0u;
+    }
+    U.win[tid] = pw0;
+    if (tid < UZ_WIN_DW - UZ_T) U.win[UZ_T + tid] = pw1;
+    if (tid < UZ_OUT / 32) U.bmc[tid] = make_uint2(0u, 0u);
+    if (tid == 0) U.flags = 0u;
+    __syncthreads();
+    const uint8_t *wb = (const uint8_t *)U.win + sh;  // wb[p]: stream byte s + p
+    const int64_t lim64 = slen - s - 1;               // the last position inside the block
+    const int lim = lim64 < UZ_POS - 1 ? (int)lim64 : UZ_POS - 1;
+    const uint32_t tag0 = wb[0];
+    if ((tag0 & 3) == 0 && (tag0 >> 2) >= 60) {
+      // ---- a long literal: the workgroup copies it
+      const int extra = (int)(tag0 >> 2) - 59;
+      if (s + 1 + extra > slen) {
+        err = E_SNAPPY;
+        break;
+      }
+      uint64_t x = 0;
+      for (int k = 0; k < extra; k++) x |= (uint64_t)wb[1 + k] << (8 * k);
+      const int64_t len = (int64_t)x + 1;
+      const int64_t hs = 1 + extra;
+      if (len > dl - dpos || len > slen - s - hs) {
+        err = E_SNAPPY;
+        break;
+      }
+      if (write) {
+        // the history's pending bytes, then the literal to HBM; its last
+        // UZ_HIST bytes also into the history
+        if (tid < dpos - F) dst[F + tid] = U.hist[(uint32_t)(F + tid) & UZ_HMASK];
+        const uint8_t *ls = src + s + hs;
+        uint8_t *D = dst + dpos;
+        const int64_t hist_from = len - UZ_HIST;  // literal offsets >= this enter the history
+        int64_t head = (int64_t)((16 - ((uintptr_t)D & 15)) & 15);
+        if (head > len) head = len;
+        if (tid < head) {
+          const uint8_t b = ls[tid];
+          D[tid] = b;
+          if (tid >= hist_from) U.hist[(uint32_t)(dpos + tid) & UZ_HMASK] = b;
+        }
+        const int64_t nch = (len - head) >> 4;
+        const uint8_t *S = ls + head;
+        const uint32_t skew = (uint32_t)((uintptr_t)S & 3);
+        const uintptr_t SA = (uintptr_t)S & ~(uintptr_t)3;
+        for (int64_t c = tid; c < nch; c += UZ_T) {
+          const uintptr_t sp = SA + 16 * (uintptr_t)c;
+          const uint32_t x0 = gld32(sp), x1 = gld32(sp + 4), x2 = gld32(sp + 8), x3 = gld32(sp + 12), x4 = gld32(sp + 16);
+          uint4 o;
+          o.x = __builtin_amdgcn_alignbyte(x1, x0, skew);
+          o.y = __builtin_amdgcn_alignbyte(x2, x1, skew);
+          o.z = __builtin_amdgcn_alignbyte(x3, x2, skew);
+          o.w = __builtin_amdgcn_alignbyte(x4, x3, skew);
+          gst128((uintptr_t)(D + head + 16 * c), o);
+          if (head + 16 * c >= hist_from) *(uint4 *)(U.hist + ((uint32_t)(dpos + head + 16 * c) & UZ_HMASK)) = o;
+        }
+        const int64_t done = head + nch * 16;
+        if (tid < len - done) {
+          const uint8_t b = ls[done + tid];
+          D[done + tid] = b;
+          if (done + tid >= hist_from) U.hist[(uint32_t)(dpos + done + tid) & UZ_HMASK] = b;
+        }
+        F = dpos + len;
+      }
+      dpos += len;
+      s += hs + len;
+      __syncthreads();  // the history's new bytes; the window's last readers
+      continue;
+    }
+    // ---- 2. J_0 for positions 4 tid .. 4 tid + 3, then the chain by pointer jumping
+    uint16_t *ja = U.jt[0], *jb = U.jt[1];
+    {
+      uint32_t j4[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int p = 4 * tid + k;
+        const uint32_t cls = snappy_tok_class(wb[p]);
+        const int nx = p + (int)(cls & 0xff);
+        j4[k] = (cls == 0 || p > lim || nx > UZ_POS) ? (uint32_t)UZ_STOP : (uint32_t)nx;
+      }
+      *(uint2 *)(ja + 4 * tid) = make_uint2(j4[0] | (j4[1] << 16), j4[2] | (j4[3] << 16));
+      if (tid == 0) {
+        ja[UZ_STOP] = UZ_STOP;
+        jb[UZ_STOP] = UZ_STOP;
+      }
+    }
+    __syncthreads();
+    int pa = 0, pb = 0;  // the positions of tokens tid (A) and UZ_T + tid (B)
+#pragma unroll
+    for (int b = 0; b < UZ_ROUNDS; b++) {
+      const int ha = ja[pa], hb = ja[pb];
+      if (b < UZ_ROUNDS - 1) {
+        const uint2 q = *(const uint2 *)(ja + 4 * tid);
+        const uint32_t n0 = ja[q.x & 0xffff], n1 = ja[q.x >> 16], n2 = ja[q.y & 0xffff], n3 = ja[q.y >> 16];
+        *(uint2 *)(jb + 4 * tid) = make_uint2(n0 | (n1 << 16), n2 | (n3 << 16));
+      }
+      if ((tid >> b) & 1) pa = ha;
+      if (((tid + UZ_T) >> b) & 1) pb = hb;
+      if (b < UZ_ROUNDS - 1) {
+        __syncthreads();
+        uint16_t *t = ja;
+        ja = jb;
+        jb = t;
+      }
+    }
+    // ---- 3. decode + check tokens A and B; output offsets by workgroup scans
+    const bool vA = pa <= lim && snappy_tok_class(wb[pa]) != 0;
+    const bool vB = pb <= lim && snappy_tok_class(wb[pb]) != 0;
+    uint32_t lenA = 0, xA = 0, lenB = 0, xB = 0;
+    bool litA = false, litB = false, badA = false, badB = false;
+    int advA = 0, advB = 0;
+    if (vA) uz_token(U, sh, pa, s + pa, slen, lenA, xA, litA, badA, advA);
+    if (vB) uz_token(U, sh, pb, s + pb, slen, lenB, xB, litB, badB, advB);
+    const int32_t iA = wave_incl_scan32((int32_t)lenA), iB = wave_incl_scan32((int32_t)lenB);
+    if (lane == 63) {
+      U.red[wv] = iA;
+      U.red[4 + wv] = iB;
+    }
+    __syncthreads();  // (also: every jump-table read is done; the table below reuses the space)
+    int32_t preA = 0, totA = 0, preB = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      const int32_t ra = U.red[w], rb = U.red[4 + w];
+      totA += ra;
+      preA += w < wv ? ra : 0;
+      preB += w < wv ? rb : 0;
+    }
+    const int32_t endA = preA + iA, endB = totA + preB + iB;  // output offsets after each token
+    const int64_t room = dl - dpos;
+    // a prefix of the tokens: those that fit the batch and start before the end
+    // of the output (of the segment: a later token belongs to the next one)
+    const bool accA = vA && endA <= UZ_OUT && (int64_t)endA - (int64_t)lenA < room;
+    const bool accB = vB && endB <= UZ_OUT && (int64_t)endB - (int64_t)lenB < room;
+    const int32_t oA = endA - (int32_t)lenA, oB = endB - (int32_t)lenB;
+    const int64_t near_lo = dpos + UZ_OUT - UZ_HIST;  // sources below: the slow path
+    uint32_t fl = 0;
+    if (accA) {
+      const int64_t dd = dpos + oA;
+      badA |= (int64_t)lenA > dl - dd;
+      if (!litA) {
+        badA |= xA == 0 || (int64_t)xA > dd - seg_lo;
+        fl |= dd - (int64_t)xA < near_lo ? 2u : 0u;
+      }
+      fl |= badA ? 1u : 0u;
+    }
+    if (accB) {
+      const int64_t dd = dpos + oB;
+      badB |= (int64_t)lenB > dl - dd;
+      if (!litB) {
+        badB |= xB == 0 || (int64_t)xB > dd - seg_lo;
+        fl |= dd - (int64_t)xB < near_lo ? 2u : 0u;
+      }
+      fl |= badB ? 1u : 0u;
+    }
+    // ---- 4. token table, start bits, per-word counts; the batch's extent
+    if (accA) {
+      U.tok[tid] = make_uint2((uint32_t)oA | (lenA << 16) | (litA ? 0x80000000u : 0u), xA);
+      __hip_atomic_fetch_or(&U.bmc[oA >> 5].x, 1u << (oA & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      for (int32_t w = (oA >> 5) + 1; w <= (endA >> 5) && w < UZ_OUT / 32; w++) U.bmc[w].y = (uint32_t)(tid + 1);
+    }
+    if (accB) {
+      U.tok[UZ_T + tid] = make_uint2((uint32_t)oB | (lenB << 16) | (litB ? 0x80000000u : 0u), xB);
+      __hip_atomic_fetch_or(&U.bmc[oB >> 5].x, 1u << (oB & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      for (int32_t w = (oB >> 5) + 1; w <= (endB >> 5) && w < UZ_OUT / 32; w++) U.bmc[w].y = (uint32_t)(UZ_T + tid + 1);
+    }
+    {
+      const uint64_t mA = ballot(accA), mB = ballot(accB);
+      const uint32_t fw = (ballot(fl & 1u) ? 1u : 0u) | (ballot(fl & 2u) ? 2u : 0u);
+      const int LA = mA ? 63 - __builtin_clzll(mA) : -1, LB = mB ? 63 - __builtin_clzll(mB) : -1;
+      if (lane == (LA < 0 ? 0 : LA)) {
+        U.last[wv][0] = LA < 0 ? 0 : tid + 1;
+        U.last[wv][1] = endA;
+        U.last[wv][2] = pa + advA;
+      }
+      if (lane == (LB < 0 ? 0 : LB)) {
+        U.last[4 + wv][0] = LB < 0 ? 0 : UZ_T + tid + 1;
+        U.last[4 + wv][1] = endB;
+        U.last[4 + wv][2] = pb + advB;
+      }
+      if (lane == 0 && fw) __hip_atomic_fetch_or(&U.flags, fw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __syncthreads();
+    int ntok = 0, T = 0, cur = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int m = U.last[q][0];
+      if (m > ntok) {
+        ntok = m;
+        T = U.last[q][1];
+        cur = U.last[q][2];
+      }
+    }
+    const uint32_t flags = U.flags;
+    if (ntok == 0 || (flags & 1u)) {  // output complete with tokens left, or a corrupt token
+      err = E_SNAPPY;
+      break;
+    }
+    // prefetch the next window (its loads overlap this batch's byte passes)
+    const int64_t sn = s + cur;
+    if (sn < slen) {
+      const uintptr_t an = (uintptr_t)(src + sn) & ~(uintptr_t)3;
+      pw0 = gld32(an + 4 * (uintptr_t)tid);
+      pw1 = tid < UZ_WIN_DW - UZ_T ? gld32(an + 4 * (uintptr_t)(UZ_T + tid)) : 0u;
+      pf_s = sn;
+    }
+    if (write) {
+      if (flags & 2u) {  // a source older than the history: the earlier flushes must be visible
+        __threadfence();
+        __syncthreads();
+      }
+      // ---- 5. every output byte: passes of 4 bytes a thread
+      for (int base = 0; base < T; base += 4 * UZ_T) {
+        uint32_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int j = base + k * UZ_T + tid;
+          v[k] = j < T ? uz_byte(U, wb, j, base, dpos, near_lo, dst) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int j = base + k * UZ_T + tid;
+          if (j < T) U.hist[(uint32_t)(dpos + j) & UZ_HMASK] = (uint8_t)v[k];
+        }
+        __syncthreads();
+      }
+      // ---- 6. to HBM: bytes up to the next 16-byte boundary (F is unaligned
+      // after a long literal), then whole 16-byte chunks up to floor16(dpos + T)
+      const int64_t end = dpos + T;
+      int64_t a16 = (F + 15) & ~(int64_t)15;
+      if (a16 > end) a16 = end;
+      if (tid < a16 - F) dst[F + tid] = U.hist[(uint32_t)(F + tid) & UZ_HMASK];
+      F = a16;
+      const int64_t e16 = end & ~(int64_t)15;
+      if ((F & 15) == 0)
+        for (int64_t c = F + 16 * (int64_t)tid; c < e16; c += 16 * UZ_T)
+          gst128((uintptr_t)(dst + c), *(const uint4 *)(U.hist + ((uint32_t)c & UZ_HMASK)));
+      if (e16 > F) F = e16;
+    } else {
+      __syncthreads();  // the window's readers (the next batch overwrites it)
+    }
+    dpos += T;
+    s += cur;
+  }
+  if (err == E_OK && dpos != dl) err = E_SNAPPY;
+  if (err == E_OK && write)
+    for (int64_t p = F + tid; p < dl; p += UZ_T) dst[p] = U.hist[(uint32_t)p & UZ_HMASK];
+  if (err == E_OK && !write) err = E_SIZE;  // compress.go:117-119
+  if (seg) {
+    // the last segment must end the stream exactly; a segment that does not
+    // decode on its own sends the page to the serial decode
+    if (err == E_OK && seg_k == a.seg_base[gi + 1] - a.seg_base[gi] - 1 && s != slen) err = E_SNAPPY;
+    if (err && tid == 0) atomicMax(&a.seg_flag[gi], 1u);
+    err = E_OK;
+  }
+  if (err && tid == 0) atomicMin(&a.status[page], make_status(ST_DECOMPRESS, err));
+}
+
+// ===========================================================================
 // K0: start of a decode — every page's status back to its host-planned value
 // (blockIdx.y == 0) and the validity bitmaps zeroed (blockIdx.y == 1 + range),
 // one launch instead of a status upload and a memset per bitmap
@@ -4994,15 +5478,20 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     hipLaunchKernelGGL(pq::k_sw_link, dim3((k.n_sw_pages + 3) / 4), dim3(256), 0, s, k);
     return launch_status(which);
   }
-  if (which == 0) {  // k_snappy over work items (pages, or segments of long pages)
+  // PQG_SNAPPY_V1=1 (analysis): the wave-per-page decoder k_snappy instead of
+  // the workgroup-per-page k_snappy_wg
+  static const bool snappy_v1 = getenv("PQG_SNAPPY_V1") && getenv("PQG_SNAPPY_V1")[0] == '1';
+  if (which == 0) {  // Snappy over work items (pages, or segments of long pages)
     if (k.nitems <= 0) return 0;
-    hipLaunchKernelGGL(pq::k_snappy<pq::SNAP_ITEMS>, dim3((k.nitems + 3) / 4), dim3(256), 0, s, k);
+    if (snappy_v1) hipLaunchKernelGGL(pq::k_snappy<pq::SNAP_ITEMS>, dim3((k.nitems + 3) / 4), dim3(256), 0, s, k);
+    else hipLaunchKernelGGL(pq::k_snappy_wg<pq::SNAP_ITEMS>, dim3(k.nitems), dim3(pq::UZ_T), 0, s, k);
     return launch_status(which);
   }
   if (which == 17 || which == 18) {  // k_snappy_walk / serial fallback over the segmented pages
     if (k.nwalk <= 0) return 0;
     if (which == 17) hipLaunchKernelGGL(pq::k_snappy_walk, dim3(k.nwalk), dim3(64), 0, s, k);
-    else hipLaunchKernelGGL(pq::k_snappy<pq::SNAP_FALLBACK>, dim3((k.nwalk + 3) / 4), dim3(256), 0, s, k);
+    else if (snappy_v1) hipLaunchKernelGGL(pq::k_snappy<pq::SNAP_FALLBACK>, dim3((k.nwalk + 3) / 4), dim3(256), 0, s, k);
+    else hipLaunchKernelGGL(pq::k_snappy_wg<pq::SNAP_FALLBACK>, dim3(k.nwalk), dim3(pq::UZ_T), 0, s, k);
     return launch_status(which);
   }
   if (k.nlist <= 0) return 0;
