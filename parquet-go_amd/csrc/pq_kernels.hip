@@ -1428,90 +1428,139 @@ __device__ __forceinline__ void copy_items(const KArgs &a, uint32_t blk, uint32_
 __global__ __launch_bounds__(256) void k_copy(KArgs a) { copy_items(a, blockIdx.x, gridDim.x); }
 
 // ===========================================================================
-// K1w: k_snappy_wg — Snappy (decode_other.go:14-101) by one 256-thread
+// K1w: k_snappy_wg — Snappy (decode_other.go:14-101) by one 512-thread
 // workgroup per work item (a whole page, or a 64 KiB segment of a long one),
 // with the whole Snappy block window (64 KiB: the encoders' block size, so the
 // reach of every copy they write) as history in LDS.  A copy never reads HBM:
-// the decode reads the compressed bytes once and writes the uncompressed ones
-// once.  72 KiB of LDS, two workgroups per CU.  Per batch (at most UZ_POS
+// the decode reads the compressed bytes and writes the uncompressed ones
+// once.  ~77 KiB of LDS, two workgroups per CU.  Per batch (at most UZ_POS
 // compressed bytes, UZ_TOK tokens, UZ_OUT output bytes):
 //  1. the batch's compressed bytes in LDS (loaded into registers while the
 //     previous batch resolved);
 //  2. the token chain by pointer jumping: J_0(p) = p + size of the token at
 //     window position p, J_b+1 = J_b o J_b; thread t applies J_b for the set
-//     bits b of t (and of t + 256), so after 9 rounds it holds the positions
-//     of tokens t and t + 256;
+//     bits b of t (and of t + UZ_T), so it lands on tokens t and t + UZ_T;
 //  3. each thread decodes and checks its two tokens (the reference's checks:
 //     header inside src, length <= remaining dst, 0 < offset <= d); workgroup
-//     scans give their output offsets and cut the batch;
+//     scans give their output offsets, cut the batch, and find each copy's
+//     chain head: the first of the consecutive copies with its offset before
+//     it (a run of overlapping copies — a repeated pattern — all read the
+//     bytes just before the run's first copy: byte q of the run is byte
+//     head - o + (q - head) mod o);
 //  4. token table + output-start bitmap with per-word token counts (token m
 //     writes count m + 1 into the words starting inside it);
-//  5. every output byte resolved by a thread, 4 bytes a thread per pass of
-//     UZ_PASS bytes: a literal byte from the window, a copy byte from the
-//     history (byte r of a copy of offset o is byte d - o + r mod o), chased
-//     to its source when that is a byte of the same pass;
+//  5. every output byte resolved by a thread, one aligned history dword a
+//     thread per pass of UZ_PASS bytes: a literal byte from the window, a
+//     copy byte from the history, chased to its source when that is a byte of
+//     the same pass;
 //  6. whole 16-byte chunks from the history to HBM.
 // Long literals (tag >= 60 << 2) are copied by the workgroup straight to HBM,
-// their last 64 KiB into the history.  A source older than the history (an
-// offset past 64 KiB - UZ_OUT, which block-structured encoders never write)
-// is read back from the staged output.
+// their last 64 KiB into the history.  A source the pass may overwrite (an
+// offset within UZ_PASS of 64 KiB) or older than the history is read back
+// from the staged output.
 // ===========================================================================
-constexpr int UZ_T = 256;                         // threads
+constexpr int UZ_T = 512;                         // threads
+constexpr int UZ_W = UZ_T / 64;                   // waves
 constexpr int UZ_HIST = 65536;                    // history (ring) bytes
 constexpr uint32_t UZ_HMASK = UZ_HIST - 1;
-constexpr int UZ_POS = 1024;                      // window positions parsed per batch
+constexpr int UZ_POS = 2048;                      // window positions parsed per batch
 constexpr int UZ_STOP = UZ_POS;                   // the chain's end in the jump tables
 constexpr int UZ_WIN_DW = (UZ_POS + 64 + 8) / 4;  // staged dwords: skew, positions, a short literal's payload
 constexpr int UZ_TOK = 2 * UZ_T;                  // tokens per batch (two per thread)
-constexpr int UZ_OUT = 4096;                      // output bytes per batch
-constexpr int UZ_ROUNDS = 9;                      // 2^9 = UZ_TOK
+constexpr int UZ_OUT = 8192;                      // output bytes per batch
+constexpr int UZ_PASS = 4 * UZ_T;                 // output bytes resolved per pass
+constexpr int UZ_ROUNDS = 10;                     // 2^10 = UZ_TOK
 static_assert((1 << UZ_ROUNDS) == UZ_TOK && UZ_WIN_DW > UZ_T && UZ_WIN_DW <= 2 * UZ_T, "k_snappy_wg shapes");
 
 struct UzLds {
   uint8_t hist[UZ_HIST];
   uint32_t win[UZ_WIN_DW + 2];
   union {
-    uint16_t jt[2][UZ_POS + 4];  // J_b ping-pong; entry UZ_STOP = UZ_STOP
-    uint2 tok[UZ_TOK];           // {out_rel | len << 16 | literal << 31, literal: window position / copy: offset}
+    uint16_t jt[2][UZ_POS + 8];  // J_b ping-pong; entry UZ_STOP = UZ_STOP
+    uint2 tok[UZ_TOK];           // {out_rel | (len - 1) << 13 | head << 19 | literal << 31,
+                                 //  literal: window position of its bytes / copy: offset}
   };
   uint2 bmc[UZ_OUT / 32];        // output-start bits, tokens starting before the word
-  int32_t red[16];               // per wave: output bytes of tokens A, B; valid tokens A, B
-  int32_t last[8][4];            // per wave and token half: {last accepted token + 1, its end, stream bytes}
-  uint32_t flags;                // 1: a bad token, 2: a source older than the history
+  int32_t red[2 * UZ_W];         // per wave and token half: output bytes
+  int32_t last[2 * UZ_W][4];     // per wave and half: {last accepted token + 1, its end, stream bytes after it}
+  uint32_t chn[2 * UZ_W][4];     // per wave and half: first / last token's copy offset (0: not a copy),
+                                 // the last token's head + 1 taking the first token as a head
+  uint32_t flags;                // 1: a bad token, 2: a source the history may not hold
   uint32_t go;
 };
 
-// Output byte j of the batch; `base`: the first byte of the current pass
-// (earlier bytes of the batch are already in the history).
-__device__ __forceinline__ uint32_t uz_byte(const UzLds &U, const uint8_t *wb, int j, int base, int64_t dpos,
-                                            int64_t near_lo, const uint8_t *dst) {
-  int q = j;
-  for (;;) {
-    const uint2 e = U.bmc[q >> 5];
-    const int k = (int)e.y + __builtin_popcount(e.x & (0xffffffffu >> (31 - (q & 31)))) - 1;
-    const uint2 t = U.tok[k];
-    const int out_rel = (int)(t.x & 0xffffu), len = (int)((t.x >> 16) & 0x7fu);
-    const uint32_t r = (uint32_t)(q - out_rel);
-    if (t.x >> 31) return wb[t.y + r];
-    const uint32_t off = t.y;
-    const int64_t q2 = (int64_t)out_rel - (int64_t)off + (int64_t)(off >= (uint32_t)len ? r : r % off);
-    if (q2 >= 0) {
-      if (q2 < base) return U.hist[(uint32_t)(dpos + q2) & UZ_HMASK];
-      q = (int)q2;  // a byte of this pass: resolve its own source
-      continue;
-    }
-    const int64_t p = dpos + q2;
-    if (p >= near_lo) return U.hist[(uint32_t)p & UZ_HMASK];
-    const uintptr_t from = (uintptr_t)(dst + p);  // older than the history: the staged output
-    const uint32_t w = __hip_atomic_load((const uint32_t *)(from & ~(uintptr_t)3), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-    return (w >> ((from & 3) * 8)) & 0xffu;
+// Four history bytes [P, P + 4) (P = 4-aligned history position, batch
+// offsets q0 .. q0 + 3) resolved; bytes outside [0, T) keep the history's.
+// `base`: the batch offset where the current pass starts (earlier bytes of the
+// batch are in the history); `safe_lo`: older positions the pass may have
+// overwritten, read from the staged output.
+__device__ __forceinline__ uint32_t uz_dword(const UzLds &U, const uint8_t *wb, int q0, int T, int base,
+                                             int64_t dpos, int64_t safe_lo, const uint8_t *dst, uint32_t old) {
+  int q[4];
+  uint32_t v[4], pend = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    q[k] = q0 + k;
+    v[k] = (old >> (8 * k)) & 0xffu;
+    if (q[k] >= 0 && q[k] < T) pend |= 1u << k;
   }
+  while (pend) {
+    // one lookup step for every pending byte, loads of the four in flight together
+    uint2 t[4];
+    int kk[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int qc = (pend >> k) & 1 ? q[k] : 0;
+      const uint2 e = U.bmc[qc >> 5];
+      kk[k] = (int)e.y + __builtin_popcount(e.x & (0xffffffffu >> (31 - (qc & 31)))) - 1;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) t[k] = U.tok[(pend >> k) & 1 ? kk[k] : 0];
+    uint32_t hx[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) hx[k] = U.tok[(pend >> k) & 1 ? (t[k].x >> 19) & 1023 : 0].x;
+    int off_lds[4];  // LDS byte to read (win or hist), -1: none
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      off_lds[k] = -1;
+      if (!((pend >> k) & 1)) continue;
+      const int o = (int)(t[k].x & 0x1fff);
+      if (t[k].x >> 31) {  // literal
+        off_lds[k] = (int)(wb - (const uint8_t *)&U) + (int)t[k].y + (q[k] - o);
+        continue;
+      }
+      const int oh = (int)(hx[k] & 0x1fff);  // the chain head's start
+      const uint32_t off = t[k].y, r = (uint32_t)(q[k] - oh);
+      const int64_t q2 = (int64_t)oh - (int64_t)off + (int64_t)(r < off ? r : r % off);
+      if (q2 >= 0) {
+        if (q2 < base) off_lds[k] = (int)((uint32_t)(dpos + q2) & UZ_HMASK);
+        else q[k] = (int)q2;  // a byte of this pass: its own source next step
+        continue;
+      }
+      const int64_t p = dpos + q2;
+      if (p >= safe_lo) {
+        off_lds[k] = (int)((uint32_t)p & UZ_HMASK);
+      } else {  // the staged output (flushed by earlier batches)
+        const uintptr_t from = (uintptr_t)(dst + p);
+        const uint32_t w = __hip_atomic_load((const uint32_t *)(from & ~(uintptr_t)3), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        v[k] = (w >> ((from & 3) * 8)) & 0xffu;
+        pend &= ~(1u << k);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (off_lds[k] >= 0) {
+        v[k] = ((const uint8_t *)&U)[off_lds[k]];
+        pend &= ~(1u << k);
+      }
+  }
+  return v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
 }
 
 // Decode the short token at window position pos (its tag is not a long
-// literal): output length, literal payload position or copy offset, header
-// bytes, and whether its header / payload lies past the block end.
+// literal): output length, literal payload position or copy offset, bytes in
+// the stream, and whether its header / payload lies past the block end.
 __device__ __forceinline__ void uz_token(const UzLds &U, int sh, int pos, int64_t sabs, int64_t slen, uint32_t &len,
                                          uint32_t &x, bool &lit, bool &bad, int &adv) {
   const int b = sh + pos;
@@ -1544,9 +1593,42 @@ __device__ __forceinline__ void uz_token(const UzLds &U, int sh, int pos, int64_
   bad = sabs + adv > slen;
 }
 
+__device__ __forceinline__ uint32_t wave_incl_max32(uint32_t v) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = shfl32(v, lane >= d ? lane - d : lane);
+    if (lane >= d) v = max(v, o);
+  }
+  return v;
+}
+
+// diagnostic build (-DPQ_SNAP_STAMPS, tools/diag_snappy.py): thread 0's
+// shader cycles per step of a batch — 0 window, 1 chain, 2 decode + scans,
+// 3 table, 4 long literals, 5 byte passes, 6 flush; 7 batches — per page
+#ifdef PQ_SNAP_STAMPS
+#define UZ_TS(i)                                                    \
+  do {                                                              \
+    if (tid == 0) {                                                 \
+      const uint64_t t_ = __builtin_amdgcn_s_memtime();             \
+      if ((i) >= 0) uz_acc[(i) < 0 ? 0 : (i)] += t_ - uz_prev;      \
+      uz_prev = t_;                                                 \
+    }                                                               \
+  } while (0)
+#else
+#define UZ_TS(i) \
+  do {           \
+  } while (0)
+#endif
+
 template <int MODE>
-__global__ __launch_bounds__(UZ_T) void k_snappy_wg(KArgs a) {
+__global__ __launch_bounds__(UZ_T) __attribute__((amdgpu_waves_per_eu(4))) void k_snappy_wg(KArgs a) {
   __shared__ __attribute__((aligned(16))) UzLds U;
+#ifdef PQ_SNAP_STAMPS
+  uint64_t uz_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t uz_prev = __builtin_amdgcn_s_memtime();
+  const uint64_t uz_t0 = uz_prev;
+#endif
   const int tid = threadIdx.x;
   const int lane = lane_id();
   const int wv = (int)ufirst((uint32_t)tid >> 6);
@@ -1591,7 +1673,7 @@ __global__ __launch_bounds__(UZ_T) void k_snappy_wg(KArgs a) {
   if (seg) {
     // k_snappy_walk checked the preamble and found the segment's first token
     s = (int64_t)__hip_atomic_load(&a.segs[a.seg_base[gi] + seg_k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s = (int64_t)ufirst64((uint64_t)s);
+    s = ufirst64(s);
     seg_lo = (int64_t)seg_k * SNAP_SEG;
     dl = min(seg_lo + SNAP_SEG, expect);
     write = true;
@@ -1661,7 +1743,9 @@ __global__ __launch_bounds__(UZ_T) void k_snappy_wg(KArgs a) {
     if (tid < UZ_WIN_DW - UZ_T) U.win[UZ_T + tid] = pw1;
     if (tid < UZ_OUT / 32) U.bmc[tid] = make_uint2(0u, 0u);
     if (tid == 0) U.flags = 0u;
+    UZ_TS(-1);
     __syncthreads();
+    UZ_TS(0);
     const uint8_t *wb = (const uint8_t *)U.win + sh;  // wb[p]: stream byte s + p
     const int64_t lim64 = slen - s - 1;               // the last position inside the block
     const int lim = lim64 < UZ_POS - 1 ? (int)lim64 : UZ_POS - 1;
@@ -1721,6 +1805,7 @@ __global__ __launch_bounds__(UZ_T) void k_snappy_wg(KArgs a) {
       dpos += len;
       s += hs + len;
       __syncthreads();  // the history's new bytes; the window's last readers
+      UZ_TS(4);
       continue;
     }
     // ---- 2. J_0 for positions 4 tid .. 4 tid + 3, then the chain by pointer jumping
@@ -1742,7 +1827,7 @@ __global__ __launch_bounds__(UZ_T) void k_snappy_wg(KArgs a) {
     }
     __syncthreads();
     int pa = 0, pb = 0;  // the positions of tokens tid (A) and UZ_T + tid (B)
-#pragma unroll
+#pragma unroll 1
     for (int b = 0; b < UZ_ROUNDS; b++) {
       const int ha = ja[pa], hb = ja[pb];
       if (b < UZ_ROUNDS - 1) {
@@ -1757,9 +1842,17 @@ __global__ __launch_bounds__(UZ_T) void k_snappy_wg(KArgs a) {
         uint16_t *t = ja;
         ja = jb;
         jb = t;
+        // the chain ends within 2^(b+1) tokens: the later tokens do not exist
+        // and the earlier ones have taken every jump they need
+        if (ja[0] == UZ_STOP) {
+          if ((tid >> (b + 1)) != 0) pa = UZ_STOP;
+          pb = UZ_STOP;
+          break;
+        }
       }
     }
-    // ---- 3. decode + check tokens A and B; output offsets by workgroup scans
+    UZ_TS(1);
+    // ---- 3. decode + check tokens A and B; output offsets and chain heads by workgroup scans
     const bool vA = pa <= lim && snappy_tok_class(wb[pa]) != 0;
     const bool vB = pb <= lim && snappy_tok_class(wb[pb]) != 0;
     uint32_t lenA = 0, xA = 0, lenB = 0, xB = 0;
@@ -1768,18 +1861,51 @@ __global__ __launch_bounds__(UZ_T) void k_snappy_wg(KArgs a) {
     if (vA) uz_token(U, sh, pa, s + pa, slen, lenA, xA, litA, badA, advA);
     if (vB) uz_token(U, sh, pb, s + pb, slen, lenB, xB, litB, badB, advB);
     const int32_t iA = wave_incl_scan32((int32_t)lenA), iB = wave_incl_scan32((int32_t)lenB);
+    // chain heads: token m continues the copy run of m - 1 when both are copies
+    // of one offset; the head of m is the last token <= m that does not
+    // (head + 1 by a max-scan, a wave's first token taken as a head for now)
+    const uint32_t keyA = vA && !litA ? xA : 0u, keyB = vB && !litB ? xB : 0u;
+    const uint32_t kpA = shfl32(keyA, lane > 0 ? lane - 1 : 0), kpB = shfl32(keyB, lane > 0 ? lane - 1 : 0);
+    const int mA = tid, mB = UZ_T + tid;
+    const uint32_t hA = wave_incl_max32(lane > 0 && keyA != 0 && keyA == kpA ? 0u : (uint32_t)mA + 1);
+    const uint32_t hB = wave_incl_max32(lane > 0 && keyB != 0 && keyB == kpB ? 0u : (uint32_t)mB + 1);
     if (lane == 63) {
       U.red[wv] = iA;
-      U.red[4 + wv] = iB;
+      U.red[UZ_W + wv] = iB;
+      U.chn[wv][1] = keyA;
+      U.chn[wv][2] = hA;
+      U.chn[UZ_W + wv][1] = keyB;
+      U.chn[UZ_W + wv][2] = hB;
+    }
+    if (lane == 0) {
+      U.chn[wv][0] = keyA;
+      U.chn[UZ_W + wv][0] = keyB;
     }
     __syncthreads();  // (also: every jump-table read is done; the table below reuses the space)
     int32_t preA = 0, totA = 0, preB = 0;
 #pragma unroll
-    for (int w = 0; w < 4; w++) {
-      const int32_t ra = U.red[w], rb = U.red[4 + w];
+    for (int w = 0; w < UZ_W; w++) {
+      const int32_t ra = U.red[w], rb = U.red[UZ_W + w];
       totA += ra;
       preA += w < wv ? ra : 0;
       preB += w < wv ? rb : 0;
+    }
+    // heads across waves: the slots in token order (A waves, then B waves),
+    // each wave's first token a continuation when it continues the previous
+    // slot's last token; carry = the final head + 1 of a slot's last token
+    uint32_t headA = hA, headB = hB;
+    {
+      uint32_t carry = 0, prev_last = 0;
+#pragma unroll 1
+      for (int i = 0; i < 2 * UZ_W; i++) {
+        const uint4 c = *(const uint4 *)U.chn[i];
+        const uint32_t mfirst = (uint32_t)((i >= UZ_W ? UZ_T : 0) + (i % UZ_W) * 64);
+        const bool c0 = i > 0 && c.x != 0 && c.x == prev_last;
+        if (i == wv && c0 && hA == mfirst + 1) headA = carry;
+        if (i == UZ_W + wv && c0 && hB == mfirst + 1) headB = carry;
+        carry = (c0 && c.z == mfirst + 1) ? carry : c.z;
+        prev_last = c.y;
+      }
     }
     const int32_t endA = preA + iA, endB = totA + preB + iB;  // output offsets after each token
     const int64_t room = dl - dpos;
@@ -1788,14 +1914,14 @@ __global__ __launch_bounds__(UZ_T) void k_snappy_wg(KArgs a) {
     const bool accA = vA && endA <= UZ_OUT && (int64_t)endA - (int64_t)lenA < room;
     const bool accB = vB && endB <= UZ_OUT && (int64_t)endB - (int64_t)lenB < room;
     const int32_t oA = endA - (int32_t)lenA, oB = endB - (int32_t)lenB;
-    const int64_t near_lo = dpos + UZ_OUT - UZ_HIST;  // sources below: the slow path
+    const int64_t risky_lo = dpos + UZ_OUT + UZ_PASS - UZ_HIST;  // sources below may take the slow path
     uint32_t fl = 0;
     if (accA) {
       const int64_t dd = dpos + oA;
       badA |= (int64_t)lenA > dl - dd;
       if (!litA) {
         badA |= xA == 0 || (int64_t)xA > dd - seg_lo;
-        fl |= dd - (int64_t)xA < near_lo ? 2u : 0u;
+        fl |= dd - (int64_t)xA < risky_lo ? 2u : 0u;
       }
       fl |= badA ? 1u : 0u;
     }
@@ -1804,41 +1930,42 @@ __global__ __launch_bounds__(UZ_T) void k_snappy_wg(KArgs a) {
       badB |= (int64_t)lenB > dl - dd;
       if (!litB) {
         badB |= xB == 0 || (int64_t)xB > dd - seg_lo;
-        fl |= dd - (int64_t)xB < near_lo ? 2u : 0u;
+        fl |= dd - (int64_t)xB < risky_lo ? 2u : 0u;
       }
       fl |= badB ? 1u : 0u;
     }
+    UZ_TS(2);
     // ---- 4. token table, start bits, per-word counts; the batch's extent
     if (accA) {
-      U.tok[tid] = make_uint2((uint32_t)oA | (lenA << 16) | (litA ? 0x80000000u : 0u), xA);
+      U.tok[mA] = make_uint2((uint32_t)oA | ((lenA - 1) << 13) | ((headA - 1) << 19) | (litA ? 0x80000000u : 0u), xA);
       __hip_atomic_fetch_or(&U.bmc[oA >> 5].x, 1u << (oA & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      for (int32_t w = (oA >> 5) + 1; w <= (endA >> 5) && w < UZ_OUT / 32; w++) U.bmc[w].y = (uint32_t)(tid + 1);
+      for (int32_t w = (oA >> 5) + 1; w <= (endA >> 5) && w < UZ_OUT / 32; w++) U.bmc[w].y = (uint32_t)(mA + 1);
     }
     if (accB) {
-      U.tok[UZ_T + tid] = make_uint2((uint32_t)oB | (lenB << 16) | (litB ? 0x80000000u : 0u), xB);
+      U.tok[mB] = make_uint2((uint32_t)oB | ((lenB - 1) << 13) | ((headB - 1) << 19) | (litB ? 0x80000000u : 0u), xB);
       __hip_atomic_fetch_or(&U.bmc[oB >> 5].x, 1u << (oB & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      for (int32_t w = (oB >> 5) + 1; w <= (endB >> 5) && w < UZ_OUT / 32; w++) U.bmc[w].y = (uint32_t)(UZ_T + tid + 1);
+      for (int32_t w = (oB >> 5) + 1; w <= (endB >> 5) && w < UZ_OUT / 32; w++) U.bmc[w].y = (uint32_t)(mB + 1);
     }
     {
-      const uint64_t mA = ballot(accA), mB = ballot(accB);
+      const uint64_t bA = ballot(accA), bB = ballot(accB);
       const uint32_t fw = (ballot(fl & 1u) ? 1u : 0u) | (ballot(fl & 2u) ? 2u : 0u);
-      const int LA = mA ? 63 - __builtin_clzll(mA) : -1, LB = mB ? 63 - __builtin_clzll(mB) : -1;
+      const int LA = bA ? 63 - __builtin_clzll(bA) : -1, LB = bB ? 63 - __builtin_clzll(bB) : -1;
       if (lane == (LA < 0 ? 0 : LA)) {
-        U.last[wv][0] = LA < 0 ? 0 : tid + 1;
+        U.last[wv][0] = LA < 0 ? 0 : mA + 1;
         U.last[wv][1] = endA;
         U.last[wv][2] = pa + advA;
       }
       if (lane == (LB < 0 ? 0 : LB)) {
-        U.last[4 + wv][0] = LB < 0 ? 0 : UZ_T + tid + 1;
-        U.last[4 + wv][1] = endB;
-        U.last[4 + wv][2] = pb + advB;
+        U.last[UZ_W + wv][0] = LB < 0 ? 0 : mB + 1;
+        U.last[UZ_W + wv][1] = endB;
+        U.last[UZ_W + wv][2] = pb + advB;
       }
       if (lane == 0 && fw) __hip_atomic_fetch_or(&U.flags, fw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     __syncthreads();
     int ntok = 0, T = 0, cur = 0;
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
+#pragma unroll 1
+    for (int q = 0; q < 2 * UZ_W; q++) {
       const int m = U.last[q][0];
       if (m > ntok) {
         ntok = m;
@@ -1847,6 +1974,7 @@ __global__ __launch_bounds__(UZ_T) void k_snappy_wg(KArgs a) {
       }
     }
     const uint32_t flags = U.flags;
+    UZ_TS(3);
     if (ntok == 0 || (flags & 1u)) {  // output complete with tokens left, or a corrupt token
       err = E_SNAPPY;
       break;
@@ -1860,25 +1988,26 @@ __global__ __launch_bounds__(UZ_T) void k_snappy_wg(KArgs a) {
       pf_s = sn;
     }
     if (write) {
-      if (flags & 2u) {  // a source older than the history: the earlier flushes must be visible
+      if (flags & 2u) {  // a slow-path source: the earlier flushes must be visible
         __threadfence();
         __syncthreads();
       }
-      // ---- 5. every output byte: passes of 4 bytes a thread
-      for (int base = 0; base < T; base += 4 * UZ_T) {
-        uint32_t v[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const int j = base + k * UZ_T + tid;
-          v[k] = j < T ? uz_byte(U, wb, j, base, dpos, near_lo, dst) : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const int j = base + k * UZ_T + tid;
-          if (j < T) U.hist[(uint32_t)(dpos + j) & UZ_HMASK] = (uint8_t)v[k];
-        }
+      // ---- 5. every output byte: passes over the history's aligned dwords,
+      // one a thread; batch offset of the first dword's first byte: a0 <= 0
+      const int a0 = -(int)((uint32_t)dpos & 3);
+      for (int base = a0; base < T; base += UZ_PASS) {
+        const int q0 = base + 4 * tid;
+        const uint32_t P = (uint32_t)(dpos + q0) & UZ_HMASK;  // 4-aligned
+        const bool inside = q0 < T && q0 + 3 >= 0;
+        const bool whole = q0 >= 0 && q0 + 3 < T;
+        uint32_t old = 0;
+        if (inside && !whole) old = *(const uint32_t *)(U.hist + P);
+        const int64_t safe_lo = dpos + base + UZ_PASS - UZ_HIST;
+        const uint32_t val = inside ? uz_dword(U, wb, q0, T, base < 0 ? 0 : base, dpos, safe_lo, dst, old) : 0u;
+        if (inside) *(uint32_t *)(U.hist + P) = val;
         __syncthreads();
       }
+      UZ_TS(5);
       // ---- 6. to HBM: bytes up to the next 16-byte boundary (F is unaligned
       // after a long literal), then whole 16-byte chunks up to floor16(dpos + T)
       const int64_t end = dpos + T;
@@ -1891,9 +2020,13 @@ __global__ __launch_bounds__(UZ_T) void k_snappy_wg(KArgs a) {
         for (int64_t c = F + 16 * (int64_t)tid; c < e16; c += 16 * UZ_T)
           gst128((uintptr_t)(dst + c), *(const uint4 *)(U.hist + ((uint32_t)c & UZ_HMASK)));
       if (e16 > F) F = e16;
+      UZ_TS(6);
     } else {
-      __syncthreads();  // the window's readers (the next batch overwrites it)
+      __syncthreads();  // the window's and the batch words' readers (the next batch rewrites them)
     }
+#ifdef PQ_SNAP_STAMPS
+    if (tid == 0) uz_acc[7] += 1;
+#endif
     dpos += T;
     s += cur;
   }
@@ -1909,6 +2042,17 @@ __global__ __launch_bounds__(UZ_T) void k_snappy_wg(KArgs a) {
     err = E_OK;
   }
   if (err && tid == 0) atomicMin(&a.status[page], make_status(ST_DECOMPRESS, err));
+#ifdef PQ_SNAP_STAMPS
+  if (tid == 0 && a.dbg2)
+    for (int q = 0; q < 8; q++) atomicAdd((unsigned long long *)&a.dbg2[(size_t)page * 8 + q], (unsigned long long)uz_acc[q]);
+  if (tid == 0 && a.dbg) {
+    const uint64_t tt = __builtin_amdgcn_s_memtime() - uz_t0;
+    atomicAdd((unsigned long long *)&a.dbg[(size_t)page * 4 + 0], (unsigned long long)tt);
+    atomicMax((unsigned long long *)&a.dbg[(size_t)page * 4 + 1], (unsigned long long)tt);
+    a.dbg[(size_t)page * 4 + 2] = (uint64_t)expect;
+    a.dbg[(size_t)page * 4 + 3] = (uint64_t)slen;
+  }
+#endif
 }
 
 // ===========================================================================

@@ -48,7 +48,8 @@ ph = ph[:8 * npg].reshape(npg, 8).astype(np.float64)
 pg = pg[:4 * npg].reshape(npg, 4).astype(np.float64)  # per page: wave-cycles (all segments), longest wave, bytes out, in
 names = [c["name"] for c in r.Columns()]
 print("%s: %d pages; longest wave %.0f kcycles" % (cfg, npg, pg[:, 1].max() / 1e3))
-steps = ["window", "chain", "decode", "far", "tables", "bytes", "flush"]
+steps = (["window", "chain", "decode", "far", "tables", "bytes", "flush"] if os.environ.get("PQG_SNAPPY_V1") == "1"
+         else ["window", "chain", "decode", "table", "longlit", "bytes", "flush"])  # k_snappy_wg
 print("%-16s %6s %8s %8s %9s | %s | %s" % ("column", "pages", "batches", "MB out", "kcyc/pg", " ".join("%7s" % s for s in steps),
                                            "cyc/batch"))
 for ci in sorted(set((pc >> 8).tolist())):
