@@ -55,6 +55,7 @@ def lib():
         L.pqref_unpack8_32.argtypes = [ctypes.c_char_p, i32, ctypes.POINTER(ctypes.c_int32)]
         L.pqref_unpack8_64.argtypes = [ctypes.c_char_p, i32, ctypes.POINTER(ctypes.c_int64)]
         L.pqref_hybrid_decode.argtypes = [ctypes.c_char_p, sz, i32, ctypes.POINTER(ctypes.c_int32), i64]
+        L.pqref_decode_quirks.argtypes = [vp, i32, i32, i32, ctypes.POINTER(vp)]
         _LIB = L
     return _LIB
 
@@ -133,6 +134,34 @@ class File:
                 p = L.pqref_result_buffer(r, bid, ctypes.byref(n))
                 out[name] = np.frombuffer(ctypes.string_at(p, n.value), dtype=np.uint8).copy() if n.value else np.zeros(0, np.uint8)
             return out
+        finally:
+            L.pqref_result_free(r)
+
+
+    def decode_quirks(self, leaf, rg0=0, rg1=None):
+        """ref-quirks mode (documentation only): the
+        values the reference's row reader returns for a fixed-width leaf —
+        'values' (one per defined level, in level order) and 'valid' (bool per
+        value: not nil) — with its column store's aliasing reproduced."""
+        if rg1 is None:
+            rg1 = self.num_row_groups
+        r = ctypes.c_void_p()
+        L = lib()
+        L.pqref_decode_quirks(self._h, leaf, rg0, rg1, ctypes.byref(r))
+        try:
+            st = L.pqref_result_status(r)
+            if st != 0:
+                raise OracleError(st, L.pqref_result_error(r).decode(),
+                                  L.pqref_result_error_rg(r), L.pqref_result_error_page(r))
+            n = L.pqref_result_count(r, CNT_NONNULL)
+            sz = ctypes.c_size_t()
+            p = L.pqref_result_buffer(r, BUF_VALUES, ctypes.byref(sz))
+            vals = np.frombuffer(ctypes.string_at(p, sz.value), np.uint8).copy() if sz.value else np.zeros(0, np.uint8)
+            p = L.pqref_result_buffer(r, BUF_VALIDITY, ctypes.byref(sz))
+            bits = np.frombuffer(ctypes.string_at(p, sz.value), np.uint8) if sz.value else np.zeros(0, np.uint8)
+            valid = np.unpackbits(bits, bitorder="little")[:n].astype(bool)
+            return {"values": vals, "valid": valid, "nonnull": n,
+                    "levels": L.pqref_result_count(r, CNT_LEVELS)}
         finally:
             L.pqref_result_free(r)
 

@@ -1519,53 +1519,40 @@ static void set_err(pqref_result *r, int code, int rg, int page, const char *fmt
 
 static void bit_set(bytebuf *b, int64_t i) { b->p[i >> 3] |= (uint8_t)(1u << (i & 7)); }
 
-int pqref_decode(const pqref_file *f, int leaf, int rg0, int rg1, pqref_result **out) {
-  pqref_result *R = (pqref_result *)calloc(1, sizeof(pqref_result));
-  R->err_rg = -1;
-  R->err_page = -1;
-  *out = R;
-  if (leaf < 0 || leaf >= f->nleaves || rg0 < 0 || rg1 > f->nrgs || rg0 > rg1) {
-    set_err(R, PQR_ERR_ARG, -1, -1, "bad arguments");
-    return R->status;
-  }
-  const pqref_leaf *L = &f->leaves[leaf];
-  int w = value_width(L);
-  int is_ba = L->physical_type == PQR_BYTE_ARRAY;
-  R->counts[PQR_CNT_VALUE_WIDTH] = is_ba ? 0 : w;
-
-  /* gather dense per-page results for all row groups */
-  bytebuf levels_def = {0}, levels_rep = {0}, dense_vals = {0}, dense_lens = {0};
-  int64_t total_levels = 0, total_nonnull = 0, total_pages = 0;
-
-  for (int rg = rg0; rg < rg1 && !R->status; rg++) {
+/* readChunk + readPages, phase 1 (chunk_reader.go:206-346, :314-346): the
+ * dictionary page decoded into *dict, every data page initialised (p.init +
+ * p.read) into *pages_out; errors into R (the first one ends the chunk) */
+static void read_chunk_pages(const pqref_file *f, const pqref_leaf *L, int leaf, int rg, pqref_result *R,
+                             dictionary *dict, page_reader **pages_out, int *npages_out) {
+  *pages_out = NULL;
+  *npages_out = 0;
+  {
     const row_group *G = &f->rgs[rg];
     if (leaf >= G->ncols) {
       set_err(R, PQR_ERR_PAGE, rg, -1, "column index %d is out of bounds", leaf);
-      break;
+      return;
     }
     const col_chunk *C = &G->cols[leaf];
     /* readChunk chunk_reader.go:314-346 */
     if (C->has_file_path) {
       set_err(R, PQR_ERR_PAGE, rg, -1, "nyi: data is in another file");
-      break;
+      return;
     }
     if (!C->has_meta) {
       set_err(R, PQR_ERR_PAGE, rg, -1, "missing meta data");
-      break;
+      return;
     }
     if (C->type != L->physical_type) {
       set_err(R, PQR_ERR_PAGE, rg, -1, "wrong type in Column chunk metadata");
-      break;
+      return;
     }
     int64_t offset = C->has_dict_off ? C->dict_page_offset : C->data_page_offset;
     if (offset < 0 || (uint64_t)offset > f->len) {
       set_err(R, PQR_ERR_SIZE, rg, -1, "seek out of range");
-      break;
+      return;
     }
     /* readPages :206-284 — phase 1 over all pages */
     int64_t pos = offset, count = 0;
-    dictionary dict;
-    memset(&dict, 0, sizeof(dict));
     page_reader *pages = NULL;
     int npages = 0, page_idx = 0;
     while (C->total_compressed - count > 0) {
@@ -1580,7 +1567,7 @@ int pqref_decode(const pqref_file *f, int leaf, int rg0, int rg1, pqref_result *
       count += (int64_t)t.pos;
       int32_t csz = h.compressed;
       if (h.type == 2) { /* DICTIONARY_PAGE */
-        if (dict.present) {
+        if (dict->present) {
           set_err(R, PQR_ERR_PAGE, rg, page_idx, "there should be only one dictionary");
           break;
         }
@@ -1592,7 +1579,7 @@ int pqref_decode(const pqref_file *f, int leaf, int rg0, int rg1, pqref_result *
           set_err(R, PQR_ERR_SCHEMA, rg, page_idx, "nil type len");
           break;
         }
-        int e = read_dict_page(f, L, &h, (size_t)pos, C->codec, &dict);
+        int e = read_dict_page(f, L, &h, (size_t)pos, C->codec, dict);
         if (e) {
           set_err(R, e, rg, page_idx, "dictionary page");
           break;
@@ -1640,6 +1627,35 @@ int pqref_decode(const pqref_file *f, int leaf, int rg0, int rg1, pqref_result *
         break;
       }
     }
+    *pages_out = pages;
+    *npages_out = npages;
+  }
+}
+
+int pqref_decode(const pqref_file *f, int leaf, int rg0, int rg1, pqref_result **out) {
+  pqref_result *R = (pqref_result *)calloc(1, sizeof(pqref_result));
+  R->err_rg = -1;
+  R->err_page = -1;
+  *out = R;
+  if (leaf < 0 || leaf >= f->nleaves || rg0 < 0 || rg1 > f->nrgs || rg0 > rg1) {
+    set_err(R, PQR_ERR_ARG, -1, -1, "bad arguments");
+    return R->status;
+  }
+  const pqref_leaf *L = &f->leaves[leaf];
+  int w = value_width(L);
+  int is_ba = L->physical_type == PQR_BYTE_ARRAY;
+  R->counts[PQR_CNT_VALUE_WIDTH] = is_ba ? 0 : w;
+
+  /* gather dense per-page results for all row groups */
+  bytebuf levels_def = {0}, levels_rep = {0}, dense_vals = {0}, dense_lens = {0};
+  int64_t total_levels = 0, total_nonnull = 0, total_pages = 0;
+
+  for (int rg = rg0; rg < rg1 && !R->status; rg++) {
+    dictionary dict;
+    memset(&dict, 0, sizeof(dict));
+    page_reader *pages = NULL;
+    int npages = 0;
+    read_chunk_pages(f, L, leaf, rg, R, &dict, &pages, &npages);
     /* phase 2: readPageData :380-402 */
     int data_idx = 0;
     for (int i = 0; i < npages && !R->status; i++) {
@@ -1759,6 +1775,214 @@ int pqref_decode(const pqref_file *f, int leaf, int rg0, int rg1, pqref_result *
   free(levels_rep.p);
   free(dense_vals.p);
   free(dense_lens.p);
+  return R->status;
+}
+
+/* ------------------------------------------------------------------------ */
+/* ref-quirks mode: the values the reference's row reader returns            */
+/* ------------------------------------------------------------------------ */
+/* Documentation only: the column store the
+ * reference fills per row group and reads back row by row, for fixed-width
+ * leaves.
+ *  - readPageData appends every page's whole `data` slice — numValues slots,
+ *    only [:notNull] filled, the rest nil — to the store
+ *    (chunk_reader.go:380-402, :397); ColumnStore.get hands the k-th defined
+ *    level the store's k-th slot (data_store.go:158-203, dictStore.getNextValue
+ *    type_dict.go:114-121).  A page with nulls therefore shifts every later
+ *    page's values by its null count, and hands nil to defined levels (D1).
+ *  - The store is reset per row group with its capacity kept
+ *    (ColumnStore.reset data_store.go:59, dictStore.init type_dict.go:72); the
+ *    dictionary page decodes into that backing array when it is large enough
+ *    (chunk_reader.go:234-235, page_dict.go:50-53), and the data pages' in-place
+ *    appends then overwrite the dictionary entries later pages look up (D2).
+ * The store's capacity is modelled as Go's append growth (go 1.13 rules:
+ * double below 1024 elements, else 1.25x; large allocations rounded to 8 KiB
+ * pages of 16-byte interfaces; the small size classes are not modelled).
+ * With row groups of equal size every append after the first row group is in
+ * place, whatever the growth rule.
+ * Output: BUF_VALUES = one value per defined level (def == max_def) in level
+ * order, BUF_VALIDITY = bit k set when that value is not nil; counts LEVELS
+ * and NONNULL. */
+static int64_t go_grow(int64_t old_cap, int64_t old_len, int64_t need) {
+  int64_t c = old_cap, dbl = old_cap + old_cap;
+  if (need > dbl) c = need;
+  else if (old_len < 1024) c = dbl;
+  else
+    while (c < need) c += c / 4;
+  if (c * 16 > 32768) c = ((c * 16 + 8191) / 8192) * 8192 / 16;
+  return c;
+}
+
+int pqref_decode_quirks(const pqref_file *f, int leaf, int rg0, int rg1, pqref_result **out) {
+  pqref_result *R = (pqref_result *)calloc(1, sizeof(pqref_result));
+  R->err_rg = -1;
+  R->err_page = -1;
+  *out = R;
+  if (leaf < 0 || leaf >= f->nleaves || rg0 < 0 || rg1 > f->nrgs || rg0 > rg1) {
+    set_err(R, PQR_ERR_ARG, -1, -1, "bad arguments");
+    return R->status;
+  }
+  const pqref_leaf *L = &f->leaves[leaf];
+  const int w = value_width(L);
+  if (L->physical_type == PQR_BYTE_ARRAY || L->physical_type == PQR_BOOLEAN || w <= 0) {
+    set_err(R, PQR_ERR_UNSUPPORTED, -1, -1, "quirks mode: fixed-width leaves only");
+    return R->status;
+  }
+  R->counts[PQR_CNT_VALUE_WIDTH] = w;
+  /* the store's backing array: values + nil flags, len / cap in elements */
+  uint8_t *sv = NULL, *snil = NULL;
+  int64_t slen = 0, scap = 0;
+  bytebuf outv = {0}, outnil = {0};
+  int64_t nout = 0, nlev = 0;
+  for (int rg = rg0; rg < rg1 && !R->status; rg++) {
+    slen = 0; /* reset: values[:0], capacity kept */
+    dictionary dict;
+    memset(&dict, 0, sizeof(dict));
+    page_reader *pages = NULL;
+    int npages = 0;
+    read_chunk_pages(f, L, leaf, rg, R, &dict, &pages, &npages);
+    /* the dictionary's entries: the store's array when it holds them (then
+       later in-place appends overwrite them), else their own array */
+    const uint8_t *dv = dict.fixed, *dnil = NULL;
+    uint8_t *own_nil = NULL;
+    int aliased = 0;
+    if (!R->status && dict.present && dict.n > 0 && scap >= dict.n) {
+      memcpy(sv, dict.fixed, (size_t)dict.n * (size_t)w);
+      memset(snil, 0, (size_t)dict.n);
+      dv = sv;
+      dnil = snil;
+      aliased = 1;
+    }
+    /* levels of the row group, for the row reader */
+    bytebuf rdef = {0};
+    for (int i = 0; i < npages && !R->status; i++) {
+      page_reader *p = &pages[i];
+      int64_t n = p->is_v2 ? p->h.v2_num_values : p->h.dp_num_values;
+      uint8_t *def = (uint8_t *)calloc((size_t)n + 1, 1);
+      int e = 0;
+      /* readValues: levels, then the first notNull values (page_v1.go:27-55) */
+      for (int64_t k = 0; k < n && !e; k++) {
+        int32_t v = 0;
+        if (!p->rl_const) e = hy_next(&p->rl, &v);
+      }
+      int64_t nn = 0;
+      for (int64_t k = 0; k < n && !e; k++) {
+        int32_t v = 0;
+        if (!p->dl_const) e = hy_next(&p->dl, &v);
+        def[k] = (uint8_t)v;
+        nn += v == L->max_def;
+      }
+      uint8_t *data = (uint8_t *)calloc((size_t)(n + 1) * (size_t)w, 1), *dnl = (uint8_t *)malloc((size_t)n + 1);
+      memset(dnl, 1, (size_t)n + 1); /* make([]interface{}, n): nil until filled */
+      if (!e && nn > 0) {
+        int enc = p->enc == ENC_PLAIN_DICT ? ENC_RLE_DICT : p->enc;
+        if (enc == ENC_RLE_DICT) { /* dictDecoder.decodeValues type_dict.go:39-59, on the current entries */
+          if (!dict.present) {
+            int32_t k;
+            e = hy_next(&p->keys, &k);
+            if (!e) e = PQR_ERR_DICT_INDEX;
+          }
+          for (int64_t k = 0; k < nn && !e; k++) {
+            int32_t key;
+            e = hy_next(&p->keys, &key);
+            if (e) break;
+            if (key < 0 || (int64_t)key >= dict.n) {
+              e = PQR_ERR_DICT_INDEX;
+              break;
+            }
+            memcpy(data + (size_t)k * (size_t)w, dv + (size_t)key * (size_t)w, (size_t)w);
+            dnl[k] = dnil ? dnil[key] : 0;
+          }
+        } else {
+          dense_page dp;
+          memset(&dp, 0, sizeof(dp));
+          e = values_decode(p, L, &dict, nn, &dp);
+          if (!e) {
+            memcpy(data, dp.vals.p, (size_t)nn * (size_t)w);
+            memset(dnl, 0, (size_t)nn);
+          }
+          free(dp.vals.p);
+          free(dp.lens.p);
+        }
+      }
+      if (e) {
+        set_err(R, e, rg, i + (dict.present ? 1 : 0), "read values");
+      } else {
+        /* s.values.values = append(s.values.values, data...) (chunk_reader.go:397) */
+        if (slen + n > scap) {
+          int64_t nc = go_grow(scap, slen, slen + n);
+          uint8_t *nv = (uint8_t *)malloc((size_t)nc * (size_t)w + 1), *nnl = (uint8_t *)malloc((size_t)nc + 1);
+          if (slen) {
+            memcpy(nv, sv, (size_t)slen * (size_t)w);
+            memcpy(nnl, snil, (size_t)slen);
+          }
+          if (aliased) { /* the dictionary keeps the old array: freeze its entries */
+            own_nil = (uint8_t *)malloc((size_t)dict.n + 1);
+            memcpy(dict.fixed, sv, (size_t)dict.n * (size_t)w);
+            memcpy(own_nil, snil, (size_t)dict.n);
+            dv = dict.fixed;
+            dnil = own_nil;
+            aliased = 0;
+          }
+          free(sv);
+          free(snil);
+          sv = nv;
+          snil = nnl;
+          scap = nc;
+        }
+        memcpy(sv + (size_t)slen * (size_t)w, data, (size_t)n * (size_t)w);
+        memcpy(snil + slen, dnl, (size_t)n);
+        slen += n;
+        bb_put(&rdef, def, (size_t)n);
+      }
+      free(def);
+      free(data);
+      free(dnl);
+    }
+    /* the row reader: the k-th defined level takes the store's k-th slot */
+    if (!R->status) {
+      int64_t vpos = 0;
+      for (size_t k = 0; k < rdef.n; k++) {
+        nlev++;
+        if (rdef.p[k] < L->max_def) continue;
+        if (vpos >= slen) { /* getNextValue: "out of range" */
+          set_err(R, PQR_ERR_COUNT, rg, -1, "out of range");
+          break;
+        }
+        bb_put(&outv, sv + (size_t)vpos * (size_t)w, (size_t)w);
+        uint8_t nil = snil[vpos];
+        bb_put(&outnil, &nil, 1);
+        vpos++;
+        nout++;
+      }
+    }
+    free(rdef.p);
+    free(own_nil);
+    for (int i = 0; i < npages; i++) {
+      if (pages[i].own_body) free(pages[i].body);
+      free(pages[i].pre);
+      free(pages[i].suf);
+      free(pages[i].prev.p);
+      delta_free(&pages[i]);
+    }
+    free(pages);
+    free(dict.fixed);
+    free(dict.str_off);
+    free(dict.str_bytes);
+  }
+  if (!R->status) {
+    R->counts[PQR_CNT_LEVELS] = nlev;
+    R->counts[PQR_CNT_NONNULL] = nout;
+    bb_put(&R->bufs[PQR_BUF_VALUES], outv.p, outv.n);
+    bytebuf *VB = &R->bufs[PQR_BUF_VALIDITY];
+    bb_zero(VB, (size_t)((nout + 7) / 8));
+    for (int64_t k = 0; k < nout; k++)
+      if (!outnil.p[k]) bit_set(VB, k);
+  }
+  free(outv.p);
+  free(outnil.p);
+  free(sv);
+  free(snil);
   return R->status;
 }
 

@@ -80,6 +80,11 @@ int pqref_leaf_info(const pqref_file *f, int leaf, pqref_leaf *out);
  * semantics, then lay the result out Arrow-style (values spaced over slots,
  * nulls zeroed, validity bitmaps LSB-first, list offsets, string offsets). */
 int pqref_decode(const pqref_file *f, int leaf, int rg0, int rg1, pqref_result **out);
+/* ref-quirks mode (documentation only): for a
+ * fixed-width leaf, the values the reference's row reader returns (its column
+ * store's aliasing included): VALUES = one per defined level, VALIDITY bit =
+ * not nil.  pqref.c documents the model. */
+int pqref_decode_quirks(const pqref_file *f, int leaf, int rg0, int rg1, pqref_result **out);
 void pqref_result_free(pqref_result *r);
 
 /* Result accessors.  Buffer ids: */

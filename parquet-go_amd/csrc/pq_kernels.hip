@@ -1468,7 +1468,7 @@ constexpr int UZ_STOP = UZ_POS;                   // the chain's end in the jump
 constexpr int UZ_WIN_DW = (UZ_POS + 64 + 8) / 4;  // staged dwords: skew, positions, a short literal's payload
 constexpr int UZ_TOK = 2 * UZ_T;                  // tokens per batch (two per thread)
 constexpr int UZ_OUT = 8192;                      // output bytes per batch
-constexpr int UZ_PASS = 4 * UZ_T;                 // output bytes resolved per pass
+constexpr int UZ_PASS = 2 * UZ_T;                 // output bytes resolved per pass (two a thread)
 constexpr int UZ_ROUNDS = 10;                     // 2^10 = UZ_TOK
 static_assert((1 << UZ_ROUNDS) == UZ_TOK && UZ_WIN_DW > UZ_T && UZ_WIN_DW <= 2 * UZ_T, "k_snappy_wg shapes");
 
@@ -1485,77 +1485,38 @@ struct UzLds {
   int32_t last[2 * UZ_W][4];     // per wave and half: {last accepted token + 1, its end, stream bytes after it}
   uint32_t chn[2 * UZ_W][4];     // per wave and half: first / last token's copy offset (0: not a copy),
                                  // the last token's head + 1 taking the first token as a head
+  uint16_t src[UZ_PASS];         // per byte of the pass: 0x8000 | value, or the pass offset of its source
+  uint32_t rflag[3];             // pointer-jumping rounds: any byte left (a slot per round mod 3)
   uint32_t flags;                // 1: a bad token, 2: a source the history may not hold
   uint32_t go;
 };
 
-// Four history bytes [P, P + 4) (P = 4-aligned history position, batch
-// offsets q0 .. q0 + 3) resolved; bytes outside [0, T) keep the history's.
-// `base`: the batch offset where the current pass starts (earlier bytes of the
-// batch are in the history); `safe_lo`: older positions the pass may have
-// overwritten, read from the staged output.
-__device__ __forceinline__ uint32_t uz_dword(const UzLds &U, const uint8_t *wb, int q0, int T, int base,
-                                             int64_t dpos, int64_t safe_lo, const uint8_t *dst, uint32_t old) {
-  int q[4];
-  uint32_t v[4], pend = 0;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    q[k] = q0 + k;
-    v[k] = (old >> (8 * k)) & 0xffu;
-    if (q[k] >= 0 && q[k] < T) pend |= 1u << k;
-  }
-  while (pend) {
-    // one lookup step for every pending byte, loads of the four in flight together
-    uint2 t[4];
-    int kk[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int qc = (pend >> k) & 1 ? q[k] : 0;
-      const uint2 e = U.bmc[qc >> 5];
-      kk[k] = (int)e.y + __builtin_popcount(e.x & (0xffffffffu >> (31 - (qc & 31)))) - 1;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; k++) t[k] = U.tok[(pend >> k) & 1 ? kk[k] : 0];
-    uint32_t hx[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) hx[k] = U.tok[(pend >> k) & 1 ? (t[k].x >> 19) & 1023 : 0].x;
-    int off_lds[4];  // LDS byte to read (win or hist), -1: none
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      off_lds[k] = -1;
-      if (!((pend >> k) & 1)) continue;
-      const int o = (int)(t[k].x & 0x1fff);
-      if (t[k].x >> 31) {  // literal
-        off_lds[k] = (int)(wb - (const uint8_t *)&U) + (int)t[k].y + (q[k] - o);
-        continue;
-      }
-      const int oh = (int)(hx[k] & 0x1fff);  // the chain head's start
-      const uint32_t off = t[k].y, r = (uint32_t)(q[k] - oh);
-      const int64_t q2 = (int64_t)oh - (int64_t)off + (int64_t)(r < off ? r : r % off);
-      if (q2 >= 0) {
-        if (q2 < base) off_lds[k] = (int)((uint32_t)(dpos + q2) & UZ_HMASK);
-        else q[k] = (int)q2;  // a byte of this pass: its own source next step
-        continue;
-      }
-      const int64_t p = dpos + q2;
-      if (p >= safe_lo) {
-        off_lds[k] = (int)((uint32_t)p & UZ_HMASK);
-      } else {  // the staged output (flushed by earlier batches)
-        const uintptr_t from = (uintptr_t)(dst + p);
-        const uint32_t w = __hip_atomic_load((const uint32_t *)(from & ~(uintptr_t)3), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-        v[k] = (w >> ((from & 3) * 8)) & 0xffu;
-        pend &= ~(1u << k);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-      if (off_lds[k] >= 0) {
-        v[k] = ((const uint8_t *)&U)[off_lds[k]];
-        pend &= ~(1u << k);
-      }
-  }
-  return v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
+// Output byte q of the batch: its value (0x8000 | value) when its source is
+// a literal byte, a byte older than the pass (`base`: the pass's first batch
+// offset; earlier bytes of the batch are in the history) or older than the
+// batch; else the pass offset of its source byte (a byte of the same pass,
+// resolved by pointer jumping).  A copy byte's source is found through its
+// run's head: byte q of a run of copies of offset o starting at h is byte
+// h - o + (q - h) mod o.  `safe_lo`: older positions the pass may overwrite,
+// read back from the staged output.
+__device__ __forceinline__ uint32_t uz_direct(const UzLds &U, const uint8_t *wb, int q, int base, int64_t dpos,
+                                              int64_t safe_lo, const uint8_t *dst) {
+  const uint2 e = U.bmc[q >> 5];
+  const int kk = (int)e.y + __builtin_popcount(e.x & (0xffffffffu >> (31 - (q & 31)))) - 1;
+  const uint2 t = U.tok[kk];
+  const int o = (int)(t.x & 0x1fff);
+  if (t.x >> 31) return 0x8000u | wb[t.y + (uint32_t)(q - o)];  // literal
+  const int h = (int)((t.x >> 19) & 1023);
+  const int oh = h == kk ? o : (int)(U.tok[h].x & 0x1fff);  // the run head's start
+  const uint32_t off = t.y, r = (uint32_t)(q - oh);
+  const int64_t q2 = (int64_t)oh - (int64_t)off + (int64_t)(r < off ? r : r % off);
+  if (q2 >= base) return (uint32_t)(q2 - base);
+  const int64_t p = dpos + q2;
+  if (q2 >= 0 || p >= safe_lo) return 0x8000u | U.hist[(uint32_t)p & UZ_HMASK];
+  const uintptr_t from = (uintptr_t)(dst + p);  // the staged output (flushed by earlier batches)
+  const uint32_t w = __hip_atomic_load((const uint32_t *)(from & ~(uintptr_t)3), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  return 0x8000u | ((w >> ((from & 3) * 8)) & 0xffu);
 }
 
 // Decode the short token at window position pos (its tag is not a long
@@ -1655,6 +1616,7 @@ __global__ __launch_bounds__(UZ_T) __attribute__((amdgpu_waves_per_eu(4))) void 
     else if (seg)
       go = go && __hip_atomic_load(&a.seg_flag[gi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
     U.go = go ? 1u : 0u;
+    U.rflag[0] = U.rflag[1] = U.rflag[2] = 0u;
     if (!seg && a.max_jobs > 0) a.njobs[gi] = 0u;  // nothing deferred to k_copy
   }
   __syncthreads();
@@ -1730,6 +1692,7 @@ __global__ __launch_bounds__(UZ_T) __attribute__((amdgpu_waves_per_eu(4))) void 
   uint32_t err = E_OK;
   int64_t pf_s = -1;   // stream position of the window prefetched into pw0 / pw1
   uint32_t pw0 = 0, pw1 = 0;
+  uint32_t uz_round = 0;  // pointer-jumping rounds so far (rflag slot = round mod 3)
   while (s < slen && (!seg || dpos < dl)) {
     // ---- 1. the window: stream bytes [s, s + UZ_POS + 64) at win byte sh
     const uintptr_t abase = (uintptr_t)(src + s) & ~(uintptr_t)3;
@@ -1914,14 +1877,16 @@ __global__ __launch_bounds__(UZ_T) __attribute__((amdgpu_waves_per_eu(4))) void 
     const bool accA = vA && endA <= UZ_OUT && (int64_t)endA - (int64_t)lenA < room;
     const bool accB = vB && endB <= UZ_OUT && (int64_t)endB - (int64_t)lenB < room;
     const int32_t oA = endA - (int32_t)lenA, oB = endB - (int32_t)lenB;
-    const int64_t risky_lo = dpos + UZ_OUT + UZ_PASS - UZ_HIST;  // sources below may take the slow path
+    // a copy whose source a pass may overwrite (an offset within UZ_PASS + 64 of
+    // the history) reads it back from the staged output: flag it
+    constexpr int64_t risky_off = UZ_HIST - UZ_PASS - 64;
     uint32_t fl = 0;
     if (accA) {
       const int64_t dd = dpos + oA;
       badA |= (int64_t)lenA > dl - dd;
       if (!litA) {
         badA |= xA == 0 || (int64_t)xA > dd - seg_lo;
-        fl |= dd - (int64_t)xA < risky_lo ? 2u : 0u;
+        fl |= (int64_t)xA > risky_off ? 2u : 0u;
       }
       fl |= badA ? 1u : 0u;
     }
@@ -1930,7 +1895,7 @@ __global__ __launch_bounds__(UZ_T) __attribute__((amdgpu_waves_per_eu(4))) void 
       badB |= (int64_t)lenB > dl - dd;
       if (!litB) {
         badB |= xB == 0 || (int64_t)xB > dd - seg_lo;
-        fl |= dd - (int64_t)xB < risky_lo ? 2u : 0u;
+        fl |= (int64_t)xB > risky_off ? 2u : 0u;
       }
       fl |= badB ? 1u : 0u;
     }
@@ -1988,23 +1953,39 @@ __global__ __launch_bounds__(UZ_T) __attribute__((amdgpu_waves_per_eu(4))) void 
       pf_s = sn;
     }
     if (write) {
-      if (flags & 2u) {  // a slow-path source: the earlier flushes must be visible
-        __threadfence();
+      if (flags & 2u) {  // a slow-path source: every earlier flush store of the workgroup done
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         __syncthreads();
       }
-      // ---- 5. every output byte: passes over the history's aligned dwords,
-      // one a thread; batch offset of the first dword's first byte: a0 <= 0
+      // ---- 5. every output byte: passes of UZ_PASS bytes, two a thread (an
+      // aligned 16-bit history word); the first pass starts at a0 <= 0, its
+      // bytes before the batch are the history's
       const int a0 = -(int)((uint32_t)dpos & 3);
       for (int base = a0; base < T; base += UZ_PASS) {
-        const int q0 = base + 4 * tid;
-        const uint32_t P = (uint32_t)(dpos + q0) & UZ_HMASK;  // 4-aligned
-        const bool inside = q0 < T && q0 + 3 >= 0;
-        const bool whole = q0 >= 0 && q0 + 3 < T;
-        uint32_t old = 0;
-        if (inside && !whole) old = *(const uint32_t *)(U.hist + P);
+        const int j0 = base + 2 * tid;
+        const uint32_t P = (uint32_t)(dpos + j0) & UZ_HMASK;  // even
         const int64_t safe_lo = dpos + base + UZ_PASS - UZ_HIST;
-        const uint32_t val = inside ? uz_dword(U, wb, q0, T, base < 0 ? 0 : base, dpos, safe_lo, dst, old) : 0u;
-        if (inside) *(uint32_t *)(U.hist + P) = val;
+        const uint32_t old = *(const uint16_t *)(U.hist + P);
+        uint32_t s0 = j0 >= 0 && j0 < T ? uz_direct(U, wb, j0, base, dpos, safe_lo, dst) : 0x8000u | (old & 0xffu);
+        uint32_t s1 = j0 + 1 >= 0 && j0 + 1 < T ? uz_direct(U, wb, j0 + 1, base, dpos, safe_lo, dst) : 0x8000u | (old >> 8);
+        *(uint32_t *)(U.src + 2 * tid) = s0 | (s1 << 16);
+        // pointer jumping over the pass: a byte's source pointer becomes its
+        // source's (a value once that is resolved); in place — a read sees the
+        // old or the new pointer, both on the byte's chain
+        for (;;) {
+          const bool left = !(s0 & 0x8000u) || !(s1 & 0x8000u);
+          if (ballot(left) && lane == 0)
+            __hip_atomic_fetch_or(&U.rflag[uz_round % 3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (tid == 0) U.rflag[(uz_round + 1) % 3] = 0u;
+          __syncthreads();
+          const bool any = U.rflag[uz_round % 3] != 0u;
+          uz_round++;
+          if (!any) break;
+          if (!(s0 & 0x8000u)) s0 = U.src[s0];
+          if (!(s1 & 0x8000u)) s1 = U.src[s1];
+          *(uint32_t *)(U.src + 2 * tid) = s0 | (s1 << 16);
+        }
+        if (j0 + 1 >= 0 && j0 < T) *(uint16_t *)(U.hist + P) = (uint16_t)((s0 & 0xffu) | ((s1 & 0xffu) << 8));
         __syncthreads();
       }
       UZ_TS(5);

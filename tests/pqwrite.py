@@ -207,3 +207,46 @@ def write_column(pages, ptype=1, encoding=5, optional=False, type_length=0, dict
     fmd = _S().i32(1, 1).list(2, T_STRUCT, elems).i64(3, n_total).list(4, T_STRUCT, [rg]).done()
     out += fmd + struct.pack("<i", len(fmd)) + b"PAR1"
     return bytes(out)
+
+
+def write_row_groups(row_groups, ptype=1, encoding=8, optional=False):
+    """One leaf `v` (parquet.Type `ptype`), several row groups, V1
+    uncompressed pages: row_groups = [{"pages": [(num_values, def_levels or
+    None, values_section_bytes)], "dict_page": bytes or None, "dict_count":
+    n}].  Values sections are given as they are stored (for RLE_DICTIONARY:
+    the bit-width byte and the hybrid key stream).  Returns the file bytes."""
+    elems = [_S().str(4, "schema").i32(5, 1), _S().i32(1, ptype).i32(3, 1 if optional else 0).str(4, "v")]
+    out = bytearray(b"PAR1")
+    rgs = []
+    total = 0
+    for g in row_groups:
+        first = len(out)
+        dict_off = None
+        if g.get("dict_page") is not None:
+            dp = g["dict_page"]
+            dph = _S().i32(1, g["dict_count"]).i32(2, 0)
+            ph = _S().i32(1, 2).i32(2, len(dp)).i32(3, len(dp)).struct(7, dph).done()
+            dict_off = len(out)
+            out += ph + dp
+        data_off = len(out)
+        n_rg = 0
+        for n, dl, body in g["pages"]:
+            b = bytearray()
+            if optional:
+                s_ = hybrid_bitpacked(dl, 1)
+                b += struct.pack("<I", len(s_)) + s_
+            b += body
+            dph = _S().i32(1, n).i32(2, encoding).i32(3, 3).i32(4, 3)
+            out += _S().i32(1, 0).i32(2, len(b)).i32(3, len(b)).struct(5, dph).done() + b
+            n_rg += n
+        size = len(out) - first
+        meta = (_S().i32(1, ptype).list(2, T_I32, [0, 3, encoding]).list(3, T_BINARY, ["v"]).i32(4, 0).i64(5, n_rg)
+                .i64(6, size).i64(7, size).i64(9, data_off))
+        if dict_off is not None:
+            meta.i64(11, dict_off)
+        chunk = _S().i64(2, first).struct(3, meta)
+        rgs.append(_S().list(1, T_STRUCT, [chunk]).i64(2, size).i64(3, n_rg))
+        total += n_rg
+    fmd = _S().i32(1, 1).list(2, T_STRUCT, elems).i64(3, total).list(4, T_STRUCT, rgs).done()
+    out += fmd + struct.pack("<i", len(fmd)) + b"PAR1"
+    return bytes(out)
