@@ -1482,9 +1482,10 @@ struct UzLds {
   };
   uint2 bmc[UZ_OUT / 32];        // output-start bits, tokens starting before the word
   int32_t red[2 * UZ_W];         // per wave and token half: output bytes
-  int32_t last[2 * UZ_W][4];     // per wave and half: {last accepted token + 1, its end, stream bytes after it}
-  uint32_t chn[2 * UZ_W][4];     // per wave and half: first / last token's copy offset (0: not a copy),
-                                 // the last token's head + 1 taking the first token as a head
+  __attribute__((aligned(16))) int32_t last[2 * UZ_W][4];  // per wave and half: {last accepted token + 1, its end,
+                                                          //  stream bytes after it}
+  __attribute__((aligned(16))) uint32_t chn[2 * UZ_W][4];  // per wave and half: first / last token's copy offset
+                                                          // (0: not a copy), the scan (lane 0 left out) at lane 63
   uint16_t src[UZ_PASS];         // per byte of the pass: 0x8000 | value, or the pass offset of its source
   uint32_t rflag[3];             // pointer-jumping rounds: any byte left (a slot per round mod 3)
   uint32_t flags;                // 1: a bad token, 2: a source the history may not hold
@@ -1554,13 +1555,28 @@ __device__ __forceinline__ void uz_token(const UzLds &U, int sh, int pos, int64_
   bad = sabs + adv > slen;
 }
 
-__device__ __forceinline__ uint32_t wave_incl_max32(uint32_t v) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = shfl32(v, lane >= d ? lane - d : lane);
-    if (lane >= d) v = max(v, o);
-  }
+// wave-wide inclusive scans by DPP row shifts and row broadcasts (VALU, no
+// LDS round trips: ds_bpermute scans cost ~100 cycles a step)
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
+template <bool MAX>
+__device__ __forceinline__ uint32_t wave_incl_dpp(uint32_t v) {
+  const int lane = lane_id(), rl = lane & 15;
+  uint32_t t;
+  t = dpp_mov<0x111>(v);  // row_shr:1
+  if (rl >= 1) v = MAX ? max(v, t) : v + t;
+  t = dpp_mov<0x112>(v);  // row_shr:2
+  if (rl >= 2) v = MAX ? max(v, t) : v + t;
+  t = dpp_mov<0x114>(v);  // row_shr:4
+  if (rl >= 4) v = MAX ? max(v, t) : v + t;
+  t = dpp_mov<0x118>(v);  // row_shr:8
+  if (rl >= 8) v = MAX ? max(v, t) : v + t;
+  t = dpp_mov<0x142>(v);  // row_bcast:15
+  if ((lane & 31) >= 16) v = MAX ? max(v, t) : v + t;
+  t = dpp_mov<0x143>(v);  // row_bcast:31
+  if (lane >= 32) v = MAX ? max(v, t) : v + t;
   return v;
 }
 
@@ -1823,15 +1839,17 @@ __global__ __launch_bounds__(UZ_T) __attribute__((amdgpu_waves_per_eu(4))) void 
     int advA = 0, advB = 0;
     if (vA) uz_token(U, sh, pa, s + pa, slen, lenA, xA, litA, badA, advA);
     if (vB) uz_token(U, sh, pb, s + pb, slen, lenB, xB, litB, badB, advB);
-    const int32_t iA = wave_incl_scan32((int32_t)lenA), iB = wave_incl_scan32((int32_t)lenB);
+    const int32_t iA = (int32_t)wave_incl_dpp<false>(lenA), iB = (int32_t)wave_incl_dpp<false>(lenB);
     // chain heads: token m continues the copy run of m - 1 when both are copies
-    // of one offset; the head of m is the last token <= m that does not
-    // (head + 1 by a max-scan, a wave's first token taken as a head for now)
+    // of one offset; the head of m is the last token <= m that does not, so
+    // head + 1 is a max-scan of (head ? m + 1 : 0) over the token order.  In a
+    // wave the scan leaves lane 0 out (whether it continues the previous wave's
+    // last token is known after the barrier)
     const uint32_t keyA = vA && !litA ? xA : 0u, keyB = vB && !litB ? xB : 0u;
-    const uint32_t kpA = shfl32(keyA, lane > 0 ? lane - 1 : 0), kpB = shfl32(keyB, lane > 0 ? lane - 1 : 0);
+    const uint32_t kpA = dpp_mov<0x138>(keyA), kpB = dpp_mov<0x138>(keyB);  // wave_shr:1 (lane - 1)
     const int mA = tid, mB = UZ_T + tid;
-    const uint32_t hA = wave_incl_max32(lane > 0 && keyA != 0 && keyA == kpA ? 0u : (uint32_t)mA + 1);
-    const uint32_t hB = wave_incl_max32(lane > 0 && keyB != 0 && keyB == kpB ? 0u : (uint32_t)mB + 1);
+    const uint32_t hA = wave_incl_dpp<true>(lane == 0 || (keyA != 0 && keyA == kpA) ? 0u : (uint32_t)mA + 1);
+    const uint32_t hB = wave_incl_dpp<true>(lane == 0 || (keyB != 0 && keyB == kpB) ? 0u : (uint32_t)mB + 1);
     if (lane == 63) {
       U.red[wv] = iA;
       U.red[UZ_W + wv] = iB;
@@ -1853,20 +1871,21 @@ __global__ __launch_bounds__(UZ_T) __attribute__((amdgpu_waves_per_eu(4))) void 
       preA += w < wv ? ra : 0;
       preB += w < wv ? rb : 0;
     }
-    // heads across waves: the slots in token order (A waves, then B waves),
-    // each wave's first token a continuation when it continues the previous
-    // slot's last token; carry = the final head + 1 of a slot's last token
+    // heads across waves: the slots (waves) in token order, A then B; a slot's
+    // first token is a head unless it continues the previous slot's last one;
+    // the max over the earlier slots and the slot's own first token complete
+    // the scan
     uint32_t headA = hA, headB = hB;
     {
-      uint32_t carry = 0, prev_last = 0;
-#pragma unroll 1
+      uint32_t pre = 0, prev_last = 0;
+#pragma unroll 4
       for (int i = 0; i < 2 * UZ_W; i++) {
-        const uint4 c = *(const uint4 *)U.chn[i];
+        const uint4 c = *(const uint4 *)U.chn[i];  // {first key, last key, scan without lane 0 at lane 63}
         const uint32_t mfirst = (uint32_t)((i >= UZ_W ? UZ_T : 0) + (i % UZ_W) * 64);
-        const bool c0 = i > 0 && c.x != 0 && c.x == prev_last;
-        if (i == wv && c0 && hA == mfirst + 1) headA = carry;
-        if (i == UZ_W + wv && c0 && hB == mfirst + 1) headB = carry;
-        carry = (c0 && c.z == mfirst + 1) ? carry : c.z;
+        const uint32_t h0 = i == 0 || c.x == 0 || c.x != prev_last ? mfirst + 1 : 0u;
+        if (i == wv) headA = max(max(headA, pre), h0);
+        if (i == UZ_W + wv) headB = max(max(headB, pre), h0);
+        pre = max(pre, max(h0, c.z));
         prev_last = c.y;
       }
     }
@@ -1929,13 +1948,13 @@ __global__ __launch_bounds__(UZ_T) __attribute__((amdgpu_waves_per_eu(4))) void 
     }
     __syncthreads();
     int ntok = 0, T = 0, cur = 0;
-#pragma unroll 1
+#pragma unroll 4
     for (int q = 0; q < 2 * UZ_W; q++) {
-      const int m = U.last[q][0];
-      if (m > ntok) {
-        ntok = m;
-        T = U.last[q][1];
-        cur = U.last[q][2];
+      const int4 l = *(const int4 *)U.last[q];
+      if (l.x > ntok) {
+        ntok = l.x;
+        T = l.y;
+        cur = l.z;
       }
     }
     const uint32_t flags = U.flags;
