@@ -94,6 +94,7 @@ struct pq_launch_args {
   const int64_t *hjobs;
   int32_t nhjobs;
   int32_t grid_cap;  // k_levels<-1>: at most this many workgroups (grid-stride loop)
+  int32_t snappy_wg;  // Snappy items by k_snappy_wg (workgroup per page, 64 KiB LDS history) instead of k_snappy
   uint32_t *status_next;
   const void *sw_pages;
   void *sw_regs;
@@ -2757,6 +2758,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   if (timed && !B->ev[B->ring_head][0])  // timing events of this ring slot, made on first use
     for (int i = 0; i < 8; i++) hipEventCreate(&B->ev[B->ring_head][i]);
   pq_launch_args a = {};
+  a.snappy_wg = getenv_flag("PQG_SNAPPY_WG") ? 1 : 0;  // (read per decode: tests switch it per batch)
   a.in = B->d_in;
   a.stage = B->d_stage;
   a.in_end = B->d_in + B->in_alloc;
@@ -3541,6 +3543,7 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
     hipMemcpyAsync(d_list, &zero, 4, hipMemcpyHostToDevice, s);
     pq_launch_args a = {};
     memset(&a, 0, sizeof(a));
+    a.snappy_wg = getenv_flag("PQG_SNAPPY_WG") ? 1 : 0;
     a.in = d_in;
     a.stage = d_out;
     a.in_end = d_in + n + kPad;

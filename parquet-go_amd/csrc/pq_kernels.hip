@@ -5451,6 +5451,7 @@ struct pq_launch_args {
   const int64_t *hjobs;
   int32_t nhjobs;
   int32_t grid_cap;  // k_levels<-1>: at most this many workgroups (grid-stride loop)
+  int32_t snappy_wg;  // Snappy items by k_snappy_wg (workgroup per page, 64 KiB LDS history) instead of k_snappy
   uint32_t *status_next;
   const void *sw_pages;
   void *sw_regs;
@@ -5622,9 +5623,9 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     hipLaunchKernelGGL(pq::k_sw_link, dim3((k.n_sw_pages + 3) / 4), dim3(256), 0, s, k);
     return launch_status(which);
   }
-  // PQG_SNAPPY_V1=1 (analysis): the wave-per-page decoder k_snappy instead of
-  // the workgroup-per-page k_snappy_wg
-  static const bool snappy_v1 = getenv("PQG_SNAPPY_V1") && getenv("PQG_SNAPPY_V1")[0] == '1';
+  // k_snappy (wave per page) by default; k_snappy_wg (workgroup per page,
+  // the whole 64 KiB history in LDS) when the batch asks for it (PQG_SNAPPY_WG=1)
+  const bool snappy_v1 = p->snappy_wg == 0;
   if (which == 0) {  // Snappy over work items (pages, or segments of long pages)
     if (k.nitems <= 0) return 0;
     if (snappy_v1) hipLaunchKernelGGL(pq::k_snappy<pq::SNAP_ITEMS>, dim3((k.nitems + 3) / 4), dim3(256), 0, s, k);

@@ -22,6 +22,18 @@ def need_gpu():
         pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
 
 
+@pytest.fixture(params=["k_snappy", "k_snappy_wg"])
+def snappy_kernel(request, monkeypatch):
+    """Run a Snappy test with both decoders: the wave-per-page k_snappy (the
+    default) and the workgroup-per-page k_snappy_wg (PQG_SNAPPY_WG=1, read by
+    the library at every decode)."""
+    if request.param == "k_snappy_wg":
+        monkeypatch.setenv("PQG_SNAPPY_WG", "1")
+    else:
+        monkeypatch.delenv("PQG_SNAPPY_WG", raising=False)
+    return request.param
+
+
 def assert_same(gpu, ora, max_def, max_rep, ctx=""):
     for k in KEYS:
         if k == "validity" and max_def == 0:
@@ -124,7 +136,7 @@ def test_row_group_subsets():
     check_file(data, "c1 rg2", 2, 3)
 
 
-def test_snappy_block_roundtrip():
+def test_snappy_block_roundtrip(snappy_kernel):
     pa = pytest.importorskip("pyarrow")
     rng = np.random.default_rng(5)
     for n in (0, 1, 5, 64, 65, 4095, 8192, 8193, 70000, 300000):
@@ -179,7 +191,7 @@ def _uvarint(v):
             return bytes(out)
 
 
-def test_snappy_segments_and_fallback():
+def test_snappy_segments_and_fallback(snappy_kernel):
     """Blocks longer than 64 KiB are decoded by one wave per 64 KiB segment
     (k_snappy_walk finds the token at each boundary); streams without that
     structure fall back to the serial decode.  Every case against the oracle."""
@@ -226,7 +238,7 @@ def test_snappy_segments_and_fallback():
     both(good, len(lit) + 40000, expect_n=len(lit) + 39999)
 
 
-def test_snappy_block_errors_match_oracle():
+def test_snappy_block_errors_match_oracle(snappy_kernel):
     """DecompressBlock = snappy.Decode + the exact-size check of newBlockReader
     (compress.go:112-119): class SNAPPY if the stream is corrupt, else SIZE if
     the decoded length differs from the page header's."""
@@ -410,7 +422,7 @@ def _c5_bytes(tmp_path, rows, rg_rows, **kw):
     return open(path, "rb").read()
 
 
-def test_c5_lineitem_shape(tmp_path):
+def test_c5_lineitem_shape(tmp_path, snappy_kernel):
     """Config C5's file shape at small scale (tools/synth.py c5: 16 leaves, 4 INT64 /
     4 DOUBLE / 4 INT32 / 4 dictionary STRING): small dictionary pages make
     l_comment (and the high-cardinality numeric columns) fall back from
@@ -593,7 +605,7 @@ def test_tiled_corrupted_key_streams_match_oracle():
     assert len(outcomes) >= 2, outcomes  # the corruptions reach more than one outcome
 
 
-def test_snappy_literal_train_pages():
+def test_snappy_literal_train_pages(snappy_kernel):
     """Incompressible Snappy pages longer than one 64 KiB encoder block are a
     train of literals: the host plan copies them with k_copy (no k_snappy).
     Data pages (required, and nullable with their levels inside the V1 body),
@@ -639,7 +651,7 @@ def _snappy_one_literal(body, varint_len):
     return bytes(vb) + tag + body
 
 
-def test_snappy_single_literal_padded_varint():
+def test_snappy_single_literal_padded_varint(snappy_kernel):
     """Flat required PLAIN INT64 / INT32 Snappy pages written as one literal
     whose length uvarint is non-minimal (3..10 bytes): the host plan and
     k_snappy must read the varint by the same rules, or a page the host left to
