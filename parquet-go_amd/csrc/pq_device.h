@@ -35,40 +35,60 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
   uint32_t lo = shfl32((uint32_t)v, src), hi = shfl32((uint32_t)(v >> 32), src);
   return ((uint64_t)hi << 32) | lo;
 }
-__device__ __forceinline__ int32_t wave_incl_scan32_impl(int32_t v) {
-  int lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    int32_t o = (int32_t)shfl32((uint32_t)v, lane >= d ? lane - d : lane);
-    if (lane >= d) v += o;
-  }
+// Wave-wide scans by DPP row shifts and row broadcasts: VALU moves between
+// lanes, ~6 instructions a scan, instead of six ds_bpermute round trips
+// through the LDS crossbar (~100 cycles each under load).  Called with every
+// lane of the wave active.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
+template <bool MAX>
+__device__ __forceinline__ uint32_t wave_incl_dpp(uint32_t v) {
+  const int lane = lane_id(), rl = lane & 15;
+  uint32_t t;
+  t = dpp_mov<0x111>(v);  // row_shr:1
+  if (rl >= 1) v = MAX ? max(v, t) : v + t;
+  t = dpp_mov<0x112>(v);  // row_shr:2
+  if (rl >= 2) v = MAX ? max(v, t) : v + t;
+  t = dpp_mov<0x114>(v);  // row_shr:4
+  if (rl >= 4) v = MAX ? max(v, t) : v + t;
+  t = dpp_mov<0x118>(v);  // row_shr:8
+  if (rl >= 8) v = MAX ? max(v, t) : v + t;
+  t = dpp_mov<0x142>(v);  // row_bcast:15
+  if ((lane & 31) >= 16) v = MAX ? max(v, t) : v + t;
+  t = dpp_mov<0x143>(v);  // row_bcast:31
+  if (lane >= 32) v = MAX ? max(v, t) : v + t;
   return v;
 }
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_mov64(uint64_t v) {
+  return ((uint64_t)dpp_mov<CTRL>((uint32_t)(v >> 32)) << 32) | dpp_mov<CTRL>((uint32_t)v);
+}
+__device__ __forceinline__ uint64_t wave_incl_add64_dpp(uint64_t v) {
+  const int lane = lane_id(), rl = lane & 15;
+  uint64_t t;
+  t = dpp_mov64<0x111>(v);
+  if (rl >= 1) v += t;
+  t = dpp_mov64<0x112>(v);
+  if (rl >= 2) v += t;
+  t = dpp_mov64<0x114>(v);
+  if (rl >= 4) v += t;
+  t = dpp_mov64<0x118>(v);
+  if (rl >= 8) v += t;
+  t = dpp_mov64<0x142>(v);
+  if ((lane & 31) >= 16) v += t;
+  t = dpp_mov64<0x143>(v);
+  if (lane >= 32) v += t;
+  return v;
+}
+__device__ __forceinline__ int32_t wave_incl_scan32_impl(int32_t v) { return (int32_t)wave_incl_dpp<false>((uint32_t)v); }
 // inclusive wave prefix sum
-__device__ __forceinline__ int64_t wave_incl_scan64(int64_t v) {
-  int lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    int64_t o = (int64_t)shfl64((uint64_t)v, lane >= d ? lane - d : lane);
-    if (lane >= d) v += o;
-  }
-  return v;
-}
-__device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {  // wrapping
-  int lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint64_t o = shfl64(v, lane >= d ? lane - d : lane);
-    if (lane >= d) v += o;
-  }
-  return v;
-}
+__device__ __forceinline__ int64_t wave_incl_scan64(int64_t v) { return (int64_t)wave_incl_add64_dpp((uint64_t)v); }
+__device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) { return wave_incl_add64_dpp(v); }  // wrapping
 // wave sum (uniform)
 __device__ __forceinline__ int32_t wave_sum32(int32_t v) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v += (int32_t)shfl32((uint32_t)v, lane ^ d);
-  return (int32_t)ufirst((uint32_t)v);
+  return (int32_t)__builtin_amdgcn_readlane(wave_incl_dpp<false>((uint32_t)v), 63);
 }
 // exclusive wave prefix sum; *total receives the wave total (uniform)
 __device__ __forceinline__ int32_t wave_excl_scan32(int32_t v, int32_t *total) {
@@ -76,15 +96,7 @@ __device__ __forceinline__ int32_t wave_excl_scan32(int32_t v, int32_t *total) {
   *total = (int32_t)__builtin_amdgcn_readlane((uint32_t)incl, 63);
   return incl - v;
 }
-__device__ __forceinline__ int32_t wave_incl_scan32(int32_t v) {
-  int lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    int32_t o = (int32_t)shfl32((uint32_t)v, lane >= d ? lane - d : lane);
-    if (lane >= d) v += o;
-  }
-  return v;
-}
+__device__ __forceinline__ int32_t wave_incl_scan32(int32_t v) { return wave_incl_scan32_impl(v); }
 
 // Unaligned little-endian loads built from aligned dwords (buffers are padded
 // so reading up to 12 bytes past any stream end stays inside the allocation).

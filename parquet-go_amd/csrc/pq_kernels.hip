@@ -1555,31 +1555,6 @@ __device__ __forceinline__ void uz_token(const UzLds &U, int sh, int pos, int64_
   bad = sabs + adv > slen;
 }
 
-// wave-wide inclusive scans by DPP row shifts and row broadcasts (VALU, no
-// LDS round trips: ds_bpermute scans cost ~100 cycles a step)
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
-}
-template <bool MAX>
-__device__ __forceinline__ uint32_t wave_incl_dpp(uint32_t v) {
-  const int lane = lane_id(), rl = lane & 15;
-  uint32_t t;
-  t = dpp_mov<0x111>(v);  // row_shr:1
-  if (rl >= 1) v = MAX ? max(v, t) : v + t;
-  t = dpp_mov<0x112>(v);  // row_shr:2
-  if (rl >= 2) v = MAX ? max(v, t) : v + t;
-  t = dpp_mov<0x114>(v);  // row_shr:4
-  if (rl >= 4) v = MAX ? max(v, t) : v + t;
-  t = dpp_mov<0x118>(v);  // row_shr:8
-  if (rl >= 8) v = MAX ? max(v, t) : v + t;
-  t = dpp_mov<0x142>(v);  // row_bcast:15
-  if ((lane & 31) >= 16) v = MAX ? max(v, t) : v + t;
-  t = dpp_mov<0x143>(v);  // row_bcast:31
-  if (lane >= 32) v = MAX ? max(v, t) : v + t;
-  return v;
-}
-
 // diagnostic build (-DPQ_SNAP_STAMPS, tools/diag_snappy.py): thread 0's
 // shader cycles per step of a batch — 0 window, 1 chain, 2 decode + scans,
 // 3 table, 4 long literals, 5 byte passes, 6 flush; 7 batches — per page
