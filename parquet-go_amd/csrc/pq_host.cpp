@@ -3073,7 +3073,19 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
       hipEventRecord(LN.join[1], LN.side[1]);
     }
     if (big && big_order == 1) e |= pq_launch(22, &a, s);
-    e |= pq_launch(9, &a, s);  // k_expand_mix (tiled pages)
+    // a batch whose data pages all have host-written records (flat required
+    // PLAIN: no level streams, no key-stream walk) gives k_level_check nothing
+    // to find: k_expand_mix plans the next decode's statuses and the launch is
+    // skipped (C1; PQG_LEVEL_CHECK=1 keeps it)
+    const bool plan_next = ndata > 0 && !getenv_flag("PQG_NO_STATUS_PLAN");
+    const bool skip_check = B->all_srec && ngen == 0 && B->dba_list.empty() && !getenv_flag("PQG_LEVEL_CHECK");
+    if (skip_check && plan_next) {
+      pq_launch_args ax = a;
+      ax.status_next = B->d_status + ((a.epoch + 1) & 1) * npages;
+      e |= pq_launch(9, &ax, s);  // k_expand_mix (tiled pages) + the next statuses
+    } else {
+      e |= pq_launch(9, &a, s);  // k_expand_mix (tiled pages)
+    }
     if (big && big_order == 0) e |= pq_launch(22, &a, s);
     if (big && big_order == 2) hipStreamWaitEvent(s, LN.join[1], 0);
     if (B->ldn[4] + B->ldn[5] > 0) e |= pq_launch(27, &a, s);  // k_expand_pass (wide dictionaries)
@@ -3084,9 +3096,8 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     a.nlist = ndata;
     // k_level_check also plans the next epoch's statuses (grid-strided copy of
     // the initial statuses into the other array)
-    const bool plan_next = ndata > 0 && !getenv_flag("PQG_NO_STATUS_PLAN");
     a.status_next = plan_next ? B->d_status + ((a.epoch + 1) & 1) * npages : nullptr;
-    e |= pq_launch(5, &a, s);
+    if (!skip_check) e |= pq_launch(5, &a, s);
     if (plan_next && !e) B->st_ready[(a.epoch + 1) & 1] = true;
     mark(false);
   }

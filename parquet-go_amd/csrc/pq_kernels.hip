@@ -5187,6 +5187,10 @@ template <int WIDTH>
 __global__ __launch_bounds__(LD_WAVES_H * 64) void k_expand_mix(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
   STAMP(0);
+  // (batches without k_level_check: the next decode's statuses, as it would)
+  if (a.status_next)
+    for (int i = blockIdx.x * (LD_WAVES_H * 64) + threadIdx.x; i < a.npages; i += gridDim.x * (LD_WAVES_H * 64))
+      a.status_next[i] = a.status0[i];
   const LdsGroup g = sload(a.lgroups + blockIdx.x);
   if (g.dpage < 0) mix_global<WIDTH>(a, g, lds_dyn);
   else mix_lds<WIDTH>(a, g, lds_dyn);
