@@ -73,6 +73,9 @@ struct PageDesc {
   int32_t job_base;      // tiled page: first entry of its job -> position table (page_jobs)
   int16_t alias_any;     // dictionary page: k_snappy may alias it at any alignment (LDS-group chunks)
   int16_t srec;          // tiled PLAIN page whose k_expand records the host wrote (no k_prepare work)
+  int16_t lvl_bits;      // flat page (max_rep 0, no level output): its level scratch holds a bit per
+                         // level (def == max_def), LSB first from the scratch's first word, not a byte
+  int16_t pad_lb[3];
   int64_t lens_base;     // BYTE_ARRAY page scratch, 2 x num_values int32 (-1: none): DELTA_(LENGTH_)BYTE_ARRAY
                          // suffix / prefix lengths; PLAIN (offset, length) per value from k_prepare's walk
   int32_t sidx;          // index in the Snappy page list (-1: not decoded by k_snappy)

@@ -557,8 +557,10 @@ struct HybT {
   // bit-packed values [lo, hi) of the run whose value 0 is at stream bit b0
   // (lo, hi relative to the run), counted: == A into cA, >= B into cB; with
   // dst (the run's value 0), each stored as a byte
+  // (with bits: bit vb + j of the bitmap set for each value j == A; the
+  // bitmap is zeroed beforehand, its words shared with neighbouring runs)
   __device__ __forceinline__ void count_packed(int64_t b0, int64_t lo, int64_t hi, uint32_t A, uint32_t B, int64_t &cA,
-                                               int64_t &cB, uint8_t *dst) {
+                                               int64_t &cB, uint8_t *dst, uint32_t *bits = nullptr, int64_t vb = 0) {
     const int lane = lane_id();
     for (int64_t j0 = lo; j0 < hi; j0 += 64) {
       const int64_t j = j0 + lane;
@@ -568,9 +570,29 @@ struct HybT {
       const int64_t blo = (b0 + j0 * bw) >> 3, bhi = ((b0 + (last + 1) * bw + 7) >> 3) + 8;
       if (window_covers(blo, bhi)) v = win_unpack(b0 + (in ? j : j0) * bw);
       else v = in ? unpack_u32(p, len, b0 + j * bw, bw) : 0u;
-      cA += __popcll(ballot(in && v == A));
+      const uint64_t ma = ballot(in && v == A);
+      cA += __popcll(ma);
       cB += __popcll(ballot(in && v >= B));
       if (dst && in) dst[j] = (uint8_t)v;
+      if (bits && ma && lane < 3) {  // up to three words: lane q ORs the q-th
+        const int64_t bi = vb + j0;
+        const uint32_t sh = (uint32_t)(bi & 31);
+        const uint64_t lo64 = ma << sh;                        // bits [0, 64) of the span from word bi >> 5
+        const uint32_t hi32 = sh ? (uint32_t)(ma >> (64 - sh)) : 0u;  // bits [64, 96)
+        const uint32_t part = lane == 0 ? (uint32_t)lo64 : lane == 1 ? (uint32_t)(lo64 >> 32) : hi32;
+        if (part) atomicOr(&bits[(bi >> 5) + lane], part);
+      }
+    }
+  }
+  // bits [lo, hi) of a zeroed bitmap set (an RLE run of the counted value)
+  __device__ __forceinline__ static void bits_range(uint32_t *bits, int64_t lo, int64_t hi) {
+    if (hi <= lo) return;
+    for (int64_t w = (lo >> 5) + lane_id(); w <= ((hi - 1) >> 5); w += 64) {
+      const int64_t b0 = w * 32;
+      const int l = (int)(max(lo, b0) - b0), h = (int)(min(hi, b0 + 32) - b0);
+      const uint32_t mask = h - l == 32 ? 0xffffffffu : (((1u << (h - l)) - 1u) << l);
+      if (mask == 0xffffffffu) bits[w] = mask;
+      else atomicOr(&bits[w], mask);
     }
   }
   // RLE value v for values [lo, hi) of dst
@@ -590,13 +612,17 @@ struct HybT {
   // (cB): the count path of k_prepare, no value leaves the run table (RLE
   // runs count whole).  Errors as next4 would report reading them.  With
   // dst, value i (since init) is also stored at dst[i] (one byte).
-  __device__ uint32_t count2(int64_t n, uint32_t A, uint32_t B, int64_t &cA, int64_t &cB, uint8_t *dst = nullptr) {
+  // With bits (instead of dst), value i is bit i of a zeroed bitmap: set when
+  // it equals A (flat pages: def == max_def, all k_decode needs).
+  __device__ uint32_t count2(int64_t n, uint32_t A, uint32_t B, int64_t &cA, int64_t &cB, uint8_t *dst = nullptr,
+                             uint32_t *bits = nullptr) {
     const int lane = lane_id();
     if (n <= 0) return E_OK;
     if (bw == 0) {  // all zeros
       cA += A == 0 ? n : 0;
       cB += B == 0 ? n : 0;
       if (dst) fill_run(dst, vdone, vdone + n, 0u);
+      if (bits && A == 0) bits_range(bits, vdone, vdone + n);
       vdone += n;
       return E_OK;
     }
@@ -610,6 +636,42 @@ struct HybT {
           const int32_t nxt = (int32_t)shfl32((uint32_t)tr_s, lane + 1 < 64 ? lane + 1 : 63);
           const int32_t e = lane + 1 < t_n ? nxt : (int32_t)(t_end - t_base);
           const bool mine = lane < t_n;
+          if (bits) {
+            // every value by its own lane as below (4 a lane), a nibble a lane,
+            // words assembled over 8 lanes; lanes start at a 32-value boundary
+            int32_t la = 0, lb = 0;
+            const int32_t a0 = rel0 - (int32_t)((t_base + rel0) & 31);
+            for (int32_t q0 = a0; q0 < rel1; q0 += 256) {
+              const int32_t q = q0 + 4 * lane;
+              uint32_t v4[4];
+              table_value4(q < rel0 ? rel0 : (q < rel1 ? q : rel0), v4);  // every lane takes part
+              uint32_t nib = 0;
+#pragma unroll
+              for (int i = 0; i < 4; i++) {
+                const bool in = q + i >= rel0 && q + i < rel1;
+                const int k = q < rel0 ? q + i - rel0 : i;
+                const uint32_t v = k >= 0 && k < 4 ? v4[k] : 0u;
+                la += in && v == A;
+                lb += in && v >= B;
+                nib |= (in && v == A ? 1u : 0u) << i;
+              }
+              uint32_t word = nib << (4 * (lane & 7));
+              word |= __shfl_xor(word, 1);
+              word |= __shfl_xor(word, 2);
+              word |= __shfl_xor(word, 4);
+              const int32_t g0 = q0 + 32 * (lane >> 3);  // the group's first value
+              if ((lane & 7) == 0 && g0 < rel1 && g0 + 32 > rel0) {
+                uint32_t *wp = bits + ((t_base + g0) >> 5);
+                if (g0 >= rel0 && g0 + 32 <= rel1) *wp = word;
+                else if (word) atomicOr(wp, word);
+              }
+            }
+            cA += wave_sum32(la);
+            cB += wave_sum32(lb);
+            vdone += take;
+            left -= take;
+            continue;
+          }
           if (dst && !lvl_serial_fill()) {
             // every value of the table's part by its own lane (run found by
             // a binary search over the lanes' run starts, table_value), one
@@ -703,9 +765,10 @@ struct HybT {
         cA += rle_val == A ? take : 0;
         cB += rle_val >= B ? take : 0;
         if (dst) fill_run(dst, vdone, vdone + take, rle_val);
+        if (bits && rle_val == A) bits_range(bits, vdone, vdone + take);
       } else {
         const int ok = readable((int)min<int64_t>(take, 1 << 30));
-        count_packed(data * 8, vi, vi + ok, A, B, cA, cB, dst ? dst + vdone - vi : nullptr);
+        count_packed(data * 8, vi, vi + ok, A, B, cA, cB, dst ? dst + vdone - vi : nullptr, bits, vdone - vi);
         if (ok < take) {
           vdone += ok;
           return E_EOF;

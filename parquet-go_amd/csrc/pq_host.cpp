@@ -1745,7 +1745,14 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
       // counts k_prepare needs, for k_prepare and k_decode
       if (L.max_def > 0 && L.max_def < 256 && d.num_values > 0) {
         B->pages.back().lvl_base = B->lvl_bytes;
-        B->lvl_bytes += (((int64_t)(L.max_rep > 0 ? 2 : 1) * d.num_values) + 15) & ~(int64_t)15;
+        // flat pages without level output: a bit per level (k_decode needs only
+        // def == max_def), an eighth of the scratch traffic (C3's nullable doubles)
+        static const bool bits_off = getenv_flag("PQG_LEVEL_BYTES");
+        B->pages.back().lvl_bits = (int16_t)(L.max_rep == 0 && !(B->flags & PQG_BATCH_LEVELS) && !bits_off);
+        // (bits: the bitmap and one word after it)
+        B->lvl_bytes += B->pages.back().lvl_bits
+                            ? ((((int64_t)d.num_values + 7) >> 3) + 8 + 15) & ~(int64_t)15
+                            : (((int64_t)(L.max_rep > 0 ? 2 : 1) * d.num_values) + 15) & ~(int64_t)15;
         if (d.kind != PAGE_V2 || d.dict >= 0) B->lvl_late = true;
       }
       if ((L.physical_type == T_BYTE_ARRAY && (d.enc == ENC_DELTA_LBA || d.enc == ENC_DELTA_BA)) ||

@@ -3378,7 +3378,17 @@ __device__ __forceinline__ void levels_page(const KArgs &a, int gi, int part) {
   def.init(ps.lvl + ps.def_off, ps.def_len, bits_len(c.max_def));
   int64_t slots = 0, nn = 0;
   if (c.max_rep > 0) lv += n;
-  e = def.count2(n, (uint32_t)c.max_def, c.max_rep > 0 ? (uint32_t)c.rep_def : 0u, nn, slots, lv);
+  if (d.lvl_bits) {
+    // flat page without level output: bit i = (def level i == max_def), all
+    // k_decode reads — an eighth of the byte scratch; the bitmap (and the word
+    // after it, read by k_decode's two-word loads) zeroed first, set by OR
+    uint32_t *bw = (uint32_t *)lv;
+    for (int w = lane; w <= ((n + 31) >> 5); w += 64) bw[w] = 0u;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    e = def.count2(n, (uint32_t)c.max_def, 0u, nn, slots, nullptr, bw);
+  } else {
+    e = def.count2(n, (uint32_t)c.max_def, c.max_rep > 0 ? (uint32_t)c.rep_def : 0u, nn, slots, lv);
+  }
   if (e) {
     set_status(a.status, page, ST_DEF, e);
     return;
@@ -3862,7 +3872,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   while (e0 < e_end) {
     const int cnt = (int)min<int64_t>(n - e0, flat ? 256 - ((slot_base + e0) & 255) : 256);
     uint32_t r[4] = {0, 0, 0, 0}, dl[4] = {0, 0, 0, 0};
-    if (d.lvl_base >= 0) {  // decoded (and checked) by k_prepare's level walk
+    if (d.lvl_bits) {  // k_levels' bitmap (flat): def == max_def or not
+      const uint32_t *lw = (const uint32_t *)(a.lvl + d.lvl_base);
+      const int64_t b = e0 + 4 * lane;
+      const uint64_t two = 4 * lane < cnt ? (uint64_t)lw[b >> 5] | ((uint64_t)lw[(b >> 5) + 1] << 32) : 0ull;
+      const uint32_t nib = (uint32_t)(two >> (b & 31)) & 15u;
+#pragma unroll
+      for (int k = 0; k < 4; k++) dl[k] = 4 * lane + k < cnt && ((nib >> k) & 1u) ? (uint32_t)c.max_def : 0u;
+    } else if (d.lvl_base >= 0) {  // decoded (and checked) by k_prepare's level walk
       const uint8_t *lr = a.lvl + d.lvl_base + e0, *ld = lr + (c.max_rep > 0 ? (int64_t)n : 0);
 #pragma unroll
       for (int k = 0; k < 4; k++) {
@@ -5283,7 +5300,10 @@ __global__ __launch_bounds__(256) void k_dba(KArgs a) {
     const uint8_t *pv = vout;
     for (int64_t e0 = 0; e0 < nvp && i < nn; e0 += 64) {
       const int cnt = (int)min<int64_t>(64, nvp - e0);
-      const int dl = lane < cnt ? (ld ? (int)ld[e0 + lane] : c.max_def) : -1;
+      const int dl = lane >= cnt ? -1
+                     : d.lvl_bits ? ((((const uint32_t *)ld)[(e0 + lane) >> 5] >> ((e0 + lane) & 31)) & 1u ? c.max_def : 0)
+                     : ld ? (int)ld[e0 + lane]
+                          : c.max_def;
       const uint64_t vm = ballot(lane < cnt && dl == c.max_def);
       const uint64_t sm = ballot(lane < cnt && (flat || dl >= c.rep_def));
       const uint32_t my_slot = (uint32_t)__builtin_popcountll(sm & ((1ull << lane) - 1));  // within the 64
