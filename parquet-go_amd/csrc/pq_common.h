@@ -47,6 +47,12 @@ enum : uint32_t {
   ST_REDO = 0x7FFF,
 };
 __host__ __device__ inline uint32_t make_status(uint32_t stage, uint32_t code) { return (stage << 16) | code; }
+// device-internal code bit: a key-stream header error found by the run walk
+// (k_prepare) is set at once with this bit, so that a dictionary-index error
+// k_expand finds among the values before it (same stage, plain code) wins the
+// atomicMin; the host masks it off (STATUS_CODE)
+constexpr uint32_t E_LATE = 0x4000u;
+constexpr uint32_t STATUS_CODE = 0x3fffu;
 constexpr uint32_t STATUS_OK = 0xFFFFFFFFu;
 
 struct PageDesc {
@@ -75,7 +81,9 @@ struct PageDesc {
   int16_t srec;          // tiled PLAIN page whose k_expand records the host wrote (no k_prepare work)
   int16_t lvl_bits;      // flat page (max_rep 0, no level output): its level scratch holds a bit per
                          // level (def == max_def), LSB first from the scratch's first word, not a byte
-  int16_t pad_lb[3];
+  int16_t pad_lb;
+  int32_t part0;         // list page split into k_decode<3> parts: index of its first part (-1: none);
+                         // k_levels counts its streams part by part into KArgs::part_pre
   int64_t lens_base;     // BYTE_ARRAY page scratch, 2 x num_values int32 (-1: none): DELTA_(LENGTH_)BYTE_ARRAY
                          // suffix / prefix lengths; PLAIN (offset, length) per value from k_prepare's walk
   int32_t sidx;          // index in the Snappy page list (-1: not decoded by k_snappy)

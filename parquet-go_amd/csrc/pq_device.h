@@ -559,6 +559,7 @@ struct HybT {
   // dst (the run's value 0), each stored as a byte
   // (with bits: bit vb + j of the bitmap set for each value j == A; the
   // bitmap is zeroed beforehand, its words shared with neighbouring runs)
+  template <bool BITS = false>
   __device__ __forceinline__ void count_packed(int64_t b0, int64_t lo, int64_t hi, uint32_t A, uint32_t B, int64_t &cA,
                                                int64_t &cB, uint8_t *dst, uint32_t *bits = nullptr, int64_t vb = 0) {
     const int lane = lane_id();
@@ -574,7 +575,7 @@ struct HybT {
       cA += __popcll(ma);
       cB += __popcll(ballot(in && v >= B));
       if (dst && in) dst[j] = (uint8_t)v;
-      if (bits && ma && lane < 3) {  // up to three words: lane q ORs the q-th
+      if (BITS && ma && lane < 3) {  // up to three words: lane q ORs the q-th
         const int64_t bi = vb + j0;
         const uint32_t sh = (uint32_t)(bi & 31);
         const uint64_t lo64 = ma << sh;                        // bits [0, 64) of the span from word bi >> 5
@@ -614,6 +615,7 @@ struct HybT {
   // dst, value i (since init) is also stored at dst[i] (one byte).
   // With bits (instead of dst), value i is bit i of a zeroed bitmap: set when
   // it equals A (flat pages: def == max_def, all k_decode needs).
+  template <bool BITS = false>
   __device__ uint32_t count2(int64_t n, uint32_t A, uint32_t B, int64_t &cA, int64_t &cB, uint8_t *dst = nullptr,
                              uint32_t *bits = nullptr) {
     const int lane = lane_id();
@@ -622,7 +624,7 @@ struct HybT {
       cA += A == 0 ? n : 0;
       cB += B == 0 ? n : 0;
       if (dst) fill_run(dst, vdone, vdone + n, 0u);
-      if (bits && A == 0) bits_range(bits, vdone, vdone + n);
+      if (BITS && A == 0) bits_range(bits, vdone, vdone + n);
       vdone += n;
       return E_OK;
     }
@@ -636,7 +638,7 @@ struct HybT {
           const int32_t nxt = (int32_t)shfl32((uint32_t)tr_s, lane + 1 < 64 ? lane + 1 : 63);
           const int32_t e = lane + 1 < t_n ? nxt : (int32_t)(t_end - t_base);
           const bool mine = lane < t_n;
-          if (bits) {
+          if (BITS) {
             // every value by its own lane as below (4 a lane), a nibble a lane,
             // words assembled over 8 lanes; lanes start at a 32-value boundary
             int32_t la = 0, lb = 0;
@@ -765,10 +767,10 @@ struct HybT {
         cA += rle_val == A ? take : 0;
         cB += rle_val >= B ? take : 0;
         if (dst) fill_run(dst, vdone, vdone + take, rle_val);
-        if (bits && rle_val == A) bits_range(bits, vdone, vdone + take);
+        if (BITS && rle_val == A) bits_range(bits, vdone, vdone + take);
       } else {
         const int ok = readable((int)min<int64_t>(take, 1 << 30));
-        count_packed(data * 8, vi, vi + ok, A, B, cA, cB, dst ? dst + vdone - vi : nullptr, bits, vdone - vi);
+        count_packed<BITS>(data * 8, vi, vi + ok, A, B, cA, cB, dst ? dst + vdone - vi : nullptr, bits, vdone - vi);
         if (ok < take) {
           vdone += ok;
           return E_EOF;

@@ -95,6 +95,8 @@ struct pq_launch_args {
   int32_t nhjobs;
   int32_t grid_cap;  // k_levels<-1>: at most this many workgroups (grid-stride loop)
   int32_t snappy_wg;  // Snappy items by k_snappy_wg (workgroup per page, 64 KiB LDS history) instead of k_snappy
+  const int32_t *part_tab;  // the list-page parts (page, first level, end level), for k_levels
+  int32_t *part_pre;        // per part: rows, slots, values before its first level (k_levels -> k_decode<3>)
   uint32_t *status_next;
   const void *sw_pages;
   void *sw_regs;
@@ -767,6 +769,7 @@ struct pqg_batch {
   uint64_t *d_dict = nullptr;
   int32_t *d_lists = nullptr;
   int32_t *d_parts = nullptr;  // nest_parts on the device
+  int32_t *d_part_pre = nullptr;  // per part: counts before it (k_levels -> k_decode<3>)
   void *d_jobs = nullptr;        // deferred long-literal copy jobs (k_snappy -> k_copy)
   uint32_t *d_njobs = nullptr;   // per Snappy page: jobs written
   int32_t *d_job_base = nullptr, *d_job_owner = nullptr;
@@ -822,6 +825,7 @@ struct pqg_batch {
   bool ready_final = false;    // `ready` recorded after every set-up copy (else copies may be in flight)
   bool counted = false;        // the last launch was the counting pass (the next decode resumes from it)
   bool all_srec = false;  // every data page has host-written records: no k_prepare work
+  bool no_levels = false;  // no data page has level streams (every selected column required, flat)
   int lane = 0;  // decode lane of the context (pqg_stream: alternate slices)
   std::vector<ExRec> recs_host;  // tiled PLAIN pages' static k_expand records (upload source)
   std::vector<uint8_t> tab_host;  // the small tables (d_pages, d_info, d_lists, ...): host image, uploaded at
@@ -1591,6 +1595,7 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
     d.job_base = -1;  // not a tiled page
     d.lens_base = -1;
     d.lvl_base = -1;
+    d.part0 = -1;
     d.sidx = -1;
     d.swalk = -1;
     d.col = ci;
@@ -2396,6 +2401,11 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   }
   B->all_srec = !B->data_list.empty();
   for (int32_t pi : B->data_list) B->all_srec &= B->pages[(size_t)pi].srec != 0;
+  B->no_levels = !B->data_list.empty();
+  for (int32_t pi : B->data_list) {
+    const auto &ci = B->cols[(size_t)B->pages[(size_t)pi].col].info;
+    B->no_levels &= ci.max_def == 0 && ci.max_rep == 0;
+  }
   phase("plan");
   // tables
   std::vector<std::pair<void **, size_t>> tab_fix;
@@ -2429,24 +2439,28 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   B->ngen_nest = (int32_t)B->general_nest.size();
   {
     // list pages split into parts of whole 256-entry steps, one k_decode<3>
-    // wave each, up to about a wave per SIMD (1,024) for the batch: a batch
-    // of few list pages (a stream slice) otherwise leaves most SIMDs idle.
-    // Past that it does not pay: C4 (1,012 pages) in 4,096 parts took as long
-    // (2.27 vs 2.30 ms), its waves are issue-bound, not chain-bound.  A part
-    // counts what comes before it from the level bytes and seeks the key
+    // wave each: ~4,096 entries a part (at least 1/16,384 of the batch's
+    // entries).  A part starts from the counts k_levels recorded for it
+    // (rows, slots, values before it: PageDesc::part0) and seeks the key
     // stream, so only pages with level scratch and PLAIN / RLE_DICTIONARY
-    // values are split.  PQG_NEST_PART: entries per part (0: whole pages).
+    // values are split.  C4 step (ms) by entries a part: whole pages 4.04,
+    // 16,384 3.81, 4,096 3.56, 2,048 3.73, 1,024 3.84 — more waves than two a
+    // SIMD (k_decode<3>'s occupancy) only queue.  PQG_NEST_PART: entries per
+    // part (0: whole pages).
     int64_t tot = 0;
     for (int32_t pg : B->general_nest) tot += std::max(B->pages[(size_t)pg].num_values, 0);
     const int64_t env_part = getenv("PQG_NEST_PART") ? atoll(getenv("PQG_NEST_PART")) : -1;
-    int64_t plen = env_part >= 0 ? env_part : std::max<int64_t>(8192, (tot / 1024 + 255) & ~(int64_t)255);
+    int64_t plen = env_part >= 0 ? env_part : std::max<int64_t>(4096, (tot / 16384 + 255) & ~(int64_t)255);
     if (plen > 0) plen = (plen + 255) & ~(int64_t)255;
     B->nest_parts.clear();
+    static const bool part_rescan = getenv_flag("PQG_PART_RESCAN");  // (analysis: parts count their own prefix)
     for (int32_t pg : B->general_nest) {
       const PageDesc &pd = B->pages[(size_t)pg];
       const int64_t n = std::max(pd.num_values, 0);
       const int64_t np = plen > 0 && pd.lvl_base >= 0 && (pd.enc == ENC_RLE_DICT || pd.enc == ENC_PLAIN) ? n / plen : 1;
       const int64_t step = np > 1 ? ((n + np - 1) / np + 255) & ~(int64_t)255 : std::max<int64_t>(n, 1);
+      // (parts after the first start from k_levels' counts: PageDesc::part0)
+      if (np > 1 && !part_rescan) B->pages[(size_t)pg].part0 = (int32_t)(B->nest_parts.size() / 3);
       for (int64_t e = 0; e < n || e == 0; e += step) {
         B->nest_parts.push_back(pg);
         B->nest_parts.push_back((int32_t)e);
@@ -2482,6 +2496,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     tab.put((void **)&B->d_status0, B->status0.data(), sizeof(uint32_t) * npages);
     tab.put((void **)&B->d_lists, lists.data(), sizeof(int32_t) * lists.size());
     tab.put((void **)&B->d_parts, B->nest_parts.data(), sizeof(int32_t) * B->nest_parts.size());
+    tab.put((void **)&B->d_part_pre, nullptr, sizeof(int32_t) * 4 * (B->nest_parts.size() / 3 + 1));
     tab.put((void **)&B->d_lgroups, B->lgroups.data(), sizeof(LdsGroup) * (B->lgroups.size() + 1));
     tab.put((void **)&B->d_page_jobs, pj.data(), sizeof(int32_t) * pj.size());
     tab.put((void **)&B->d_sitems, B->snap_items.data(), 4 * B->snap_items.size());
@@ -2794,6 +2809,8 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.copy_idx = B->d_copy_idx;
   a.lens = B->d_lens;
   a.lvl = B->d_lvl;
+  a.part_tab = B->d_parts;
+  a.part_pre = B->d_part_pre;
   a.status0 = B->d_status0;
   a.zr = B->d_zr;
   a.nzr = upto_scan ? 0 : B->nzr;  // the bitmaps are written by the decode kernels only
@@ -2891,7 +2908,6 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     // GPU on their own — beside the whole data pages.  Only the whole data
     // pages defer literals to k_copy (after the join).
     const int32_t nall = (int32_t)(B->snap_items.size() / 2), nwhole = B->n_whole_items, ndict = B->n_dict_items;
-    pqg_ctx *ctx = B->ctx;
     // without segmented pages or string dictionaries to prepare, the whole
     // data pages and the dictionary pages are one launch on the context
     // stream (items [0, nwhole + ndict) are contiguous): the fork / join
@@ -3014,7 +3030,6 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     // the three k_decode instances run side by side: <1> and <2> on side
     // streams forked here, joined before anything reads their output
     const int32_t ng0 = ngen - B->ngen_flat - B->ngen_str - B->ngen_nest;
-    pqg_ctx *ctx = B->ctx;
     const int32_t npstr = (int32_t)(B->pstr_items.size() / 2);
     const bool str_side = B->ngen_str > 0 || npstr > 0;
     const bool fork = B->ngen_flat > 0 || str_side || B->ngen_nest > 0;
@@ -3085,7 +3100,10 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     // to find: k_expand_mix plans the next decode's statuses and the launch is
     // skipped (C1; PQG_LEVEL_CHECK=1 keeps it)
     const bool plan_next = ndata > 0 && !getenv_flag("PQG_NO_STATUS_PLAN");
-    const bool skip_check = B->all_srec && ngen == 0 && B->dba_list.empty() && !getenv_flag("PQG_LEVEL_CHECK");
+    // (likewise a batch without level streams: the run walk sets its own
+    // errors, k_level_check would only re-walk levels — C2)
+    const bool skip_check = ((B->all_srec && ngen == 0 && B->dba_list.empty()) || B->no_levels) &&
+                            B->ldn[0] + B->ldn[1] > 0 && !getenv_flag("PQG_LEVEL_CHECK");
     if (skip_check && plan_next) {
       pq_launch_args ax = a;
       ax.status_next = B->d_status + ((a.epoch + 1) & 1) * npages;
@@ -3172,7 +3190,7 @@ int pqg_batch_sync(pqg_batch *B) {
   for (size_t i = 0; i < npages; i++) {
     if (st[i] == STATUS_OK) continue;
     const PageDesc &d = B->pages[i];
-    uint32_t stage = st[i] >> 16, code = st[i] & 0xffff;
+    uint32_t stage = st[i] >> 16, code = st[i] & STATUS_CODE;
     consider({d.rg, B->cols[(size_t)d.col].leaf, stage >= ST_PHASE2 ? 1 : 0, d.ord, stage, code});
   }
   for (auto &ce : B->chunk_errors) consider({ce.rg, ce.leaf, 0, ce.ord, ce.stage, ce.code});
@@ -3549,6 +3567,7 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
   if (!rc) {
     PageDesc d;
     memset(&d, 0, sizeof(d));
+    d.part0 = -1;
     d.kind = PAGE_DICT;
     d.comp_len = (int32_t)n;
     d.body_len = (int32_t)expect;

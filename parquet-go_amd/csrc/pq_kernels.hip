@@ -100,6 +100,8 @@ struct KArgs {
   uint32_t *seg_flag;     // per Snappy-list position: 0 segments ok, 1 serial fallback, 2 nothing to do
   const int32_t *parts;   // k_decode<3>: (page, first level, end level) per wave, instead of `list`
   int32_t redo;           // k_decode<3>: the pages left at ST_REDO by their parts, decoded whole
+  const int32_t *part_tab;  // list-page parts (as `parts`), for k_levels
+  int32_t *part_pre;        // per part: rows, slots, values before it (4 ints; PageDesc::part0)
 };
 
 #ifdef PQ_STAMPS
@@ -2764,6 +2766,12 @@ struct RunBuf {
 // sum of their lengths.  Anything unusual (multi-byte header, an error, the
 // end of the stream) is left to the exact serial step below.
 constexpr uint32_t NX_STOP = 0xFFFFu;
+#ifndef PQ_DEC_DICT_LDS
+#define PQ_DEC_DICT_LDS 8192  // k_decode<3> / <2>: dictionaries (<2>: entry tables) up to this many bytes gathered from LDS (0: off)
+#endif
+#ifndef PQ_LV_AHEAD
+#define PQ_LV_AHEAD 1  // k_decode: a step's level scratch loaded one step ahead (0: when the step starts)
+#endif
 
 __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const uint8_t *ks, int64_t slen,
                           int32_t n, int bw, uint8_t *lbytes, uint16_t *lnx, const uint8_t *dict, uint32_t dict_n) {
@@ -2997,6 +3005,7 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
     pi->walk_err = err;
     pi->pad = nr;
   }
+  if (err) set_status(a.status, (int)(pi - a.info), ST_VALUES, err | E_LATE);
   // k_expand records, lane k = job k (read back this wave's own tile stores)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int32_t njobs = (n + EX_WAVE_VALUES - 1) / EX_WAVE_VALUES;
@@ -3362,11 +3371,24 @@ __device__ __forceinline__ void levels_page(const KArgs &a, int gi, int part) {
   }
   const int n = d.num_values;
   uint8_t *lv = a.lvl + d.lvl_base;
+  // a list page split into k_decode<3> parts: the streams are counted part by
+  // part and the counts before each part kept for it (no rescan of the levels)
+  const bool pre = d.part0 >= 0 && a.part_pre != nullptr;
   if (part != 1 && c.max_rep > 0) {
     Hyb rep;
     rep.init(ps.lvl + ps.rep_off, ps.rep_len, bits_len(c.max_rep));
     int64_t rows = 0, unused = 0;
-    e = rep.count2(n, 0u, 0xffffffffu, rows, unused, lv);
+    if (pre) {
+      e = E_OK;
+      for (int k = d.part0, done = 0; done < n && !e; k++) {
+        if (lane == 0) a.part_pre[4 * k] = (int32_t)rows;
+        const int hi = ufirst(a.part_tab[3 * k + 2]);
+        e = rep.count2(hi - done, 0u, 0xffffffffu, rows, unused, lv);
+        done = hi;
+      }
+    } else {
+      e = rep.count2(n, 0u, 0xffffffffu, rows, unused, lv);
+    }
     if (e) {
       set_status(a.status, page, ST_REP, e);
       return;
@@ -3385,7 +3407,18 @@ __device__ __forceinline__ void levels_page(const KArgs &a, int gi, int part) {
     uint32_t *bw = (uint32_t *)lv;
     for (int w = lane; w <= ((n + 31) >> 5); w += 64) bw[w] = 0u;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    e = def.count2(n, (uint32_t)c.max_def, 0u, nn, slots, nullptr, bw);
+    e = def.template count2<true>(n, (uint32_t)c.max_def, 0u, nn, slots, nullptr, bw);
+  } else if (pre) {
+    e = E_OK;
+    for (int k = d.part0, done = 0; done < n && !e; k++) {
+      if (lane == 0) {
+        a.part_pre[4 * k + 1] = (int32_t)slots;
+        a.part_pre[4 * k + 2] = (int32_t)nn;
+      }
+      const int hi = ufirst(a.part_tab[3 * k + 2]);
+      e = def.count2(hi - done, (uint32_t)c.max_def, c.max_rep > 0 ? (uint32_t)c.rep_def : 0u, nn, slots, lv);
+      done = hi;
+    }
   } else {
     e = def.count2(n, (uint32_t)c.max_def, c.max_rep > 0 ? (uint32_t)c.rep_def : 0u, nn, slots, lv);
   }
@@ -3407,8 +3440,11 @@ __device__ __forceinline__ void levels_page(const KArgs &a, int gi, int part) {
 // both in turn.  Workgroups loop over the pages with a grid stride
 // (PQG_LEVELS_CAP: a capped grid for the launch beside the Snappy phase;
 // measured slower, so the full grid is the default)
+#ifndef PQ_LEVELS_WPE
+#define PQ_LEVELS_WPE 4  // k_levels: registers capped for 4 waves a SIMD (the bitmap path took it to 141 VGPRs)
+#endif
 template <int MODE, bool SPLIT>
-__global__ __launch_bounds__(256) void k_levels(KArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PQ_LEVELS_WPE))) void k_levels(KArgs a) {
   const int wv = (int)ufirst(threadIdx.x >> 6);
   const int part = SPLIT ? (wv & 1) : 2;  // 0: repetition levels, 1: definition levels, 2: both
   for (uint32_t b = blockIdx.x;; b += gridDim.x) {
@@ -3821,6 +3857,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   BaLds &bl = ba_all[threadIdx.x >> 6];
   __shared__ uint32_t bmw_all[4][12];  // nested-column bitmap words of a step
   uint32_t *bmw = bmw_all[threadIdx.x >> 6];
+  // lists of 4/8-byte dictionary values (KIND 3): a dictionary of up to
+  // DEC_DICT_LDS bytes is copied into the wave's LDS once, and the step's
+  // gathers read it there instead of from L2 (one dependent global round trip
+  // less a step; C4's 2,001-entry INT32 dictionaries)
+  // (KIND 2, dictionary strings: the entries' (offset, length) pairs)
+  constexpr int DLW = (KIND == 3 || KIND == 2) && PQ_DEC_DICT_LDS >= 8 ? PQ_DEC_DICT_LDS / 4 : 1;
+  __shared__ uint32_t dlds_all[4][DLW];
+  uint32_t *dlds = dlds_all[threadIdx.x >> 6];
+  const int64_t dlb = KIND == 2 ? dict_n * 8 : dict_n * (int64_t)w;  // bytes staged
+  const bool dict_lds = (KIND == 3 || KIND == 2) && DLW > 1 && dp && d.enc == ENC_RLE_DICT &&
+                        (KIND == 2 || w == 4 || w == 8) && dlb <= (int64_t)DLW * 4;
+  if (dict_lds) {
+    const int nw = (int)((dlb + 3) >> 2);
+    if (KIND == 2) {
+      const uint32_t *ent = (const uint32_t *)(a.dict_ent + dict_base);
+      for (int i = lane; i < nw; i += 64) dlds[i] = ent[i];
+    } else {
+      for (int i = lane; i < nw; i += 64) dlds[i] = load_u32_unaligned(dict_vals + 4 * (int64_t)i);
+    }
+    wave_lds_sync();
+  }
   int64_t spos = 0;
   // DELTA strings: lengths decoded and validated by k_prepare (scratch); suffix
   // bytes start at str_data.  DELTA_BYTE_ARRAY bytes are written by k_dba.
@@ -3835,7 +3892,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   int64_t e0 = 0, slot_run = 0, row_run = 0, nn_run = 0, str_run = pi.str_base;
   uint32_t err = E_OK, err_stage = 0;
   const int64_t e_end = part ? min<int64_t>(e_hi, (int64_t)n) : (int64_t)n;
-  if (part && e_lo > 0) {
+  if (part && e_lo > 0 && d.part0 >= 0) {
+    // rows (rep 0), slots (def >= rep_def) and values (def == max_def) before
+    // the part: counted by k_levels
+    row_run = ufirst(a.part_pre[4 * gi]);
+    slot_run = ufirst(a.part_pre[4 * gi + 1]);
+    nn_run = ufirst(a.part_pre[4 * gi + 2]);
+    e0 = e_lo;
+    if (d.enc == ENC_RLE_DICT && keys.skip(nn_run) != E_OK) {
+      set_status(a.status, page, ST_REDO, 0);
+      return;
+    }
+  } else if (part && e_lo > 0) {
     // rows (rep 0), slots (def >= rep_def) and values (def == max_def) of the
     // entries before the part: 16 level bytes of each stream a lane a pass
     const uint8_t *lr = a.lvl + d.lvl_base, *ld = lr + n;
@@ -3869,25 +3937,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
     }
   }
 
-  while (e0 < e_end) {
-    const int cnt = (int)min<int64_t>(n - e0, flat ? 256 - ((slot_base + e0) & 255) : 256);
-    uint32_t r[4] = {0, 0, 0, 0}, dl[4] = {0, 0, 0, 0};
-    if (d.lvl_bits) {  // k_levels' bitmap (flat): def == max_def or not
+  // the level scratch of the step at e: its 4 entries of this lane, packed —
+  // bitmap: the def == max_def bits; bytes: rep bytes (low word), def bytes.
+  // Loaded a step ahead (PQ_LV_AHEAD): the next step's level loads are in
+  // flight beside this step's key / dictionary / value loads, so a step waits
+  // on one round trip instead of two
+  auto step_cnt = [&](int64_t e) { return (int)min<int64_t>(n - e, flat ? 256 - ((slot_base + e) & 255) : 256); };
+  auto lv_load = [&](int64_t e) -> uint64_t {
+    if (e >= e_end) return 0;
+    const int ce = step_cnt(e);
+    if (d.lvl_bits) {
       const uint32_t *lw = (const uint32_t *)(a.lvl + d.lvl_base);
-      const int64_t b = e0 + 4 * lane;
-      const uint64_t two = 4 * lane < cnt ? (uint64_t)lw[b >> 5] | ((uint64_t)lw[(b >> 5) + 1] << 32) : 0ull;
-      const uint32_t nib = (uint32_t)(two >> (b & 31)) & 15u;
+      const int64_t b = e + 4 * lane;
+      const uint64_t two = 4 * lane < ce ? (uint64_t)lw[b >> 5] | ((uint64_t)lw[(b >> 5) + 1] << 32) : 0ull;
+      return (two >> (b & 31)) & 15u;
+    }
+    if (d.lvl_base < 0) return 0;
+    const uint8_t *lr = a.lvl + d.lvl_base + e, *ld = lr + (c.max_rep > 0 ? (int64_t)n : 0);
+    uint32_t pr = 0, pd = 0;
 #pragma unroll
-      for (int k = 0; k < 4; k++) dl[k] = 4 * lane + k < cnt && ((nib >> k) & 1u) ? (uint32_t)c.max_def : 0u;
-    } else if (d.lvl_base >= 0) {  // decoded (and checked) by k_prepare's level walk
-      const uint8_t *lr = a.lvl + d.lvl_base + e0, *ld = lr + (c.max_rep > 0 ? (int64_t)n : 0);
+    for (int k = 0; k < 4; k++) {
+      const int j = 4 * lane + k;
+      if (j < ce) {
+        if (!flat) pr |= (uint32_t)lr[j] << (8 * k);
+        pd |= (uint32_t)ld[j] << (8 * k);
+      }
+    }
+    return (uint64_t)pr | ((uint64_t)pd << 32);
+  };
+  uint64_t lv_next = PQ_LV_AHEAD ? lv_load(e0) : 0;
+  while (e0 < e_end) {
+    const int cnt = step_cnt(e0);
+    uint32_t r[4] = {0, 0, 0, 0}, dl[4] = {0, 0, 0, 0};
+    const uint64_t lv = PQ_LV_AHEAD ? lv_next : lv_load(e0);
+    if (PQ_LV_AHEAD) lv_next = lv_load(e0 + cnt);
+    if (d.lvl_bits) {  // k_levels' bitmap (flat): def == max_def or not
+#pragma unroll
+      for (int k = 0; k < 4; k++) dl[k] = 4 * lane + k < cnt && ((lv >> k) & 1u) ? (uint32_t)c.max_def : 0u;
+    } else if (d.lvl_base >= 0) {  // decoded (and checked) by k_levels
 #pragma unroll
       for (int k = 0; k < 4; k++) {
-        const int j = 4 * lane + k;
-        if (j < cnt) {
-          if (!flat) r[k] = lr[j];
-          dl[k] = ld[j];
-        }
+        r[k] = (uint32_t)(lv >> (8 * k)) & 0xffu;
+        dl[k] = (uint32_t)(lv >> (32 + 8 * k)) & 0xffu;
       }
     } else {
       if (!flat) {
@@ -4045,13 +4136,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
         for (int k = 0; k < 4; k++)
           if (valid[k]) {
             if (is_ba) {
-              uint64_t ent = a.dict_ent[dict_base + key[k]];
+              const uint64_t ent = dict_lds ? ((uint64_t)dlds[2 * key[k]] | ((uint64_t)dlds[2 * key[k] + 1] << 32))
+                                            : a.dict_ent[dict_base + key[k]];
               soff[k] = (int64_t)(ent >> 32);
               slen[k] = (int64_t)(ent & 0xffffffffu);
             } else if (w == 4) {
-              v[k] = load_u32_unaligned(dict_vals + (int64_t)key[k] * 4);
+              v[k] = dict_lds ? dlds[key[k]] : load_u32_unaligned(dict_vals + (int64_t)key[k] * 4);
             } else if (w == 8) {
-              v[k] = load_u64_unaligned(dict_vals + (int64_t)key[k] * 8);
+              v[k] = dict_lds ? ((uint64_t)dlds[2 * key[k]] | ((uint64_t)dlds[2 * key[k] + 1] << 32))
+                              : load_u64_unaligned(dict_vals + (int64_t)key[k] * 8);
             } else {
               soff[k] = (int64_t)key[k] * w;
             }
@@ -5451,6 +5544,8 @@ struct pq_launch_args {
   int32_t nhjobs;
   int32_t grid_cap;  // k_levels<-1>: at most this many workgroups (grid-stride loop)
   int32_t snappy_wg;  // Snappy items by k_snappy_wg (workgroup per page, 64 KiB LDS history) instead of k_snappy
+  const int32_t *part_tab;  // the list-page parts (page, first level, end level), for k_levels
+  int32_t *part_pre;        // per part: rows, slots, values before its first level (k_levels -> k_decode<3>)
   uint32_t *status_next;
   const void *sw_pages;
   void *sw_regs;
@@ -5506,6 +5601,8 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   k.lgroups = (const pq::LdsGroup *)p->lgroups;
   k.parts = p->parts;
   k.redo = p->redo;
+  k.part_tab = p->part_tab;
+  k.part_pre = p->part_pre;
   k.hjobs = p->hjobs;
   k.status_next = p->status_next;
   k.sw_pages = (const pq::SwPage *)p->sw_pages;
