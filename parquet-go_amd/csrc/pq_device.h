@@ -198,6 +198,50 @@ __device__ __forceinline__ uint32_t read_uvarint(Win &W, const uint8_t *p, int64
   }
 }
 
+// In-order bitmap writer (wave-uniform state): bits are appended in value
+// order; every word is stored once, whole, when its 32 bits are known (the
+// partial word in `carry` until then), so a level bitmap costs its own size
+// in writes — no zeroing pass, no atomics.
+struct BitOut {
+  uint32_t *g;     // the bitmap
+  int64_t pos;     // bits appended
+  uint32_t carry;  // bits [pos & ~31, pos) of word pos >> 5
+  // append the n <= 64 low bits of b
+  __device__ __forceinline__ void put64(uint64_t b, int n) {
+    if (n <= 0) return;
+    const int sh = (int)(pos & 31);
+    b &= n == 64 ? ~0ull : ((1ull << n) - 1);
+    const uint64_t lo = (uint64_t)carry | (b << sh);
+    const uint32_t hiw = sh ? (uint32_t)(b >> (64 - sh)) : 0u;
+    const int tot = sh + n;
+    const int64_t w = pos >> 5;
+    const int l = lane_id();
+    if ((l == 0 && tot >= 32) || (l == 1 && tot >= 64)) g[w + l] = l ? (uint32_t)(lo >> 32) : (uint32_t)lo;
+    carry = tot >= 64 ? hiw : tot >= 32 ? (uint32_t)(lo >> 32) : (uint32_t)lo;
+    pos += n;
+  }
+  // append n copies of one bit value
+  __device__ __forceinline__ void fill(int64_t n, bool one) {
+    const int sh = (int)(pos & 31);
+    if (sh) {
+      const int k = (int)min<int64_t>(n, 32 - sh);
+      put64(one ? ~0ull : 0ull, k);
+      n -= k;
+    }
+    if (n <= 0) return;
+    const int64_t w0 = pos >> 5, nw = n >> 5;
+    for (int64_t w = lane_id(); w < nw; w += 64) g[w0 + w] = one ? 0xffffffffu : 0u;
+    pos += nw * 32;
+    n -= nw * 32;
+    carry = one && n ? (1u << n) - 1u : 0u;
+    pos += n;
+  }
+  // the last, partial word
+  __device__ __forceinline__ void finish() {
+    if ((pos & 31) && lane_id() == 0) g[pos >> 5] = carry;
+  }
+};
+
 // ---------------------------------------------------------------------------
 // RLE / bit-packed hybrid stream (hybrid_decoder.go:30-166)
 // ---------------------------------------------------------------------------
@@ -557,11 +601,10 @@ struct HybT {
   // bit-packed values [lo, hi) of the run whose value 0 is at stream bit b0
   // (lo, hi relative to the run), counted: == A into cA, >= B into cB; with
   // dst (the run's value 0), each stored as a byte
-  // (with bits: bit vb + j of the bitmap set for each value j == A; the
-  // bitmap is zeroed beforehand, its words shared with neighbouring runs)
+  // (with bo: one bit a value, set when it equals A, appended in order)
   template <bool BITS = false>
   __device__ __forceinline__ void count_packed(int64_t b0, int64_t lo, int64_t hi, uint32_t A, uint32_t B, int64_t &cA,
-                                               int64_t &cB, uint8_t *dst, uint32_t *bits = nullptr, int64_t vb = 0) {
+                                               int64_t &cB, uint8_t *dst, BitOut *bo = nullptr) {
     const int lane = lane_id();
     for (int64_t j0 = lo; j0 < hi; j0 += 64) {
       const int64_t j = j0 + lane;
@@ -575,25 +618,7 @@ struct HybT {
       cA += __popcll(ma);
       cB += __popcll(ballot(in && v >= B));
       if (dst && in) dst[j] = (uint8_t)v;
-      if (BITS && ma && lane < 3) {  // up to three words: lane q ORs the q-th
-        const int64_t bi = vb + j0;
-        const uint32_t sh = (uint32_t)(bi & 31);
-        const uint64_t lo64 = ma << sh;                        // bits [0, 64) of the span from word bi >> 5
-        const uint32_t hi32 = sh ? (uint32_t)(ma >> (64 - sh)) : 0u;  // bits [64, 96)
-        const uint32_t part = lane == 0 ? (uint32_t)lo64 : lane == 1 ? (uint32_t)(lo64 >> 32) : hi32;
-        if (part) atomicOr(&bits[(bi >> 5) + lane], part);
-      }
-    }
-  }
-  // bits [lo, hi) of a zeroed bitmap set (an RLE run of the counted value)
-  __device__ __forceinline__ static void bits_range(uint32_t *bits, int64_t lo, int64_t hi) {
-    if (hi <= lo) return;
-    for (int64_t w = (lo >> 5) + lane_id(); w <= ((hi - 1) >> 5); w += 64) {
-      const int64_t b0 = w * 32;
-      const int l = (int)(max(lo, b0) - b0), h = (int)(min(hi, b0 + 32) - b0);
-      const uint32_t mask = h - l == 32 ? 0xffffffffu : (((1u << (h - l)) - 1u) << l);
-      if (mask == 0xffffffffu) bits[w] = mask;
-      else atomicOr(&bits[w], mask);
+      if (BITS) bo->put64(ma, (int)(last + 1 - j0));
     }
   }
   // RLE value v for values [lo, hi) of dst
@@ -613,18 +638,18 @@ struct HybT {
   // (cB): the count path of k_prepare, no value leaves the run table (RLE
   // runs count whole).  Errors as next4 would report reading them.  With
   // dst, value i (since init) is also stored at dst[i] (one byte).
-  // With bits (instead of dst), value i is bit i of a zeroed bitmap: set when
-  // it equals A (flat pages: def == max_def, all k_decode needs).
+  // With BITS (bo instead of dst), value i is bit i of a bitmap: set when it
+  // equals A (flat pages: def == max_def, all k_decode needs).
   template <bool BITS = false>
   __device__ uint32_t count2(int64_t n, uint32_t A, uint32_t B, int64_t &cA, int64_t &cB, uint8_t *dst = nullptr,
-                             uint32_t *bits = nullptr) {
+                             BitOut *bo = nullptr) {
     const int lane = lane_id();
     if (n <= 0) return E_OK;
     if (bw == 0) {  // all zeros
       cA += A == 0 ? n : 0;
       cB += B == 0 ? n : 0;
       if (dst) fill_run(dst, vdone, vdone + n, 0u);
-      if (BITS && A == 0) bits_range(bits, vdone, vdone + n);
+      if (BITS) bo->fill(n, A == 0);
       vdone += n;
       return E_OK;
     }
@@ -638,6 +663,72 @@ struct HybT {
           const int32_t nxt = (int32_t)shfl32((uint32_t)tr_s, lane + 1 < 64 ? lane + 1 : 63);
           const int32_t e = lane + 1 < t_n ? nxt : (int32_t)(t_end - t_base);
           const bool mine = lane < t_n;
+          if (BITS && bw == 1) {
+            // bit width 1 (max_def 1): a bit-packed run's data bytes are the
+            // bitmap's bits themselves (LSB first), an RLE run of A a range of
+            // set bits — lane j builds output word j of a pass (its first run
+            // by a binary search over the lanes' run starts, then run by run),
+            // instead of a table search per value
+            int32_t la = 0;
+            const int64_t A0 = t_base + rel0, A1 = t_base + rel1;  // this part, absolute values
+            const int64_t wa = A0 >> 5;
+            const int64_t nwd = ((A1 - 1) >> 5) - wa + 1;
+            const int32_t tlast = (int32_t)(t_end - t_base);
+            for (int64_t w0 = 0; w0 < nwd; w0 += 64) {
+              const int64_t W = wa + w0 + lane;
+              const bool act = w0 + lane < nwd;
+              const int32_t v0 = (int32_t)(max(W * 32, A0) - t_base), v1 = (int32_t)(min(W * 32 + 32, A1) - t_base);
+              int r = 0;
+#pragma unroll
+              for (int st = 32; st >= 1; st >>= 1) {
+                const int32_t s2 = (int32_t)shfl32((uint32_t)tr_s, r + st < 64 ? r + st : 63);
+                if (r + st < t_n && s2 <= v0) r += st;
+              }
+              uint32_t word = 0;
+              int32_t v = v0;
+              // (every lane takes part in the shuffles; a lane past the part idles)
+              for (int it = 0; it < 32; it++) {
+                const bool go = act && v < v1;
+                if (!ballot(go)) break;
+                const int32_t s0 = (int32_t)shfl32((uint32_t)tr_s, r);
+                const int32_t sn = (int32_t)shfl32((uint32_t)tr_s, r + 1 < 64 ? r + 1 : 63);
+                const int32_t s1 = r + 1 < t_n ? sn : tlast;
+                const uint32_t tv = shfl32(tr_v, r);
+                const int32_t tk = (int32_t)shfl32((uint32_t)tr_k, r);
+                if (go) {
+                  const int32_t e2 = min(s1, v1);
+                  const int n2 = e2 - v;
+                  const uint32_t m = n2 >= 32 ? 0xffffffffu : ((1u << n2) - 1u);
+                  uint32_t x;
+                  if (tk) {
+                    x = tv == A ? m : 0u;
+                  } else {
+                    const int64_t q = (int64_t)tv * 8 + (v - s0);
+                    x = (uint32_t)(load_u64_unaligned(p + (q >> 3)) >> (q & 7)) & m;
+                  }
+                  word |= x << (int)((t_base + v) & 31);
+                  v = e2;
+                  r++;
+                }
+              }
+              la += __builtin_popcount(word);
+              // whole words stored; the part's first word completes the
+              // writer's carry, its last (partial) word becomes the carry
+              const bool first = act && w0 + lane == 0, lastw = act && w0 + lane == nwd - 1;
+              if (first) word |= bo->carry;
+              const bool partial_end = lastw && (A1 & 31) != 0;
+              if (act && !partial_end) bo->g[W] = word;
+              const uint64_t pe = ballot(partial_end);
+              if (pe) bo->carry = __builtin_amdgcn_readlane(word, (int)__builtin_ctzll(pe));
+              else if (ballot(lastw)) bo->carry = 0u;
+            }
+            bo->pos = A1;
+            cA += wave_sum32(la);
+            cB += take;  // (bitmaps are for flat pages: B = 0, every value counts)
+            vdone += take;
+            left -= take;
+            continue;
+          }
           if (BITS) {
             // every value by its own lane as below (4 a lane), a nibble a lane,
             // words assembled over 8 lanes; lanes start at a 32-value boundary
@@ -662,12 +753,15 @@ struct HybT {
               word |= __shfl_xor(word, 2);
               word |= __shfl_xor(word, 4);
               const int32_t g0 = q0 + 32 * (lane >> 3);  // the group's first value
-              if ((lane & 7) == 0 && g0 < rel1 && g0 + 32 > rel0) {
-                uint32_t *wp = bits + ((t_base + g0) >> 5);
-                if (g0 >= rel0 && g0 + 32 <= rel1) *wp = word;
-                else if (word) atomicOr(wp, word);
-              }
+              const bool own = (lane & 7) == 0 && g0 < rel1 && g0 + 32 > rel0;
+              if (own && g0 < rel0) word |= bo->carry;  // the part's first word: the bits before it
+              const bool partial_end = own && g0 + 32 > rel1;
+              if (own && !partial_end) bo->g[(t_base + g0) >> 5] = word;
+              const uint64_t pe = ballot(partial_end);
+              if (pe) bo->carry = __builtin_amdgcn_readlane(word, (int)__builtin_ctzll(pe));
+              else if (ballot(own && g0 + 32 == rel1)) bo->carry = 0u;
             }
+            bo->pos = t_base + rel1;
             cA += wave_sum32(la);
             cB += wave_sum32(lb);
             vdone += take;
@@ -767,10 +861,10 @@ struct HybT {
         cA += rle_val == A ? take : 0;
         cB += rle_val >= B ? take : 0;
         if (dst) fill_run(dst, vdone, vdone + take, rle_val);
-        if (BITS && rle_val == A) bits_range(bits, vdone, vdone + take);
+        if (BITS) bo->fill(take, rle_val == A);
       } else {
         const int ok = readable((int)min<int64_t>(take, 1 << 30));
-        count_packed<BITS>(data * 8, vi, vi + ok, A, B, cA, cB, dst ? dst + vdone - vi : nullptr, bits, vdone - vi);
+        count_packed<BITS>(data * 8, vi, vi + ok, A, B, cA, cB, dst ? dst + vdone - vi : nullptr, bo);
         if (ok < take) {
           vdone += ok;
           return E_EOF;

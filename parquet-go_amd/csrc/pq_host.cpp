@@ -1486,6 +1486,7 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
   ColumnPlan &cp = B->cols[(size_t)ci];
   const pqg_column_info &L = cp.info;
   const RowGroupMeta &G = f->rgs[(size_t)rg];
+  const bool bits_off = getenv_flag("PQG_LEVEL_BYTES");  // (per chunk: tests switch it per batch)
   auto chunk_err = [&](int ord, uint32_t stage, int code, const char *msg) {
     B->chunk_errors.push_back({rg, cp.leaf, ord, stage, (uint32_t)code});
     (void)msg;
@@ -1752,7 +1753,6 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
         B->pages.back().lvl_base = B->lvl_bytes;
         // flat pages without level output: a bit per level (k_decode needs only
         // def == max_def), an eighth of the scratch traffic (C3's nullable doubles)
-        static const bool bits_off = getenv_flag("PQG_LEVEL_BYTES");
         B->pages.back().lvl_bits = (int16_t)(L.max_rep == 0 && !(B->flags & PQG_BATCH_LEVELS) && !bits_off);
         // (bits: the bitmap and one word after it)
         B->lvl_bytes += B->pages.back().lvl_bits

@@ -163,6 +163,9 @@ __device__ __forceinline__ const uint8_t *body_ptr(const KArgs &a, const PageDes
 #ifndef PQ_RING
 #define PQ_RING 4096
 #endif
+#ifndef PQ_FAR_DEFER
+#define PQ_FAR_DEFER 1  // k_snappy: short far copies' loads overlap the token tables (0: written at once)
+#endif
 #ifndef PQ_SNAPPY_WPE
 #define PQ_SNAPPY_WPE 6
 #endif
@@ -526,7 +529,9 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
     // output position, all such loads in flight together
     const int64_t near_lo = dpos + T - RING;  // older bytes may be overwritten by this batch
     const int64_t S = dpos + out_rel - (int64_t)x;  // copy: absolute source start
-    bool pre = false;
+    bool pre = false, fdefer = false;
+    uint64_t fq0 = 0, fq1 = 0;
+    int fsh = 0;
     if (ballot(act && !lit && S < near_lo)) {
       // this wave's earlier staging stores must be visible to the loads below
       // (unless every source lies in output known written)
@@ -551,7 +556,18 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
           }
         }
       }
-      if (pre) {
+      if (pre && PQ_FAR_DEFER && (int)(fsrc & 7) + (int)len <= 16) {
+        // a short far copy (two aligned qwords): loads issued now, bytes
+        // written to the history after the token tables are built, so the
+        // round trip overlaps them
+        const uintptr_t b8 = fsrc & ~(uintptr_t)7;
+        const uint64_t *qp = (const uint64_t *)b8;
+        fq0 = in_payload ? qp[0] : __hip_atomic_load(qp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((int)(fsrc & 7) + (int)len > 8)
+          fq1 = in_payload ? qp[1] : __hip_atomic_load(qp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fsh = (int)(fsrc & 7);
+        fdefer = true;
+      } else if (pre) {
         // <= 64 source bytes: up to 9 aligned qwords; staged output read at
         // device scope (bypasses a possibly stale L1 line)
         const uintptr_t b8 = fsrc & ~(uintptr_t)7;
@@ -594,6 +610,15 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
     int32_t tot2;
     const int32_t before = wave_excl_scan32((int32_t)__builtin_popcount(bits), &tot2);
     if (lane < SB_OUT / 32) L.bmc[lane].y = (uint32_t)before;
+    if (fdefer) {  // the deferred far copies' bytes (their loads overlapped the tables)
+      const int64_t o = dpos + out_rel;
+#pragma unroll
+      for (int i2 = 0; i2 < 16; i2++) {
+        if (i2 >= (int)len) break;
+        const int bi = fsh + i2;
+        ring[(o + i2) & RING_MASK] = (uint8_t)((bi < 8 ? fq0 >> (8 * bi) : fq1 >> (8 * (bi - 8))) & 0xffu);
+      }
+    }
     wave_lds_sync();
     SNAP_T(4);
     // 5. every output byte by its own lane, 64 bytes per pass: a copy byte is
@@ -3402,12 +3427,14 @@ __device__ __forceinline__ void levels_page(const KArgs &a, int gi, int part) {
   if (c.max_rep > 0) lv += n;
   if (d.lvl_bits) {
     // flat page without level output: bit i = (def level i == max_def), all
-    // k_decode reads — an eighth of the byte scratch; the bitmap (and the word
-    // after it, read by k_decode's two-word loads) zeroed first, set by OR
-    uint32_t *bw = (uint32_t *)lv;
-    for (int w = lane; w <= ((n + 31) >> 5); w += 64) bw[w] = 0u;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    e = def.template count2<true>(n, (uint32_t)c.max_def, 0u, nn, slots, nullptr, bw);
+    // k_decode reads — an eighth of the byte scratch, each word written once
+    // (BitOut; k_decode's two-word loads mask what lies past the page)
+    BitOut bo;
+    bo.g = (uint32_t *)lv;
+    bo.pos = 0;
+    bo.carry = 0;
+    e = def.template count2<true>(n, (uint32_t)c.max_def, 0u, nn, slots, nullptr, &bo);
+    bo.finish();
   } else if (pre) {
     e = E_OK;
     for (int k = d.part0, done = 0; done < n && !e; k++) {

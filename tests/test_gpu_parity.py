@@ -314,6 +314,36 @@ def test_generated_nullable_mix():
                    "mix v" + ver)
 
 
+def test_flat_level_bitmaps():
+    """Flat pages without level output keep their definition levels as a
+    bitmap (def == max_def) written in order by k_levels (BitOut): null
+    densities from none to all (RLE-only streams, long bit-packed runs on the
+    serial path, short mixed runs through the run tables, bit width 1 and
+    the per-value path of an optional field inside an optional struct,
+    max_def 2), V1 and V2, against the oracle — with and without level
+    output (check_file), and with the byte scratch (PQG_LEVEL_BYTES=1)."""
+    pa = pytest.importorskip("pyarrow")
+    rng = np.random.default_rng(13)
+    n = 90000
+    cols = {}
+    for name, frac in (("none", 0.0), ("all", 1.0), ("rare", 0.001), ("half", 0.5), ("dense", 0.97)):
+        cols[name] = pa.array(rng.integers(-9, 9, n).astype(np.int64), mask=rng.random(n) < frac)
+    # runs: blocks of nulls and values of random lengths (long RLE and bit-packed runs)
+    blk = np.repeat(rng.random(n // 300) < 0.5, 300)[:n]
+    cols["blocks"] = pa.array(rng.standard_normal(n), mask=np.pad(blk, (0, n - len(blk))))
+    inner = pa.array(rng.integers(0, 100, n).astype(np.int32), mask=rng.random(n) < 0.2)
+    cols["st"] = pa.StructArray.from_arrays([inner], names=["v"], mask=pa.array(rng.random(n) < 0.1))
+    t = pa.table(cols)
+    for ver in ("1.0", "2.0"):
+        data = _pq_bytes(t, compression="snappy", data_page_version=ver, use_dictionary=False, row_group_size=40000)
+        check_file(data, "level bitmaps v" + ver)
+        os.environ["PQG_LEVEL_BYTES"] = "1"
+        try:
+            check_file(data, "level bytes v" + ver)
+        finally:
+            del os.environ["PQG_LEVEL_BYTES"]
+
+
 def test_generated_lists():
     pa = pytest.importorskip("pyarrow")
     rng = np.random.default_rng(12)
