@@ -163,6 +163,15 @@ __device__ __forceinline__ const uint8_t *body_ptr(const KArgs &a, const PageDes
 #ifndef PQ_RING
 #define PQ_RING 4096
 #endif
+#ifndef PQ_SNAP_TOKEN
+#define PQ_SNAP_TOKEN 1  // k_snappy: token-parallel output when the batch allows it (0: the per-byte chase always)
+#endif
+#ifndef SNAP_DEP_MAX
+#define SNAP_DEP_MAX 64  // copies overlapping their own batch written one after another (more: per-byte chase)
+#endif
+#ifndef SNAP_TOK_SHORT
+#define SNAP_TOK_SHORT 16  // token-parallel output: longer literals / near copies take the whole wave each
+#endif
 #ifndef PQ_FAR_DEFER
 #define PQ_FAR_DEFER 1  // k_snappy: short far copies' loads overlap the token tables (0: written at once)
 #endif
@@ -599,6 +608,63 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
       }
     }
     SNAP_T(3);
+    const uint8_t *winb = (const uint8_t *)L.win;
+    // Token-parallel output (PQ_SNAP_TOKEN): when every copy's source is
+    // either already in the history (older than the batch: `near`), or was
+    // prefilled / is being loaded (`pre`), or lies partly inside the batch
+    // (`dep`, at most SNAP_DEP_MAX of them), the tokens are written by their
+    // own lanes — literals from the window, near copies history to history,
+    // all at once — and then the dep copies one after another in token order,
+    // a byte a lane (an overlapping copy by pattern: byte r from
+    // S + r mod offset).  No token table, no start bitmap, no per-byte chase.
+    const bool nearc = act && !lit && !pre && S >= near_lo && S + (int64_t)len <= dpos;
+    const bool depc = act && !lit && !pre && S >= near_lo && S + (int64_t)len > dpos;
+    const uint64_t depm = ballot(depc);
+    const bool fast = PQ_SNAP_TOKEN && !ballot(act && !lit && !pre && S < near_lo) && __popcll(depm) <= SNAP_DEP_MAX;
+    if (fast) {
+      const int64_t o = dpos + out_rel;
+      // tokens of up to SNAP_TOK_SHORT bytes by their own lanes, two bytes a
+      // step; longer ones (long literals) one after another by the whole wave
+      const bool indep = act && (lit || nearc);
+      const uint32_t mylen = indep && len <= SNAP_TOK_SHORT ? len : 0u;
+      const uint32_t maxlen = __builtin_amdgcn_readlane(wave_incl_dpp<true>(mylen), 63);
+      for (uint32_t i = 0; i < maxlen; i += 2) {
+        uint8_t b0 = 0, b1 = 0;
+        if (i < mylen) b0 = lit ? winb[x + i] : ring[(S + i) & RING_MASK];
+        if (i + 1 < mylen) b1 = lit ? winb[x + i + 1] : ring[(S + i + 1) & RING_MASK];
+        if (i < mylen) ring[(o + i) & RING_MASK] = b0;
+        if (i + 1 < mylen) ring[(o + i + 1) & RING_MASK] = b1;
+      }
+      for (uint64_t lm = ballot(indep && len > SNAP_TOK_SHORT); lm; lm &= lm - 1) {
+        const int k = (int)__builtin_ctzll(lm);
+        const int64_t ok = dpos + (int64_t)__builtin_amdgcn_readlane(out_rel, k);
+        const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)len, k);
+        const uint32_t xk = (uint32_t)__builtin_amdgcn_readlane((int)x, k);
+        const bool litk = __builtin_amdgcn_readlane((int)lit, k) != 0;
+        if ((uint32_t)lane < lk) ring[(ok + lane) & RING_MASK] = litk ? winb[xk + lane] : ring[(ok - xk + lane) & RING_MASK];
+      }
+      if (fdefer) {  // the deferred far copies' bytes
+#pragma unroll
+        for (int i2 = 0; i2 < 16; i2++) {
+          if (i2 >= (int)len) break;
+          const int bi = fsh + i2;
+          ring[(o + i2) & RING_MASK] = (uint8_t)((bi < 8 ? fq0 >> (8 * bi) : fq1 >> (8 * (bi - 8))) & 0xffu);
+        }
+      }
+      wave_lds_sync();
+      SNAP_T(4);
+      for (uint64_t dm = depm; dm; dm &= dm - 1) {
+        const int k = (int)__builtin_ctzll(dm);
+        const int64_t ok = dpos + (int64_t)__builtin_amdgcn_readlane(out_rel, k);
+        const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)len, k);
+        const uint32_t xk = (uint32_t)__builtin_amdgcn_readlane((int)x, k);
+        if ((uint32_t)lane < lk) {
+          const int64_t sb = ok - (int64_t)xk + (int64_t)(xk >= lk ? (uint32_t)lane : (uint32_t)lane % xk);
+          ring[(ok + lane) & RING_MASK] = ring[sb & RING_MASK];
+        }
+        wave_lds_sync();
+      }
+    } else {
     // token table + start bitmap
     if (act) L.tok[lane] = make_uint4((uint32_t)out_rel, len | (lit ? 0x80000000u : 0u) | (pre ? 0x40000000u : 0u), x, 0u);
     if (lane < SB_OUT / 32) L.bmc[lane] = make_uint2(0u, 0u);
@@ -624,7 +690,6 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
     // 5. every output byte by its own lane, 64 bytes per pass: a copy byte is
     // chased back to a literal, a prefilled far copy, a byte resolved by an
     // earlier pass (already in the history), or a byte before the batch
-    const uint8_t *winb = (const uint8_t *)L.win;
     for (int it = 0; it * 64 < T; it++) {
       const int j = lane + 64 * it;
       if (j < T) {
@@ -695,6 +760,7 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
       }
       wave_lds_sync();
     }
+    }  // (per-byte path)
     wave_lds_sync();
     SNAP_T(5);
     // 6. to HBM: bytes up to the next 16-byte boundary (F is unaligned after
