@@ -232,6 +232,13 @@ int pqg_stream_open(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const i
  * PQG_OK after the last slice; a slice whose planning failed returns that
  * error (the stream ends there). *rg_first: the slice's first row group. */
 int pqg_stream_next(pqg_stream *s, pqg_batch **out, int *rg_first);
+/* pqg_stream_open flag: the first two slices hold a quarter and a half of
+ * rgs_per_slice row groups (at least one), so the first decode starts after a
+ * short upload and the pipeline fills sooner; later slices hold rgs_per_slice.
+ * Each slice's row groups: pqg_batch_row_groups. */
+enum { PQG_STREAM_RAMP = 1 << 8 };
+/* Row groups [*rg_begin, *rg_end) of a batch (a stream slice's range). */
+int pqg_batch_row_groups(const pqg_batch *b, int *rg_begin, int *rg_end);
 void pqg_stream_close(pqg_stream *s);
 
 #ifdef __cplusplus

@@ -3206,6 +3206,13 @@ int pqg_batch_sync(pqg_batch *B) {
   return (int)best.code;
 }
 
+int pqg_batch_row_groups(const pqg_batch *B, int *rg_begin, int *rg_end) {
+  if (!B) return PQG_ERR_ARG;
+  if (rg_begin) *rg_begin = B->rg_begin;
+  if (rg_end) *rg_end = B->rg_end;
+  return PQG_OK;
+}
+
 int pqg_batch_error_location(const pqg_batch *B, int *rg, int *leaf, int *page) {
   if (rg) *rg = B->err_rg;
   if (leaf) *leaf = B->err_leaf;
@@ -3443,9 +3450,16 @@ int pqg_stream_open(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const i
   S->ctx = ctx;
   S->f = f;
   if (nleaves > 0) S->leaves.assign(leaves, leaves + nleaves);
-  S->flags = flags;
   S->depth = depth;
-  for (int r = rg_begin; r < rg_end; r += rgs_per_slice) S->slices.push_back({r, std::min(rg_end, r + rgs_per_slice)});
+  // (PQG_STREAM_RAMP: slices of a quarter and a half first, so the pipeline
+  // fills after a short upload; the flag is the stream's, not the batches')
+  const bool ramp = (flags & PQG_STREAM_RAMP) != 0;
+  S->flags = flags & ~PQG_STREAM_RAMP;
+  for (int r = rg_begin, k = 0; r < rg_end; k++) {
+    const int per = !ramp || k >= 2 ? rgs_per_slice : std::max(1, rgs_per_slice / (k == 0 ? 4 : 2));
+    S->slices.push_back({r, std::min(rg_end, r + per)});
+    r += per;
+  }
   S->built.assign(S->slices.size(), nullptr);
   S->rcs.assign(S->slices.size(), 0);
   S->errs.assign(S->slices.size(), std::string());

@@ -55,7 +55,7 @@ EXPORTS = [
     "pqg_file_row_group_cost", "pqg_batch_stream",
     "pqg_file_column_count", "pqg_file_column_info", "pqg_file_find_column", "pqg_file_select_columns",
     "pqg_file_last_error", "pqg_batch_create", "pqg_batch_decode", "pqg_batch_sync",
-    "pqg_batch_error_location", "pqg_batch_column", "pqg_batch_copy", "pqg_batch_stats_get",
+    "pqg_batch_error_location", "pqg_batch_row_groups", "pqg_batch_column", "pqg_batch_copy", "pqg_batch_stats_get",
     "pqg_batch_kernel_times", "pqg_batch_set_timing", "pqg_batch_destroy",
     "pqg_stream_open", "pqg_stream_next", "pqg_stream_close", "pqg_file_open_many", "pqg_release_cache",
 ]
@@ -129,6 +129,7 @@ def lib():
                 "pqg_batch_create": (i32, [vp, vp, i32, i32, P(ctypes.c_int), i32, i32, P(vp)]),
                 "pqg_batch_decode": (i32, [vp]), "pqg_batch_sync": (i32, [vp]),
                 "pqg_batch_error_location": (i32, [vp, P(ctypes.c_int), P(ctypes.c_int), P(ctypes.c_int)]),
+                "pqg_batch_row_groups": (i32, [vp, P(ctypes.c_int), P(ctypes.c_int)]),
                 "pqg_batch_column": (i32, [vp, i32, P(ColumnView)]),
                 "pqg_batch_copy": (i32, [vp, i32, i32, vp, sz, P(sz)]),
                 "pqg_batch_stats_get": (i32, [vp, P(BatchStats)]),
@@ -328,12 +329,18 @@ class Batch:
             pass
 
 
+STREAM_RAMP = 1 << 8  # pqg_stream_open: the first two slices a quarter / half of rgs_per_slice (pqgpu.h)
+
+
 class _SliceBatch(Batch):
     """A slice handed out by a Stream: the stream owns (and frees) its handle."""
 
     def __init__(self, reader, handle, rg0, leaves, ctx):
         self.reader, self.ctx, self.leaves, self.rg0 = reader, ctx, list(leaves), rg0
         self._h = ctypes.c_void_p(handle)
+        lo, hi = ctypes.c_int(), ctypes.c_int()
+        _check(lib().pqg_batch_row_groups(self._h, ctypes.byref(lo), ctypes.byref(hi)), "pqg_batch_row_groups")
+        self.rg1 = hi.value  # the slice is row groups [rg0, rg1)
 
     def close(self):
         self._h = ctypes.c_void_p()
@@ -462,7 +469,9 @@ class FileReader:
         return Batch(self, rg0, rg1, self.selected if leaves is None else leaves, flags)
 
     def stream(self, rg0=0, rg1=None, rgs_per_slice=1, leaves=None, depth=2, flags=0):
-        """Pipelined decode of row groups [rg0, rg1) slice by slice (Stream)."""
+        """Pipelined decode of row groups [rg0, rg1) slice by slice (Stream;
+        flags | STREAM_RAMP: the first two slices smaller, each slice's range
+        is its batch's rg0 / rg1)."""
         rg1 = self.RowGroupCount() if rg1 is None else rg1
         return Stream(self, rg0, rg1, self.selected if leaves is None else leaves, rgs_per_slice, depth, flags)
 

@@ -487,12 +487,13 @@ def test_c5_lineitem_large_string_dictionary(tmp_path):
         del os.environ["PQG_SNAPPY_SEG_MIN"]
 
 
-@pytest.mark.parametrize("per,depth", [(1, 2), (2, 1), (3, 3)])
-def test_stream_slices_match_oracle(tmp_path, per, depth):
+@pytest.mark.parametrize("per,depth,ramp", [(1, 2, False), (2, 1, False), (3, 3, False), (4, 3, True)])
+def test_stream_slices_match_oracle(tmp_path, per, depth, ramp):
     """pqg_stream: row-group slices planned and uploaded by the host worker
     while the previous slice decodes; every slice bit-exact against the oracle's
     decode of the same row-group range (C5 shape: 16 leaves, strings, fallback
-    to PLAIN; C4 golden: lists and nullable strings)."""
+    to PLAIN; C4 golden: lists and nullable strings); with STREAM_RAMP the
+    first two slices hold a quarter and a half of `per` row groups."""
     pytest.importorskip("pyarrow")
     for data, ctx in ((_c5_bytes(tmp_path, 70000, 10000, dictionary_pagesize_limit=64 << 10), "c5"),
                       (golden_bytes("c4_list_str.parquet"), "c4")):
@@ -500,17 +501,24 @@ def test_stream_slices_match_oracle(tmp_path, per, depth):
         r = pqgpu.FileReader(data)
         leaves = list(range(len(r.Columns())))
         seen = []
-        with r.stream(0, None, per, leaves, depth) as st:
+        starts, rg = [], 0
+        while rg < o.num_row_groups:
+            starts.append(rg)
+            k = len(starts) - 1
+            rg += per if not ramp or k >= 2 else max(1, per // (4 if k == 0 else 2))
+        with r.stream(0, None, per, leaves, depth, pqgpu.STREAM_RAMP if ramp else 0) as st:
             for b in st:
                 rc = b.sync(raise_on_error=False)
                 assert rc == 0, (ctx, b.rg0, pqgpu.last_error())
-                rg1 = min(b.rg0 + per, o.num_row_groups)
+                rg1 = b.rg1
+                k = starts.index(b.rg0)
+                assert rg1 == (starts[k + 1] if k + 1 < len(starts) else o.num_row_groups), (ctx, b.rg0, rg1)
                 for i, leaf in enumerate(leaves):
                     info = o.leaves()[leaf]
                     assert_same(b.column(i), o.decode(leaf, b.rg0, rg1), info["max_def"], info["max_rep"],
                                 "%s stream slice %d leaf %d" % (ctx, b.rg0, leaf))
                 seen.append(b.rg0)
-        assert seen == list(range(0, o.num_row_groups, per)), (ctx, seen)
+        assert seen == starts, (ctx, seen)
 
 
 @pytest.mark.parametrize("maxlen", [0, 3, 20, 60, 300])
