@@ -181,17 +181,30 @@ def _child_cmd(args, steps=3):
     return cmd
 
 
-# every full decode ends with k_level_check (pq_host.cpp launch_all), and the
-# child's timed loop is the last thing it launches: the dispatches after the
-# (CHILD_STEPS + 1)-th last k_level_check are exactly CHILD_STEPS decode steps
+# every full decode ends with the same launch (pq_host.cpp launch_all):
+# k_level_check, or — in a batch without level streams, which skips it — the
+# last tiled-expand launch; the child's timed loop is the last thing it
+# launches, so the dispatches after the (CHILD_STEPS + 1)-th last step end are
+# exactly CHILD_STEPS decode steps
 CHILD_STEPS = 3
 STEP_END = "k_level_check"
+
+
+def _step_end(rows, key_name):
+    """The kernel that ends every decode of this run: k_level_check when it is
+    launched, else the run's last dispatch of a pq kernel (host submission
+    order)."""
+    if any(_kname(r[key_name]) == STEP_END for r in rows):
+        return STEP_END
+    ours = [r for r in rows if not r[key_name].startswith("__amd")]  # (the runtime's blit kernels: copies)
+    return _kname(ours[-1][key_name]) if ours else STEP_END
 
 
 def _last_steps(rows, key_id, key_name, steps=CHILD_STEPS):
     """Rows of the last `steps` decode steps, in dispatch (host submission) order."""
     rows = sorted(rows, key=lambda r: int(r[key_id]))
-    ends = [i for i, r in enumerate(rows) if _kname(r[key_name]) == STEP_END]
+    end = _step_end(rows, key_name)
+    ends = [i for i, r in enumerate(rows) if _kname(r[key_name]) == end]
     if len(ends) < steps + 1:
         return None
     return rows[ends[-steps - 1] + 1:ends[-1] + 1]
@@ -242,7 +255,8 @@ def kernel_trace(args):
         with open(os.path.join(keep, "rocprof_kernel_steps_%s.csv" % args.config), "w") as f:
             f.write("# bench.py --config %s: the %d timed decode steps of the rocprofv3 --kernel-trace child run "
                     "(dispatches after the %d-th last %s), per kernel\n" % (args.config, CHILD_STEPS,
-                                                                            CHILD_STEPS + 1, STEP_END))
+                                                                            CHILD_STEPS + 1,
+                                                                            _step_end(sorted(rows, key=lambda r: int(r["Dispatch_Id"])), "Kernel_Name")))
             f.write("Name,CallsPerStep,AverageNs,NsPerStep\n")
             for k, v in sorted(res.items(), key=lambda kv: -kv[1]["us_per_step"]):
                 f.write("%s,%g,%.0f,%.0f\n" % (k, v["calls_per_step"], v["avg_us"] * 1e3, v["us_per_step"] * 1e3))
