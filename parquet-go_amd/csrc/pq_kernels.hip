@@ -163,6 +163,9 @@ __device__ __forceinline__ const uint8_t *body_ptr(const KArgs &a, const PageDes
 #ifndef PQ_RING
 #define PQ_RING 4096
 #endif
+#ifndef PQ_PF_EARLY
+#define PQ_PF_EARLY 1  // k_snappy: the next batch's window prefetched right after the token chain (0: after the far copies)
+#endif
 #ifndef PQ_SNAP_TOKEN
 #define PQ_SNAP_TOKEN 1  // k_snappy: token-parallel output when the batch allows it (0: the per-byte chase always)
 #endif
@@ -430,6 +433,7 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
   // m-th token (no serial walk on the scalar unit)
   const int64_t lim64 = (int64_t)sh + (slen - s) - 1;  // last position inside the block
   const int lim = lim64 < 255 ? (int)lim64 : 255;
+  int pos = sh;
   uint16_t *ja = L.jt[0], *jb = L.jt[1];
 #pragma unroll
   for (int j = 0; j < 4; j++) {
@@ -444,7 +448,6 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
     jb[256] = 256;
   }
   wave_lds_sync();
-  int pos = sh;
 #pragma unroll
   for (int b = 0; b < 6; b++) {
     // every read of a round issued before its writes (the tables are both
@@ -479,6 +482,19 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
   }
   const int T = (int)__builtin_amdgcn_readlane(incl, ntok - 1);
   const int cur = (int)__builtin_amdgcn_readlane(pos, ntok - 1) + (int)(__builtin_amdgcn_readlane(pc, ntok - 1) & 0xff);
+  if (PQ_PF_EARLY) {
+    // the next batch's window, prefetched as soon as this batch's end is
+    // known: its loads overlap this batch's decode, far copies and output
+    const int64_t sn = s + (cur - sh);
+    if (sn < slen) {
+      const uint32_t *gn = (const uint32_t *)((uintptr_t)(src + sn) & ~(uintptr_t)3);
+      pg0 = gn[lane];
+      pg1 = gn[lane + 64];
+      pg2 = lane < 4 ? gn[lane + 128] : 0u;
+      pf_s = sn;
+      pf_F = F;
+    }
+  }
   const uint32_t tokpos = (uint32_t)pos;
   wave_lds_sync();
   SNAP_T(1);
@@ -595,8 +611,8 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
         }
       }
     }
-    // prefetch the next batch's window (its loads overlap this batch's byte passes)
-    {
+    // prefetch the next batch's window (its loads overlap this batch's output)
+    if (!PQ_PF_EARLY) {
       const int64_t sn = s + (cur - sh);
       if (sn < slen) {
         const uint32_t *gn = (const uint32_t *)((uintptr_t)(src + sn) & ~(uintptr_t)3);
