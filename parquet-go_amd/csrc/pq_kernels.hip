@@ -2873,6 +2873,11 @@ struct RunBuf {
 // sum of their lengths.  Anything unusual (multi-byte header, an error, the
 // end of the stream) is left to the exact serial step below.
 constexpr uint32_t NX_STOP = 0xFFFFu;
+#ifndef PQ_CHAIN_WIN
+#define PQ_CHAIN_WIN 2048  // run walk chain window (bytes, a multiple of 1 KiB; lbytes / lnx hold it)
+#endif
+constexpr int CW = PQ_CHAIN_WIN;
+static_assert(CW % 1024 == 0 && CW <= 2048, "chain window: lnx holds 2,048 positions");
 #ifndef PQ_DEC_DICT_LDS
 #define PQ_DEC_DICT_LDS 8192  // k_decode<3> / <2>: dictionaries (<2>: entry tables) up to this many bytes gathered from LDS (0: off)
 #endif
@@ -2915,30 +2920,40 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
         a.dbg3[iters * 4 + 3] = (uint64_t)(R.base + R.cnt);
       }
 #endif
-      if (!W.ab || ks + hpos < W.ab || (ks + hpos) - W.ab > 512) W.fill(ks + hpos);
-      const int64_t wbo = W.ab - ks;  // stream offset of window byte 0
-      if (W.ab != nx_ab) {
-        nx_ab = W.ab;
-        *(uint4 *)(lbytes + 16 * lane) = W.w;
-        const uint32_t wd[4] = {W.w.x, W.w.y, W.w.z, W.w.w};
+      // the chain window: CW bytes of the stream in LDS (lbytes), 16 bytes a
+      // lane a load, re-anchored at the next header once it is past the
+      // window's first half (bit width 1 pages: 5 window steps with 1 KiB, 2
+      // with 2 KiB)
+      if (!nx_ab || ks + hpos < nx_ab || (ks + hpos) - nx_ab > CW / 2) {
+        nx_ab = (const uint8_t *)((uintptr_t)(ks + hpos) & ~(uintptr_t)15);
+        u32x4 wv[CW / 1024];
 #pragma unroll
-        for (int i = 0; i < 16; i += 2) {
-          uint32_t two = 0;
+        for (int h = 0; h < CW / 1024; h++)
+          wv[h] = *(const __attribute__((address_space(1))) u32x4 *)(nx_ab + 1024 * h + 16 * lane);
 #pragma unroll
-          for (int k = 0; k < 2; k++) {
-            const uint32_t b = (wd[(i + k) >> 2] >> (8 * ((i + k) & 3))) & 0xffu;
-            const uint32_t r = 16 * lane + i + k, g = b >> 1;
-            uint32_t nx = NX_STOP;
-            if (b < 0x80 && g != 0) nx = min(r + 1 + ((b & 1) ? g * (uint32_t)bw : (uint32_t)sz), NX_STOP - 1);
-            two |= nx << (16 * k);
+        for (int h = 0; h < CW / 1024; h++) {
+          *(u32x4 *)(lbytes + 1024 * h + 16 * lane) = wv[h];
+          const uint32_t wd[4] = {wv[h].x, wv[h].y, wv[h].z, wv[h].w};
+#pragma unroll
+          for (int i = 0; i < 16; i += 2) {
+            uint32_t two = 0;
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+              const uint32_t b = (wd[(i + k) >> 2] >> (8 * ((i + k) & 3))) & 0xffu;
+              const uint32_t r = 1024 * h + 16 * lane + i + k, g = b >> 1;
+              uint32_t nx = NX_STOP;
+              if (b < 0x80 && g != 0) nx = min(r + 1 + ((b & 1) ? g * (uint32_t)bw : (uint32_t)sz), NX_STOP - 1);
+              two |= nx << (16 * k);
+            }
+            *(uint32_t *)(lnx + 1024 * h + 16 * lane + i) = two;
           }
-          *(uint32_t *)(lnx + 16 * lane + i) = two;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
+      const int64_t wbo = nx_ab - ks;  // stream offset of window byte 0
       int32_t r = (int32_t)(hpos - wbo), cnt = 0;
       uint32_t myr = 0;
-      while (cnt < 64 && r <= 1024 - 8 - sz && wbo + r < slen) {
+      while (cnt < 64 && r <= CW - 8 - sz && wbo + r < slen) {
         const uint32_t nx = ufirst((uint32_t)lnx[r]);
         if (nx == NX_STOP) break;
         if (lane == cnt) myr = (uint32_t)r;
@@ -3442,7 +3457,7 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
 
 template <int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_prepare(KArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t wl_bytes[4][1024];  // run walk: window bytes
+  __shared__ __attribute__((aligned(16))) uint8_t wl_bytes[4][CW];  // run walk: chain window bytes
   __shared__ __attribute__((aligned(16))) uint16_t wl_nx[4][2048];    // run walk: chain table (BYTE_ARRAY walk: two)
   const int wv = (int)ufirst(threadIdx.x >> 6);
   prepare_page(a, (int)blockIdx.x * 4 + wv, wl_bytes[wv], wl_nx[wv], MODE);
@@ -3570,7 +3585,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PQ_LEVELS_W
 // dictionaries, which k_prepare only points at).  Neither waits on the other;
 // pages that do wait are prepared by k_prepare<1> after this launch.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_prepare_copy(KArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t wl_bytes[4][1024];
+  __shared__ __attribute__((aligned(16))) uint8_t wl_bytes[4][CW];
   __shared__ __attribute__((aligned(16))) uint16_t wl_nx[4][2048];
   const uint32_t pb = ((uint32_t)a.nlist + 3) / 4;
   if (blockIdx.x < pb) {
