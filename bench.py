@@ -625,13 +625,17 @@ def main():
     wb.sync()
     wb.close()
     # one-shot PCIe-inclusive time (not `value`): host plan + H2D upload + one
-    # decode, to the decode's sync (the upload's DMAs finish inside it)
-    t_oneshot = time.perf_counter()
-    b1 = reader.batch(rg0, rg1)
-    b1.decode()
-    b1.sync()
-    t_oneshot = time.perf_counter() - t_oneshot
-    b1.close()
+    # decode, to the decode's sync (the upload's DMAs finish inside it); best of
+    # three (a single trial now and then reads ~30 ms on C2: kept in the line)
+    oneshot_trials = []
+    for _ in range(3):
+        t_oneshot = time.perf_counter()
+        b1 = reader.batch(rg0, rg1)
+        b1.decode()
+        b1.sync()
+        oneshot_trials.append(time.perf_counter() - t_oneshot)
+        b1.close()
+    t_oneshot = min(oneshot_trials)
     t_create = time.perf_counter()
     batch = reader.batch(rg0, rg1)  # host plan (page headers) + one H2D upload of the chunks
     t_create = time.perf_counter() - t_create
@@ -733,6 +737,7 @@ def main():
                    # upload's DMAs end)
                    "e2e": {"batch_create_ms": round(t_create * 1e3, 2),
                            "oneshot_ms": round(t_oneshot * 1e3, 2),
+                           "oneshot_trials_ms": [round(t * 1e3, 2) for t in oneshot_trials],
                            "GBps_incl_plan_and_h2d": round(out_b / t_oneshot / 1e9, 1)},
                    "parallelism": "row-group shards, one process per GPU, no data-path collective"
                                   + ("" if world == 1 else " (%s for the barrier / time reduction)"
