@@ -18,8 +18,8 @@ FileReader.RowGroupCost) on its own GPU: weak scaling, no
 collective on the data path; value = decoded bytes of all ranks / max-over-ranks
 time.  `--gpus N` without WORLD_SIZE in the environment starts the N rank
 processes itself (spawn_ranks); under torch.distributed.run WORLD_SIZE must
-equal N.  `--allgather` additionally times the optional column all-gather over
-RCCL (pqgather, never inside the timed steps).
+equal N.  `--allgather` additionally times the optional column all-gather and the
+all-to-one gather to rank 0 over RCCL (pqgather, never inside the timed steps).
 
 Besides the timed loop (rank 0, N = 1), outside the timed region:
   * every pipeline phase is timed with HIP events on a second batch of the
@@ -571,7 +571,8 @@ def main():
     ap.add_argument("--no-pmc", action="store_true", help="(compat) same as --no-prof")
     ap.add_argument("--no-parity", action="store_true", help="skip the whole-shard oracle comparison")
     ap.add_argument("--child", action="store_true", help="internal: a profiled child run (timed loop only)")
-    ap.add_argument("--allgather", action="store_true", help="N > 1: time the optional column all-gather (RCCL)")
+    ap.add_argument("--allgather", action="store_true",
+                    help="N > 1: time the optional column all-gather and gather-to-root (RCCL)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="N > 1: process group backend for the barrier / max-time reduction (gloo: ranks may "
                          "share a GPU, as in the CPU-box test)")
@@ -689,7 +690,19 @@ def main():
         torch.cuda.synchronize(dev)
         ta = time.perf_counter() - ta
         gb = sum(v.numel() * v.element_size() for v in col.values() if hasattr(v, "numel")) / 1e9
-        allgather = {"leaf": 0, "GB_per_rank": round(gb, 4), "ms": round(ta * 1e3, 3), "GBps_per_rank": round(gb / ta, 1)}
+        del col
+        # the all-to-one form: the whole column on rank 0 only
+        barrier()
+        tr = time.perf_counter()
+        col = pqgather.gather_column_to(shard, 0)
+        torch.cuda.synchronize(dev)
+        tr = time.perf_counter() - tr
+        del col
+        tr_max = torch.tensor([tr], dtype=torch.float64, device=dev)
+        dist.all_reduce(tr_max, op=dist.ReduceOp.MAX)
+        tr = float(tr_max.item())
+        allgather = {"leaf": 0, "GB_per_rank": round(gb, 4), "ms": round(ta * 1e3, 3), "GBps_per_rank": round(gb / ta, 1),
+                     "gather_to_root_ms": round(tr * 1e3, 3), "gather_to_root_GBps": round(gb / tr, 1)}
     parity = None
     if not (args.child or args.no_parity):
         # the timed batch's own output, on every rank, before it is closed

@@ -2,8 +2,10 @@
 
 Decoding needs no collective: row groups are independent (one dictionary per
 chunk, chunk_reader.go:221-251) and each rank decodes its own shard.  This
-module is the one exchange step §8(e) allows: an all-gather that gives every
-rank the whole column, assembled in row-group order from the ranks' shards.
+module is the one exchange step §8(e) allows, in two forms: `gather_column_to`
+materialises the whole column on one device (all-to-one point-to-point sends,
+the topology SURVEY.md §5 prefers over xGMI), `allgather_column` gives every
+rank the whole column; both assemble it in row-group order from the shards.
 
 * fixed-width values, validity bitmaps, list validity: all-gather-v (shards
   padded to the largest, one `all_gather` per buffer, then trimmed);
@@ -95,16 +97,9 @@ def _bool_to_bits(b):
     return (pad.reshape(-1, 8) * w).sum(1, dtype=torch.int32).to(torch.uint8)
 
 
-def allgather_column(shard, group=None):
-    """Whole column on every rank from each rank's decoded shard (row groups in
-    rank order, as pqgpu.plan_row_group_shards assigns them).
-
-    shard: dict as returned by shard_tensors (or the same keys as host/CPU
-    tensors for gloo): values uint8, validity uint8 bitmap or None,
-    list_offsets int32 or None, list_validity uint8 or None, str_offsets
-    int64 or None, plus slots / rows ints.
-    Returns the same keys for the whole column.
-    """
+def _layout(shard, group):
+    """Every rank's (slots, rows, value bytes) and the buffers the column has
+    (a tiny all-gather of 7 int64s, the only collective both exchanges share)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
@@ -116,44 +111,120 @@ def allgather_column(shard, group=None):
     dist.all_gather(metas, meta, group=group)
     metas = [m.tolist() for m in metas]
     if any(m[3:] != metas[0][3:] for m in metas):
-        raise ValueError("allgather_column: ranks hold different column layouts")
-    slots = [m[0] for m in metas]
-    rows = [m[1] for m in metas]
-    vbytes = [m[2] for m in metas]
-    out = {"slots": sum(slots), "rows": sum(rows), "value_width": shard.get("value_width", 0)}
-    out["values"] = torch.cat(_gather_v(shard["values"], vbytes, group))
+        raise ValueError("pqgather: ranks hold different column layouts")
+    return [m[0] for m in metas], [m[1] for m in metas], [m[2] for m in metas], has
+
+
+def _counts(name, slots, rows, vbytes):
+    """Elements of buffer `name` in each rank's shard."""
+    return {"values": vbytes,
+            "validity": [(s + 7) // 8 for s in slots],
+            "list_offsets": [r + 1 for r in rows],
+            "list_validity": [(r + 7) // 8 for r in rows],
+            "str_offsets": [s + 1 for s in slots]}[name]
+
+
+_BUFS = ("values", "validity", "list_offsets", "list_validity", "str_offsets")
+
+
+def _assemble(parts, slots, rows, vbytes, has, value_width, dev):
+    """The whole column from the shards' buffers in rank (= row-group) order:
+    bitmaps re-packed at shard boundaries, offsets rebased (data_store.go:15-31)."""
+    import torch
+    out = {"slots": sum(slots), "rows": sum(rows), "value_width": value_width}
+    out["values"] = torch.cat(parts["values"])
+    out["validity"] = None
     if has[0]:
-        parts = _gather_v(shard["validity"], [(s + 7) // 8 for s in slots], group)
-        out["validity"] = _bool_to_bits(torch.cat([_bits_to_bool(p, s) for p, s in zip(parts, slots)]))
-    else:
-        out["validity"] = None
+        out["validity"] = _bool_to_bits(torch.cat([_bits_to_bool(p, s) for p, s in zip(parts["validity"], slots)]))
+    out["list_offsets"] = None
     if has[1]:
         # list offsets index element slots: rank r's offsets shift by the
         # element slots of ranks < r
-        parts = _gather_v(shard["list_offsets"], [r + 1 for r in rows], group)
         base, segs = 0, [torch.zeros(1, dtype=torch.int32, device=dev)]
-        for p, s in zip(parts, slots):
+        for p, s in zip(parts["list_offsets"], slots):
             segs.append(p[1:] - p[0] + base)
             base += s
         out["list_offsets"] = torch.cat(segs)
-    else:
-        out["list_offsets"] = None
+    out["list_validity"] = None
     if has[2]:
-        parts = _gather_v(shard["list_validity"], [(r + 7) // 8 for r in rows], group)
-        out["list_validity"] = _bool_to_bits(torch.cat([_bits_to_bool(p, r) for p, r in zip(parts, rows)]))
-    else:
-        out["list_validity"] = None
+        out["list_validity"] = _bool_to_bits(
+            torch.cat([_bits_to_bool(p, r) for p, r in zip(parts["list_validity"], rows)]))
+    out["str_offsets"] = None
     if has[3]:
         # string offsets: one per slot + 1, rebased by the preceding shards' bytes
-        parts = _gather_v(shard["str_offsets"], [s + 1 for s in slots], group)
         base, segs = 0, [torch.zeros(1, dtype=torch.int64, device=dev)]
-        for p, nb in zip(parts, vbytes):
+        for p, nb in zip(parts["str_offsets"], vbytes):
             segs.append(p[1:] - p[0] + base)
             base += nb
         out["str_offsets"] = torch.cat(segs)
-    else:
-        out["str_offsets"] = None
     return out
+
+
+def _present(name, has):
+    return name == "values" or has[_BUFS.index(name) - 1]
+
+
+def allgather_column(shard, group=None):
+    """Whole column on every rank from each rank's decoded shard (row groups in
+    rank order, as pqgpu.plan_row_group_shards assigns them).
+
+    shard: dict as returned by shard_tensors (or the same keys as host/CPU
+    tensors for gloo): values uint8, validity uint8 bitmap or None,
+    list_offsets int32 or None, list_validity uint8 or None, str_offsets
+    int64 or None, plus slots / rows ints.
+    Returns the same keys for the whole column.
+    """
+    slots, rows, vbytes, has = _layout(shard, group)
+    parts = {}
+    for name in _BUFS:
+        if _present(name, has):
+            parts[name] = _gather_v(shard[name], _counts(name, slots, rows, vbytes), group)
+    return _assemble(parts, slots, rows, vbytes, has, shard.get("value_width", 0), shard["values"].device)
+
+
+def gather_column_to(shard, root=0, group=None):
+    """Whole column on ONE rank (`root`, a rank of `group`): the all-to-one
+    materialisation of SURVEY.md §5 / §8(e).  Every other rank sends its shard's
+    buffers straight to the root (point-to-point sends, posted together with
+    `batch_isend_irecv`, so over xGMI each source uses its own link to the
+    root); nothing is padded and no rank but the root holds the whole column —
+    1/N of `allgather_column`'s memory and link traffic.  Same shard dict as
+    `allgather_column`; returns the whole column on the root, None elsewhere.
+    """
+    import torch
+    import torch.distributed as dist
+    slots, rows, vbytes, has = _layout(shard, group)
+    me = dist.get_rank(group)
+    world = len(slots)
+    g_root = root if group is None else dist.get_global_rank(group, root)
+    dev = shard["values"].device
+    ops, parts = [], {}
+    for name in _BUFS:
+        if not _present(name, has):
+            continue
+        cnt = _counts(name, slots, rows, vbytes)
+        t = shard[name]
+        if me != root:
+            if cnt[me]:
+                ops.append(dist.P2POp(dist.isend, t[:cnt[me]].contiguous(), g_root, group))
+            continue
+        bufs = []
+        for r in range(world):
+            if r == root:
+                bufs.append(t[:cnt[r]])
+                continue
+            b = torch.empty(cnt[r], dtype=t.dtype, device=dev)
+            if cnt[r]:
+                src = r if group is None else dist.get_global_rank(group, r)
+                ops.append(dist.P2POp(dist.irecv, b, src, group))
+            bufs.append(b)
+        parts[name] = bufs
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    if me != root:
+        return None
+    return _assemble(parts, slots, rows, vbytes, has, shard.get("value_width", 0), dev)
 
 
 def to_numpy(col):

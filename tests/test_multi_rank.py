@@ -130,7 +130,7 @@ def test_two_rank_gloo_shards_match_whole_file(tmp_path):
     assert a0 == 0 and a1 == b0 and b1 == pq.ParquetFile(path).num_row_groups
 
 
-def _gather_main(rank, world, port, path, leaf, out_dir):
+def _gather_main(rank, world, port, path, leaf, out_dir, root=-1):
     import torch
     import torch.distributed as dist
     sys.path[:0] = [os.path.join(ROOT, "parquet-go_amd"), os.path.join(ROOT, "oracle")]
@@ -162,9 +162,16 @@ def _gather_main(rank, world, port, path, leaf, out_dir):
     shard = {"slots": int(got["slots"]), "rows": int(got["rows"]), "values": torch.from_numpy(got["values"].copy()),
              "validity": t("validity", np.uint8), "list_offsets": t("list_offsets", np.int32),
              "list_validity": t("list_validity", np.uint8), "str_offsets": t("str_offsets", np.int64)}
-    col = pqgather.to_numpy(pqgather.allgather_column(shard))
-    if rank == world - 1:
-        np.savez(os.path.join(out_dir, "gathered.npz"), **{k: np.asarray(v) for k, v in col.items()})
+    if root < 0:
+        col = pqgather.to_numpy(pqgather.allgather_column(shard))
+        if rank == world - 1:
+            np.savez(os.path.join(out_dir, "gathered.npz"), **{k: np.asarray(v) for k, v in col.items()})
+    else:
+        col = pqgather.gather_column_to(shard, root)
+        assert (col is None) == (rank != root), (rank, root)
+        if rank == root:
+            col = pqgather.to_numpy(col)
+            np.savez(os.path.join(out_dir, "gathered.npz"), **{k: np.asarray(v) for k, v in col.items()})
     dist.destroy_process_group()
 
 
@@ -189,6 +196,30 @@ def test_allgather_column_gloo(tmp_path, name, leaf, world):
     for k in ("values", "validity", "list_offsets", "list_validity", "str_offsets"):
         if k == "validity" and info["max_def"] == 0:
             continue  # a required column has no bitmap on the GPU (the oracle's is all ones)
+        assert np.array_equal(got[k].view(np.uint8).ravel(), whole[k]), k
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("name,leaf,world,root", [("c4_list_str", 0, 2, 0), ("c4_list_str", 1, 3, 2),
+                                                  ("c3_delta_v2", 1, 3, 1), ("plain_strings", 0, 2, 1),
+                                                  ("c2_dict_bw8", 0, 3, 0),
+                                                  # more ranks than row groups: empty shards send nothing
+                                                  ("c4_list_str", 0, 5, 3), ("gzip_int64", 0, 5, 0)])
+def test_gather_column_to_root_gloo(tmp_path, name, leaf, world, root):
+    """The all-to-one materialisation over gloo: only the
+    root ends with the whole column, equal to the whole-file decode."""
+    pytest.importorskip("torch")
+    import torch.multiprocessing as mp
+    import oracle
+    path = os.path.join(GOLDEN, name + ".parquet")
+    mp.spawn(_gather_main, args=(world, _free_port(), path, leaf, str(tmp_path), root), nprocs=world, join=True)
+    got = np.load(str(tmp_path / "gathered.npz"))
+    o = oracle.File(open(path, "rb").read())
+    whole, info = o.decode(leaf), o.leaves()[leaf]
+    assert int(got["slots"]) == whole["slots"] and int(got["rows"]) == whole["rows"]
+    for k in ("values", "validity", "list_offsets", "list_validity", "str_offsets"):
+        if k == "validity" and info["max_def"] == 0:
+            continue
         assert np.array_equal(got[k].view(np.uint8).ravel(), whole[k]), k
 
 
@@ -286,7 +317,7 @@ def test_bench_timed_batch_parity_every_rank(tmp_path, config):
             assert line["config"]["parity"].startswith("all 2 ranks")
 
 
-def _gpu_rccl_main(rank, world, port, path, leaf, out_dir):
+def _gpu_rccl_main(rank, world, port, path, leaf, out_dir, mode="all"):
     import torch
     import torch.distributed as dist
     sys.path[:0] = [os.path.join(ROOT, "parquet-go_amd")]
@@ -301,18 +332,26 @@ def _gpu_rccl_main(rank, world, port, path, leaf, out_dir):
     b.decode()
     shard = pqgather.shard_tensors(b, 0, torch.device("cuda", rank))
     b.close()
-    col = pqgather.allgather_column(shard)  # device tensors through RCCL
+    if mode == "all":
+        col = pqgather.allgather_column(shard)  # device tensors through RCCL
+    else:  # all-to-one on the last rank, point-to-point over RCCL
+        col = pqgather.gather_column_to(shard, world - 1)
+        if rank != world - 1:
+            assert col is None
+            dist.destroy_process_group()
+            return
     assert all(v.is_cuda for v in col.values() if hasattr(v, "is_cuda"))
     col = pqgather.to_numpy(col)
-    if rank == 0:
+    if rank == (0 if mode == "all" else world - 1):
         np.savez(os.path.join(out_dir, "gathered.npz"), **{k: np.asarray(v) for k, v in col.items()})
     dist.destroy_process_group()
 
 
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("name,leaf", [("c4_list_str", 0), ("c4_list_str", 1), ("c3_delta_v2", 1)])
-def test_gpu_allgather_rccl_device_tensors(tmp_path, name, leaf):
+@pytest.mark.parametrize("name,leaf,mode", [("c4_list_str", 0, "all"), ("c4_list_str", 1, "all"),
+                                            ("c3_delta_v2", 1, "all"), ("c4_list_str", 1, "root")])
+def test_gpu_allgather_rccl_device_tensors(tmp_path, name, leaf, mode):
     """allgather_column over RCCL on device tensors (one rank per GPU the box
     has: RCCL does not put two ranks on one GPU); the gloo tests above cover
     the re-packing at shard boundaries with more ranks."""
@@ -324,7 +363,7 @@ def test_gpu_allgather_rccl_device_tensors(tmp_path, name, leaf):
         pytest.skip("an RCCL all-gather needs >= 2 GPUs (a 1-rank 'collective' proves nothing); "
                     "the gloo tests cover the re-packing")
     path = os.path.join(GOLDEN, name + ".parquet")
-    mp.spawn(_gpu_rccl_main, args=(world, _free_port(), path, leaf, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_gpu_rccl_main, args=(world, _free_port(), path, leaf, str(tmp_path), mode), nprocs=world, join=True)
     got = np.load(str(tmp_path / "gathered.npz"))
     o = oracle.File(open(path, "rb").read())
     whole, info = o.decode(leaf), o.leaves()[leaf]
