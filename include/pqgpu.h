@@ -185,6 +185,12 @@ typedef struct {
   int64_t h2d_bytes;        /* bytes uploaded by pqg_batch_create */
   int64_t snappy_in_bytes;  /* compressed bytes of the Snappy pages (k_snappy's input) */
   int64_t dict_bytes;       /* uncompressed bytes of the dictionary pages */
+  /* host time (ms) of pqg_batch_create's stages: page plan, device-cache
+   * allocation, input upload (of which: gathering into the pinned ring, and
+   * waiting for a ring buffer's previous DMA), output allocation + tables
+   * (including a counting pass's launch, not its device time) */
+  double create_plan_ms, create_alloc_ms, create_upload_ms, create_tables_ms;
+  double upload_gather_ms, upload_wait_ms;
 } pqg_batch_stats;
 
 int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const int *leaves, int nleaves, int flags,

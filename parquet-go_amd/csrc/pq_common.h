@@ -138,16 +138,16 @@ struct ZeroRange {
 constexpr int LD_WAVES_H = 4;             // waves of a k_expand_mix workgroup
 constexpr int LD_LDS_MAX = 160 * 1024;    // LDS of one CU (gfx950)
 constexpr int LD_MIX_MAX = 32 * 1024;     // k_expand_mix LDS per workgroup with a dictionary (default)
-// k_expand_big: dictionaries past LD_MIX_MAX that still fit one CU's LDS beside
-// BIG_WAVES waves' staged keys; one workgroup of BIG_WAVES waves per group,
-// its own launch (the dynamic LDS size is per launch)
-constexpr int BIG_WAVES = 8;
-constexpr int BIG_JOBS = 16;              // jobs per group (default; PQG_BIG_JOBS)
-// k_expand_pass: workgroups of PASS_WAVES_H waves (one job each) streaming a
-// dictionary too large for LDS through it in slices of the launch's LDS
-// (PQG_PASS_WAVES=8: half-size workgroups and slices, two per CU)
-int pass_waves_h();
-inline int pass_waves(int width) { return width == 4 ? pass_waves_h() : pass_waves_h() / 2; }
+// k_expand_wg: chunks whose dictionary is past the mixed launch's LDS groups,
+// up to WG_MAX_SLICES slices of a CU's LDS (a workgroup of 16 waves a CU);
+// groups of WG_JOBS jobs by default
+#ifndef PQ_WG_WAVES
+#define PQ_WG_WAVES 16
+#endif
+constexpr int WG_WAVES = PQ_WG_WAVES;
+constexpr uint32_t WG_SLICE = 160 * 1024;  // LDS bytes of a slice (the CU's LDS)
+constexpr int WG_MAX_SLICES = 4;
+constexpr int WG_JOBS = 64;
 constexpr int PLAIN_STR_ITEM = 2048;      // k_plain_str: values per work item
 struct LdsGroup {
   int32_t job0, njobs;   // jobs [job0, job0 + njobs) of the launch order

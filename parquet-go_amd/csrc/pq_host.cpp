@@ -35,13 +35,6 @@
 #include "../../include/pqgpu.h"
 #include "pq_common.h"
 
-namespace pq {
-// k_expand_pass workgroup size (PQG_PASS_WAVES=8: half-size groups and slices)
-int pass_waves_h() {
-  static const int n = getenv("PQG_PASS_WAVES") && atoi(getenv("PQG_PASS_WAVES")) == 8 ? 8 : 16;
-  return n;
-}
-}  // namespace pq
 
 
 using namespace pq;
@@ -607,8 +600,10 @@ struct pqg_ctx {
 // while the DMA of the previous one runs); alignment gaps are zeroed.  The
 // DMAs are queued on `s` and the call returns without waiting for the last
 // ones (a later upload waits for a buffer's event before refilling it).
+static bool getenv_flag(const char *name);
 template <class Layout>
-static int ring_upload(pqg_ctx *c, uint8_t *dst, const Layout &in, hipStream_t s) {
+static int ring_upload(pqg_ctx *c, uint8_t *dst, const Layout &in, hipStream_t s, double *gather_ms = nullptr,
+                       double *wait_ms = nullptr) {
   const size_t n = in.n;
   std::lock_guard<std::mutex> lk(c->upload_mu);
   if (!c->pin[0]) {
@@ -637,7 +632,16 @@ static int ring_upload(pqg_ctx *c, uint8_t *dst, const Layout &in, hipStream_t s
     const int k = c->pin_next;
     const size_t m = std::min(pqg_ctx::kRingBytes, n - off);
     auto t0 = now();
-    if (c->pin_busy[k] && hipEventSynchronize(c->pin_ev[k]) != hipSuccess) return 1;
+    static const bool poll = getenv_flag("PQG_RING_POLL");
+    if (c->pin_busy[k]) {
+      if (poll) {  // (analysis: busy-poll the buffer's event instead of a blocking wait)
+        hipError_t q;
+        while ((q = hipEventQuery(c->pin_ev[k])) == hipErrorNotReady) std::this_thread::yield();
+        if (q != hipSuccess) return 1;
+      } else if (hipEventSynchronize(c->pin_ev[k]) != hipSuccess) {
+        return 1;
+      }
+    }
     auto t1 = now();
     t_wait += std::chrono::duration<double, std::milli>(t1 - t0).count();
     c->pin_busy[k] = false;
@@ -675,6 +679,8 @@ static int ring_upload(pqg_ctx *c, uint8_t *dst, const Layout &in, hipStream_t s
     off += m;
     c->pin_next = (k + 1) % pqg_ctx::kRingBufs;
   }
+  if (gather_ms) *gather_ms += t_gather;
+  if (wait_ms) *wait_ms += t_wait;
   if (trace)
     fprintf(stderr, "ring_upload %.1f MB: gather %.2f ms (%.1f GB/s, %d threads), ring wait %.2f ms\n", n / 1e6, t_gather,
             t_gather > 0 ? n / t_gather / 1e6 : 0.0, nthreads, t_wait);
@@ -797,6 +803,7 @@ struct pqg_batch {
   uint64_t *d_dbg = nullptr;     // diagnostic stamps (PQ_STAMPS builds only)
   uint64_t *d_dbg2 = nullptr;
   void *d_runs = nullptr;        // run tables (k_prepare's run walk -> k_expand)
+  void *d_runs_alloc = nullptr;  // the allocation d_runs lives in (PQG_DEBUG_INPUT_HIGH_WORD shifts it too)
   void *d_tile_info = nullptr;     // per RUN_TILE values of a tiled page: {first run, first key byte}
   int32_t ex_lds = 0;              // k_expand staged key bytes per wave
   void *d_recs = nullptr;          // k_expand job records (k_prepare writes them every decode)
@@ -806,8 +813,10 @@ struct pqg_batch {
   TileJob *d_tiles = nullptr;
   std::vector<LdsGroup> lgroups;     // k_expand_ld groups, 4-byte columns first
   LdsGroup *d_lgroups = nullptr;
+  double create_ms[4] = {};          // host time of pqg_batch_create: plan, alloc, upload, outputs + tables
+  double upload_gather_ms = 0, upload_wait_ms = 0;  // inside upload: pinned-ring gather, ring-buffer waits
   int32_t ldn[6] = {}, ldl[6] = {};  // groups and LDS bytes: [0], [1] k_expand_mix (width 4, 8),
-                                     // [2], [3] k_expand_big (width 4, 8)
+                                     // [2], [3] k_expand_wg (width 4, 8)
   std::vector<ColDesc> hcols;
   // timing: a ring of event sets, one per decode, harvested by pqg_batch_kernel_times
   static constexpr int kRing = 64;
@@ -1938,13 +1947,16 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     cp.levels = 0;
     B->cols.push_back(cp);
   }
-  // PQG_TRACE_CREATE=1: host time of each batch-creation phase on stderr
+  // host time of each batch-creation phase (pqg_batch_stats::create_*_ms;
+  // PQG_TRACE_CREATE=1: also on stderr)
   const bool trace = getenv("PQG_TRACE_CREATE") != nullptr;
   auto t_last = std::chrono::steady_clock::now();
+  int nphase = 0;
   auto phase = [&](const char *what) {
-    if (!trace) return;
     auto t = std::chrono::steady_clock::now();
-    fprintf(stderr, "pqg_batch_create %-14s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
+    const double ms = std::chrono::duration<double, std::milli>(t - t_last).count();
+    if (nphase < 4) B->create_ms[nphase++] = ms;
+    if (trace) fprintf(stderr, "pqg_batch_create %-14s %8.2f ms\n", what, ms);
     t_last = t;
   };
   HostBuf in;
@@ -2052,18 +2064,13 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   // the machine for the whole launch.
   B->ex_lds = (B->ex_lds + 255) & ~255;  // LDS-DMA pieces of 16 bytes per lane, the last one partial
   const bool ld_off = getenv("PQG_NO_LDS_DICT") != nullptr;
-  std::vector<TileJob> slot_tiles, ld_tiles, big_tiles, pass_tiles;
-  std::vector<LdsGroup> big_groups[2], pass_groups[2];
+  std::vector<TileJob> slot_tiles, ld_tiles, big_tiles;
+  std::vector<LdsGroup> big_groups[2];
   const int64_t ld_max = getenv("PQG_LD_MAX_KB") ? 1024 * (int64_t)atoi(getenv("PQG_LD_MAX_KB")) : LD_MIX_MAX;
-  const int64_t big_jobs = getenv("PQG_BIG_JOBS") ? std::max(1, atoi(getenv("PQG_BIG_JOBS"))) : BIG_JOBS;
-  // which chunks fit the mixed launch's LDS groups, or only k_expand_big's
-  // k_expand_pass (opt-in, PQG_PASS=1; measured slower than the L1/L2
-  // gathers it replaces): dictionaries past the mixed launch's
-  // LDS groups up to PQG_PASS_MAX_KB (default 1 MiB)
-  static const bool pass_on = getenv("PQG_PASS") != nullptr && getenv("PQG_PASS")[0] == '1';
-  static const int64_t pass_max =
-      getenv("PQG_PASS_MAX_KB") ? 1024 * (int64_t)atoi(getenv("PQG_PASS_MAX_KB")) : (int64_t)1 << 20;
-  const int64_t pass_lds = pass_waves_h() == 16 ? LD_LDS_MAX : LD_LDS_MAX / 2;
+  // which chunks fit the mixed launch's LDS groups (class 1), or k_expand_wg's
+  // workgroup-a-CU form (class 2: the dictionary in at most WG_MAX_SLICES
+  // slices of a CU's LDS), else the mixed launch's L1/L2 blocks
+  bool wg_off = false;
   auto ld_class = [&](const std::vector<TileJob> &ct, int32_t W, int64_t &dbytes, int32_t &ks) {
     dbytes = 0;
     ks = 0;
@@ -2075,27 +2082,28 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     if (dbytes <= 0 || ks <= 0) return 0;
     const bool amortised = dbytes * 4 <= J * EX_WAVE_VALUES * W;
     if (amortised && dbytes + (int64_t)LD_WAVES_H * ks <= ld_max) return 1;
-    if (pass_on && dbytes <= pass_max && (int64_t)pass_waves(W) * ks <= pass_lds) return 3;
-    if (amortised && dbytes + (int64_t)BIG_WAVES * ks <= LD_LDS_MAX) return 2;
+    // (8-byte values: one slice at most — k_expand_wg keeps no sliced form for them)
+    if (!wg_off && dbytes <= (int64_t)(W == 4 ? WG_MAX_SLICES : 1) * WG_SLICE && dbytes <= J * EX_WAVE_VALUES * W)
+      return 2;
     return 0;
   };
-  // k_expand_big is its own launch: it pays when its chunks are a good part
-  // of the tiled jobs (measured: single-width files at bit widths 13-15 gain
-  // 45-70 %; in C2, where they are 15 % of the jobs beside L2-bound blocks of
-  // wider dictionaries that hide them, the extra launch costs 13 %).
+  // k_expand_wg is its own launch after the mixed one: it pays when its chunks
+  // are a good part of the tiled jobs (single-width files at bit widths 13-17:
+  // 1.3-2.4x the L1/L2 rates); in C2, where they are a quarter of the jobs,
+  // the mixed launch's L1/L2 blocks run beside its LDS groups while the extra
+  // launch runs alone (measured: C2 decode phase 0.193 -> 0.212 ms with it).
   // PQG_BIG=1 / PQG_NO_BIG=1 force it on / off.
-  bool big_off;
   {
-    int64_t nbig = 0, nall = 0;
+    int64_t nwg = 0, nall = 0;
     for (const auto &ct : chunk_tiles) {
       if (ct.empty()) continue;
       const int32_t W = B->cols[(size_t)B->pages[(size_t)ct[0].page].col].info.value_width;
       int64_t db;
       int32_t ks;
       nall += (int64_t)ct.size();
-      if (ld_class(ct, W, db, ks) == 2) nbig += (int64_t)ct.size();
+      if (ld_class(ct, W, db, ks) == 2) nwg += (int64_t)ct.size();
     }
-    big_off = getenv("PQG_NO_BIG") != nullptr || (getenv("PQG_BIG") == nullptr && nbig * 3 < nall);
+    wg_off = getenv("PQG_NO_BIG") != nullptr || (getenv("PQG_BIG") == nullptr && nwg * 3 < nall);
   }
   for (int ws = 0; ws < 2; ws++) {
     const int32_t W = ws == 0 ? 4 : 8;
@@ -2107,7 +2115,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     std::vector<LdG> ldg;
     std::vector<std::vector<TileJob>> bins(8);
     std::vector<const std::vector<TileJob> *> gchunks;  // chunks gathering through L1/L2
-    std::vector<std::pair<const std::vector<TileJob> *, int32_t>> pass_chunks;  // (chunk, kspan)
+    std::vector<std::pair<const std::vector<TileJob> *, int64_t>> wg_chunks;  // (chunk, dictionary bytes)
     for (const auto &ct : chunk_tiles) {
       if (ct.empty() || B->cols[(size_t)B->pages[(size_t)ct[0].page].col].info.value_width != W) continue;
       bool ld = false;
@@ -2125,30 +2133,12 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
           for (int64_t q = 0; q < ng; q++) ldg.push_back({&ct, q * J / ng, (q + 1) * J / ng, (int32_t)dbytes, ks});
           ld = true;
           B->pages[(size_t)ct[0].dict].alias_any = 1;  // copied into LDS with a funnel shift anyway
-        } else if (cls == 3) {
-          // k_expand_pass: groups of pass_waves(W) jobs; a chunk's groups go
-          // to one XCD residue (its dictionary stays in that L2), chunks
-          // dealt to the least-loaded residue
-          pass_chunks.push_back({&ct, ks});
+        } else {
+          // k_expand_wg: groups of WG_JOBS jobs (one round of WG_WAVES jobs when
+          // the dictionary is sliced: every round streams the whole of it)
+          wg_chunks.push_back({&ct, dbytes});
           ld = true;
           B->pages[(size_t)ct[0].dict].alias_any = 1;  // copied into LDS with a funnel shift
-        } else if (!big_off) {
-          // a dictionary past the mixed launch's LDS that one CU holds beside
-          // BIG_WAVES waves' keys: groups of big_jobs jobs in k_expand_big
-          const int64_t ng = (J + big_jobs - 1) / big_jobs;
-          for (int64_t q = 0; q < ng; q++) {
-            LdsGroup g = {};
-            g.job0 = -1 - (int32_t)big_tiles.size();  // rebased below
-            for (int64_t j = q * J / ng; j < (q + 1) * J / ng; j++) big_tiles.push_back(ct[(size_t)j]);
-            g.njobs = (int32_t)((q + 1) * J / ng - q * J / ng);
-            g.dpage = ct[0].dict;
-            g.dict_bytes = (int32_t)dbytes;
-            g.kspan = ks;
-            big_groups[ws].push_back(g);
-            B->ldl[2 + ws] = std::max(B->ldl[2 + ws], (int32_t)(dbytes + (int64_t)BIG_WAVES * ks));
-          }
-          ld = true;
-          B->pages[(size_t)ct[0].dict].alias_any = 1;
         }
       }
       if (!ld) gchunks.push_back(&ct);
@@ -2246,29 +2236,35 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
       else lr++;
     }
     B->ldn[ws] = (int32_t)B->lgroups.size() - nb0;
-    if (!pass_chunks.empty()) {
+    if (!wg_chunks.empty()) {
+      // a chunk's groups go to one XCD residue (its dictionary stays in that
+      // L2), chunks dealt to the least-loaded residue by their cost (jobs x
+      // slices), largest first; then rounds of 8 blocks (block b on XCD b % 8)
+      static const int64_t wg_jobs = getenv("PQG_WG_JOBS") ? std::max(1, atoi(getenv("PQG_WG_JOBS"))) : WG_JOBS;
       std::vector<std::vector<LdsGroup>> res(8);
       int64_t load[8] = {};
-      std::stable_sort(pass_chunks.begin(), pass_chunks.end(),
-                       [](const auto &x, const auto &y) { return x.first->size() > y.first->size(); });
-      for (auto &pc : pass_chunks) {
-        const std::vector<TileJob> &ct = *pc.first;
+      auto slices = [&](int64_t db) { return (db + WG_SLICE - 1) / WG_SLICE; };
+      std::stable_sort(wg_chunks.begin(), wg_chunks.end(), [&](const auto &x, const auto &y) {
+        return (int64_t)x.first->size() * slices(x.second) > (int64_t)y.first->size() * slices(y.second);
+      });
+      for (auto &wc : wg_chunks) {
+        const std::vector<TileJob> &ct = *wc.first;
         size_t q = 0;
         for (size_t r = 1; r < 8; r++)
           if (load[r] < load[q]) q = r;
         const int64_t J = (int64_t)ct.size();
-        const int64_t ng = (J + pass_waves(W) - 1) / pass_waves(W);
+        const int64_t G = slices(wc.second) > 1 ? WG_WAVES : wg_jobs;
+        const int64_t ng = (J + G - 1) / G;
         for (int64_t k = 0; k < ng; k++) {
           LdsGroup g = {};
-          g.job0 = -1 - (int32_t)pass_tiles.size();  // rebased below
-          for (int64_t jj = k * J / ng; jj < (k + 1) * J / ng; jj++) pass_tiles.push_back(ct[(size_t)jj]);
+          g.job0 = -1 - (int32_t)big_tiles.size();  // rebased below
+          for (int64_t jj = k * J / ng; jj < (k + 1) * J / ng; jj++) big_tiles.push_back(ct[(size_t)jj]);
           g.njobs = (int32_t)((k + 1) * J / ng - k * J / ng);
           g.dpage = ct[0].dict;
-          g.dict_bytes = pass_lds;  // slice bytes: the launch's whole LDS
-          g.kspan = pc.second;
+          g.dict_bytes = (int32_t)wc.second;
           res[q].push_back(g);
         }
-        load[q] += J;
+        load[q] += J * slices(wc.second);
       }
       size_t rounds = 0;
       for (auto &v : res) rounds = std::max(rounds, v.size());
@@ -2277,9 +2273,8 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
           LdsGroup g = {};
           g.dpage = -1;
           if (r < res[q].size()) g = res[q][r];
-          pass_groups[ws].push_back(g);
+          big_groups[ws].push_back(g);
         }
-      B->ldl[4 + ws] = (int32_t)pass_lds;
     }
   }
   // job indices are relative to the launch's first slot (the 8-byte launch
@@ -2289,29 +2284,19 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     if (g.job0 < 0) g.job0 = (int32_t)slot_tiles.size() + (-1 - g.job0);
     if (b >= (size_t)B->ldn[0]) g.job0 -= B->ldn[0] * LD_WAVES_H;
   }
-  // k_expand_big groups after the mixed ones, with absolute job indices (their
+  // k_expand_wg groups after the mixed ones, with absolute job indices (their
   // launches start at the first slot)
   const size_t big_base = slot_tiles.size() + ld_tiles.size();
   for (int ws = 0; ws < 2; ws++) {
     for (LdsGroup g : big_groups[ws]) {
-      g.job0 = (int32_t)big_base + (-1 - g.job0);
+      if (g.njobs > 0) g.job0 = (int32_t)big_base + (-1 - g.job0);
       B->lgroups.push_back(g);
     }
     B->ldn[2 + ws] = (int32_t)big_groups[ws].size();
   }
-  // k_expand_pass groups last, absolute job indices
-  const size_t pass_base = big_base + big_tiles.size();
-  for (int ws = 0; ws < 2; ws++) {
-    for (LdsGroup g : pass_groups[ws]) {
-      if (g.njobs > 0) g.job0 = (int32_t)pass_base + (-1 - g.job0);
-      B->lgroups.push_back(g);
-    }
-    B->ldn[4 + ws] = (int32_t)pass_groups[ws].size();
-  }
   B->tiles = std::move(slot_tiles);
   B->tiles.insert(B->tiles.end(), ld_tiles.begin(), ld_tiles.end());
   B->tiles.insert(B->tiles.end(), big_tiles.begin(), big_tiles.end());
-  B->tiles.insert(B->tiles.end(), pass_tiles.begin(), pass_tiles.end());
 
   // k_snappy takes pages in list order, one wave each: the longest bodies
   // first (longest-processing-time order), so that the long serial token
@@ -2545,7 +2530,20 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   rc |= alloc_dev(&B->d_recs, sizeof(ExRec) * (B->tiles.size() + 1));
   rc |= alloc_dev((void **)&B->d_cols, sizeof(ColDesc) * B->cols.size());
   rc |= alloc_dev((void **)&B->d_dict, sizeof(uint64_t) * (size_t)B->dict_entries);
-  rc |= alloc_dev(&B->d_runs, 8 * (size_t)(B->run_entries + 64));
+  if (getenv("PQG_DEBUG_INPUT_HIGH_WORD") && 8 * (size_t)(B->run_entries + 64) < (1u << 30)) {
+    // the same for the run tables (k_expand_wg widens a record's run-table
+    // pointer from two lane words)
+    const size_t n = 8 * (size_t)(B->run_entries + 64);
+    rc |= alloc_dev(&B->d_runs_alloc, n + (size_t{1} << 32));
+    if (!rc) {
+      const uint32_t lw = (uint32_t)(uintptr_t)B->d_runs_alloc;
+      const bool ok = lw >= 0x80000000u && (uint64_t)lw + n <= 0xFFFFFFFFull;
+      B->d_runs = (uint8_t *)B->d_runs_alloc + (ok ? 0 : (size_t)(uint32_t)(0x80000000u - lw));
+    }
+  } else {
+    rc |= alloc_dev(&B->d_runs, 8 * (size_t)(B->run_entries + 64));
+    B->d_runs_alloc = B->d_runs;
+  }
   rc |= alloc_dev(&B->d_tile_info, 8 * (size_t)(B->tile_entries + EX_WAVE_VALUES / RUN_TILE + 1));
   rc |= alloc_dev((void **)&B->d_tiles, sizeof(TileJob) * (B->tiles.size() + 1));
   rc |= alloc_dev(&B->d_jobs, 32 * (size_t)B->max_jobs);
@@ -2566,7 +2564,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   // one upload of all chunk bytes through the context's pinned ring, queued on
   // the upload stream (decodes wait on `ready`; the host goes on planning)
   {
-    if (in_bytes && ring_upload(ctx, B->d_in, in, ctx->upload)) {
+    if (in_bytes && ring_upload(ctx, B->d_in, in, ctx->upload, &B->upload_gather_ms, &B->upload_wait_ms)) {
       set_err("input upload failed");
       return PQG_ERR_DEVICE;
     }
@@ -3084,7 +3082,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
       e |= pq_launch(10, &a, s);
     }
     a.nlist = (int32_t)B->tiles.size();
-    // k_expand_big (dictionaries that need a CU's LDS): after the mixed
+    // k_expand_wg (dictionaries that need a CU's LDS): after the mixed
     // launch, before it (PQG_BIG_ORDER=1) or beside it on a side stream (=2)
     static const int big_order = getenv("PQG_BIG_ORDER") ? atoi(getenv("PQG_BIG_ORDER")) : 0;
     const bool big = B->ldn[2] + B->ldn[3] > 0;
@@ -3113,7 +3111,6 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     }
     if (big && big_order == 0) e |= pq_launch(22, &a, s);
     if (big && big_order == 2) hipStreamWaitEvent(s, LN.join[1], 0);
-    if (B->ldn[4] + B->ldn[5] > 0) e |= pq_launch(27, &a, s);  // k_expand_pass (wide dictionaries)
     if (B->ngen_flat > 0) hipStreamWaitEvent(s, LN.join[0], 0);
     if (B->ngen_nest > 0) hipStreamWaitEvent(s, LN.join[2], 0);
     mark(true);
@@ -3282,6 +3279,12 @@ int pqg_batch_stats_get(const pqg_batch *B, pqg_batch_stats *o) {
   o->host_inflated_pages = B->host_inflated;
   o->staged_bytes = B->staged_bytes;
   o->h2d_bytes = B->h2d_bytes;
+  o->create_plan_ms = B->create_ms[0];
+  o->create_alloc_ms = B->create_ms[1];
+  o->create_upload_ms = B->create_ms[2];
+  o->create_tables_ms = B->create_ms[3];
+  o->upload_gather_ms = B->upload_gather_ms;
+  o->upload_wait_ms = B->upload_wait_ms;
   // B_in: stored payload bytes of the planned pages
   int64_t bin = 0;
   for (auto &d : B->pages) {
@@ -3365,7 +3368,7 @@ void pqg_batch_destroy(pqg_batch *B) {
   free_dev(B->d_lvl);
   free_dev(B->d_dbg);
   free_dev(B->d_dbg2);
-  free_dev(B->d_runs);
+  free_dev(B->d_runs_alloc);
   free_dev(B->d_tile_info);
   free_dev(B->d_tiles);
   free_dev(B->d_segs);

@@ -125,11 +125,31 @@ struct KArgs {
       sl_[6] = t_;                                                                            \
     }                                                                                         \
   } while (0)
+// k_expand_wg: the same slots per wave of its 16-wave workgroups
+#define WSTAMP(i)                                                                             \
+  do {                                                                                        \
+    if (a.dbg && lane_id() == 0) {                                                            \
+      const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                                   \
+      uint64_t *sl_ = a.dbg + ((size_t)blockIdx.x * WG_WAVES + (threadIdx.x >> 6)) * 8;       \
+      if ((i) == 0) {                                                                         \
+        sl_[0] = t_;                                                                          \
+        sl_[7] = 0;                                                                           \
+        for (int q_ = 1; q_ < 6; q_++) sl_[q_] = 0;                                           \
+      } else {                                                                                \
+        sl_[(i)] += t_ - sl_[6];                                                              \
+        if ((i) == 2) sl_[7] += 1;                                                            \
+      }                                                                                       \
+      sl_[6] = t_;                                                                            \
+    }                                                                                         \
+  } while (0)
 #define PSTAMP(page, i, v)                              \
   do {                                                   \
     if (a.dbg2 && lane_id() == 0) a.dbg2[(size_t)(page) * 8 + (i)] = (v); \
   } while (0)
 #else
+#define WSTAMP(i) \
+  do {                 \
+  } while (0)
 #define PSTAMP(page, i, v) \
   do {                     \
   } while (0)
@@ -5084,116 +5104,211 @@ __device__ __forceinline__ void expand_job(const KArgs &a, const TileJob &tj, co
 
 
 // ===========================================================================
-// K5p: k_expand_pass — RLE_DICTIONARY jobs whose dictionary is too large for
-// the mixed launch's LDS groups (C2's bit widths 14-20: 64 KiB .. 4 MiB).
-// Gathering those through L1/L2 is bound by the L2's request rate (about one
-// request per value, ~230 Gvalues/s for the whole chip); here a workgroup of
-// pass_waves(WIDTH) waves takes pass_waves(WIDTH) jobs of one chunk, extracts their keys into
-// registers (staged key bytes in LDS, as k_expand_mix does), and then streams
-// the dictionary through its LDS in slices of the launch's whole LDS: per
-// slice, every key inside it gathers with ds_read.  The dictionary reaches
-// the CU as 16-byte loads (a slice is ~1-3 K L2 requests instead of one per
-// value), at the cost of one pass over the keys per slice; the host sends
-// only dictionaries of a few slices here (PQG_PASS_MAX_KB).
+// K5w: k_expand_wg — RLE_DICTIONARY chunks whose dictionary is past the mixed
+// launch's LDS groups (C2's bit widths 13-17: 32 KiB .. 640 KiB).  Gathering
+// those through L1/L2 is bound by the L2's request rate (one 128-byte line a
+// value: ~250-300 Gvalues/s for the whole chip, tools/gather_bench2.hip,
+// whatever the load's cache policy); from LDS the same gathers run at ~1,150.
+// One 1,024-thread workgroup a CU (sixteen waves) owns the CU's whole LDS:
+//  * the dictionary fits (<= WG_SLICE bytes): copied once, then the waves take
+//    the group's jobs in turn and gather with ds_read;
+//  * otherwise (at most WG_SLICES slices): the group's jobs go in rounds of
+//    sixteen, one a wave; a round's keys are extracted into registers, then
+//    the dictionary streams through the LDS slice by slice and every key
+//    inside a slice gathers from it (the L2 serves whole lines of the
+//    dictionary instead of one line a value).
+// Keys are read straight from the key stream into registers (no LDS staging:
+// the LDS is the dictionary's): per row of 256 values a lane loads the 16
+// bytes holding its four keys; a lane where a run starts among them loads the
+// next run's first bytes too; rows the fast form does not cover (RLE runs,
+// the stream's end, a page's last partial row) load each key's 8 bytes.
 // ===========================================================================
 
-// The keys of job tj (values [v0, lim) of its page) into key[][][] (value
-// v0 + 256 r + 4 lane + q -> key[r / HR][r % HR][q]), with the run-window and
-// staging logic of expand_job.  Returns 0 (keys valid, every one < dict_n),
-// 1 (the job does not fit the staged form: the caller decodes it with
-// expand_direct) or 2 (a dictionary index out of range: status set).
-template <int WIDTH>
-__device__ __forceinline__ int job_keys(const KArgs &a, const TileJob &tj, const ExRec &rc, uint32_t *kspan,
-                                        int ex_lds, uint32_t (&key)[2][EX_ROWS / 2][4]) {
-  constexpr int HR = EX_ROWS / 2;
+// bits [o, o + 32) of the 128-bit little-endian value d, o < 96
+__device__ __forceinline__ uint32_t bits_at(const u32x4 &d, uint32_t o) {
+  const uint32_t s = o & 31, i = o >> 5;
+  const uint32_t x0 = __builtin_amdgcn_alignbit(d.y, d.x, s);
+  const uint32_t x1 = __builtin_amdgcn_alignbit(d.z, d.y, s);
+  const uint32_t x2 = __builtin_amdgcn_alignbit(d.w, d.z, s);
+  return i == 0 ? x0 : i == 1 ? x1 : x2;
+}
+
+// A job's ExRec and TileJob as ONE lane-distributed vector load (lane l < 16:
+// dword l of the record, lanes 16..23: dword l - 16 of the tile entry), so a
+// wave loads its next jobs' descriptors ahead under vmcnt: a scalar load in
+// flight would be waited for by the first LDS read of the job in between.
+__device__ __forceinline__ uint32_t job_load(const KArgs &a, int j) {
+  const int lane = lane_id();
+  const uint32_t *p = lane < 16 ? (const uint32_t *)(a.recs + j) + lane : (const uint32_t *)(a.tiles + j) + (lane & 7);
+  return *p;
+}
+__device__ __forceinline__ void job_unpack(uint32_t v, TileJob &tj, ExRec &rc) {
+  union {
+    ExRec r;
+    uint32_t d[16];
+  } ur;
+  union {
+    TileJob t;
+    uint32_t d[8];
+  } ut;
+#pragma unroll
+  for (int i = 0; i < 16; i++) ur.d[i] = __builtin_amdgcn_readlane(v, i);
+#pragma unroll
+  for (int i = 0; i < 8; i++) ut.d[i] = __builtin_amdgcn_readlane(v, 16 + i);
+  rc = ur.r;
+  tj = ut.t;
+}
+
+// a vector-held descriptor's job is a live RLE_DICTIONARY job (record of
+// this decode, values to decode, not PLAIN); its run window
+__device__ __forceinline__ bool job_dict_live(const KArgs &a, uint32_t v) {
+  const uint32_t ep = __builtin_amdgcn_readlane(v, 14);
+  const int32_t v0 = (int32_t)__builtin_amdgcn_readlane(v, 6), lim = (int32_t)__builtin_amdgcn_readlane(v, 7);
+  const int32_t bw = (int32_t)__builtin_amdgcn_readlane(v, 8);
+  return rec_live(ep, a.epoch) && v0 < lim && bw >= 0;
+}
+__device__ __forceinline__ void job_window(RunWin &W, uint32_t v) {
+  // (readlane returns int: each word through uint32_t, or a low word with bit 31 set sign-extends)
+  const uint64_t rp = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(v, 5) << 32) | (uint32_t)__builtin_amdgcn_readlane(v, 4);
+  W.load((const uint2 *)rp, (int32_t)__builtin_amdgcn_readlane(v, 9), (int32_t)__builtin_amdgcn_readlane(v, 10));
+}
+
+// The keys of job tj (values [v0, lim) of its page) into key[r][q] (value
+// v0 + 256 r + 4 lane + q), read from the key stream without staging; W: the
+// job's run window (RunWin::load(rc.runs, rc.nr, rc.first_run), loaded ahead).
+// Returns 0 (keys valid, each < dict_n), 1 (the job is outside this form:
+// more runs than the window holds, two run starts in one row, a lane where
+// runs start in two rows, or a bit width past 20 — the caller uses
+// expand_direct) or 2 (a dictionary index out of range: status set,
+// type_dict.go:51-53).
+__device__ __forceinline__ int keys_direct(const KArgs &a, const TileJob &tj, const ExRec &rc, const RunWin &W,
+                                           uint32_t (&key)[EX_ROWS][4]) {
   const int lane = lane_id();
   const int32_t v0 = rc.v0, lim = rc.lim;
   const int bw = rc.bw;
+  if (bw > 20) return 1;
   const uint8_t *ks = rc.vals + 1;
-  const int64_t slen = (int64_t)rc.val_len - 1;
-  RunWin W;
-  W.load(rc.runs, rc.nr, rc.first_run);
-  const int64_t byte_lo = rc.byte_lo, byte_hi = (int64_t)rc.byte_hi + 16;
-  const uintptr_t A = ((uintptr_t)ks + (uintptr_t)byte_lo) & ~(uintptr_t)15;
-  const int64_t nb = (int64_t)((uintptr_t)ks + (uintptr_t)byte_hi - A);
-  const bool staged = nb <= ex_lds;
-  if (staged) {
-    const uintptr_t src = A + 16 * (uintptr_t)lane;
-    for (int32_t off = 0; off < nb; off += 1024)
-      if (off + 16 * lane < nb)
-        __builtin_amdgcn_global_load_lds((const void *)(src + off),
-                                         (__attribute__((address_space(3))) void *)(kspan + off / 4), 16, 0, 0);
-  }
+  const int32_t slen = rc.val_len - 1;
+  // every run meeting [v0, lim) must sit in lanes 0..62 (its end is the next lane's start),
+  // and no row of EX_ROW values may hold two run starts (rows meet at most two runs)
   const int32_t rs = W.start > v0 && W.start < lim && ((W.start - v0) & (EX_ROW - 1)) ? (W.start - v0) / EX_ROW : -1 - lane;
   const int32_t rs_next = (int32_t)shfl32((uint32_t)rs, min(lane + 1, 63));
-  const bool fits = staged && (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, 63) >= lim &&
-                    !ballot(lane < 63 && rs >= 0 && rs == rs_next);
-  if (!fits) return 1;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the staged bytes (LDS-DMA) and the window
-  const int64_t lbase = (int64_t)(A - (uintptr_t)ks) * 8;
-  const int32_t end_bit32 = (int32_t)(slen * 8);
-  const uint32_t mask = bw >= 32 ? 0xffffffffu : ((1u << bw) - 1);
+  if ((int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, 63) < lim || ballot(lane < 63 && rs >= 0 && rs == rs_next))
+    return 1;
+  // the key stream as a buffer from its first aligned dword, 20 bytes past its
+  // end readable (a page's body is followed by >= 16 bytes of the batch's
+  // buffers: the next 16-byte aligned body or the input's pad), so a 16-byte
+  // load holding a stream's last keys is never cut by the range check; bits
+  // past the end are masked off below (general rows) or never used (fast rows)
+  const uintptr_t kb = (uintptr_t)ks & ~(uintptr_t)3;
+  const int32_t ksh = (int32_t)((uintptr_t)ks & 3) * 8;
+  const __amdgpu_buffer_rsrc_t krs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)kb, (short)0, (int)((uint32_t)slen + 20u), 0x00020000);
+  const uint32_t mask = (1u << bw) - 1;
   const int32_t w_end = (int32_t)shfl32((uint32_t)W.start, min(lane + 1, 63));
-  const int32_t w_c = (int32_t)(W.prm * 8) - W.start * bw - (int32_t)lbase;
+  // per window lane (run): the buffer bit of its key j is w_c + j * bw; okm marks
+  // bit-packed runs whose keys all lie inside the stream (the fast rows)
+  const int32_t w_c = (int32_t)(W.prm * 8) + ksh - W.start * bw;
   const uint64_t okm = ballot(!W.rle && W.start != 0x7fffffff &&
-                              (int64_t)W.prm * 8 + (int64_t)(min(w_end, lim) - W.start) * bw <= slen * 8);
-  bool bad = false;
-  uint32_t kmax = 0;
+                              (int64_t)W.prm * 8 + (int64_t)(min(w_end, lim) - W.start) * bw <= (int64_t)slen * 8);
+  // the rows' plan (wave-uniform): the run of the row start, the next run's
+  // start, fast = full, bit-packed only, inside the stream; and the one row
+  // where this lane's four keys meet a run start (a lane meeting two: outside)
+  int32_t ri[EX_ROWS], s1[EX_ROWS];
+  uint32_t fastm = 0;
+  int strow = -1, nst = 0;
 #pragma unroll
-  for (int h = 0; h < 2; h++) {
-#pragma unroll
-    for (int r = 0; r < HR; r++) {
-      const int32_t rl = v0 + (h * HR + r) * EX_ROW;
-      const int32_t j0 = rl + 4 * lane;
-#pragma unroll
-      for (int q = 0; q < 4; q++) key[h][r][q] = 0;
-      if (rl >= lim) continue;
-      const int32_t rh = min(rl + EX_ROW, lim);
-      const uint64_t m = ballot(W.start <= rl);
-      const int32_t ri = max((int32_t)__popcll(m) - 1, 0);
-      const int32_t s1 = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, ri + 1);
-      const int32_t c0 = (int32_t)__builtin_amdgcn_readlane((uint32_t)w_c, ri);
-      const bool one = s1 >= rh;
-      const bool fast = ((okm >> ri) & 1) && (one || ((okm >> (ri + 1)) & 1)) && rh - rl == EX_ROW;
-      if (fast) {  // full row, bit-packed runs only, nothing past the stream end
-        const int32_t c1 = one ? c0 : (int32_t)__builtin_amdgcn_readlane((uint32_t)w_c, ri + 1);
-        const uint32_t lb0 = (uint32_t)((j0 >= s1 ? c1 : c0) + j0 * bw);
-        if (bw <= 8) row_keys<0>(kspan, lb0, bw, mask, key[h][r]);
-        else if (bw <= 16) row_keys<1>(kspan, lb0, bw, mask, key[h][r]);
-        else row_keys<2>(kspan, lb0, bw, mask, key[h][r]);
-        if (!one && j0 < s1 && j0 + 3 >= s1) {  // the one lane of the row where a run starts
-#pragma unroll
-          for (int q = 0; q < 4; q++) {
-            const int32_t j = j0 + q;
-            const uint32_t lb = (uint32_t)((j >= s1 ? c1 : c0) + j * bw);
-            const uint32_t *dq = kspan + (lb >> 5);
-            key[h][r][q] = __builtin_amdgcn_alignbit(dq[1], dq[0], lb & 31) & mask;
-          }
-        }
-        kmax = max(kmax, max(max(key[h][r][0], key[h][r][1]), max(key[h][r][2], key[h][r][3])));
-        continue;
-      }
-      const int32_t s0 = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, ri);
-      const uint32_t p0 = __builtin_amdgcn_readlane(W.prm, ri), f0 = __builtin_amdgcn_readlane(W.rle, ri);
-      const uint32_t p1 = __builtin_amdgcn_readlane(W.prm, ri + 1), f1 = __builtin_amdgcn_readlane(W.rle, ri + 1);
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int32_t j = j0 + q;
-        const bool act = j < lim;
-        const bool sel = j >= s1;
-        const uint32_t pr = sel ? p1 : p0, fr = sel ? f1 : f0;
-        const int32_t sr = sel ? s1 : s0;
-        const int32_t bb = (int32_t)pr * 8 + (j - sr) * bw;
-        const uint32_t lb = (fr || !act) ? 0u : (uint32_t)(bb - (int32_t)lbase);
-        const uint32_t *dw = kspan + (lb >> 5);
-        uint32_t kv = __builtin_amdgcn_alignbit(dw[1], dw[0], lb & 31) & mask;
-        const int32_t avail = end_bit32 - bb;  // zero-fill past the stream end (hybrid_decoder.go:133-141)
-        kv &= avail >= bw ? 0xffffffffu : avail <= 0 ? 0u : ((1u << avail) - 1);
-        kv = fr ? pr : kv;
-        bad |= act && kv >= rc.dict_n;
-        key[h][r][q] = act ? kv : 0u;
+  for (int r = 0; r < EX_ROWS; r++) {
+    const int32_t rl = v0 + r * EX_ROW, j0 = rl + 4 * lane;
+    const int32_t rh = min(rl + EX_ROW, lim);
+    ri[r] = max((int32_t)__popcll(ballot(W.start <= rl)) - 1, 0);
+    s1[r] = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, ri[r] + 1);
+    const bool one = s1[r] >= rh;
+    if (rl < lim && ((okm >> ri[r]) & 1) && (one || ((okm >> (ri[r] + 1)) & 1)) && rh - rl == EX_ROW) {
+      fastm |= 1u << r;
+      if (!one && j0 < s1[r] && j0 + 3 >= s1[r]) {
+        strow = r;
+        nst++;
       }
     }
+  }
+  if (ballot(nst > 1)) return 1;
+  // 1. the fast rows' loads, all in flight together: 16 bytes from the lane's
+  //    first key, and at the straddling lane the next run's first bytes
+  u32x4 d[EX_ROWS], e = u32x4{0, 0, 0, 0};
+  uint32_t lbs = 0;
+#pragma unroll
+  for (int r = 0; r < EX_ROWS; r++) {
+    d[r] = u32x4{0, 0, 0, 0};
+    if (!((fastm >> r) & 1)) continue;
+    const int32_t j0 = v0 + r * EX_ROW + 4 * lane;
+    const int32_t c0 = (int32_t)__builtin_amdgcn_readlane((uint32_t)w_c, ri[r]);
+    const int32_t c1 = (int32_t)__builtin_amdgcn_readlane((uint32_t)w_c, ri[r] + 1);
+    const uint32_t lb0 = (uint32_t)((j0 >= s1[r] ? c1 : c0) + j0 * bw);
+    d[r] = __builtin_amdgcn_raw_buffer_load_b128(krs, (lb0 >> 5) * 4, 0, 0);
+    if (strow == r) {
+      lbs = (uint32_t)(c1 + s1[r] * bw);
+      e = __builtin_amdgcn_raw_buffer_load_b128(krs, (lbs >> 5) * 4, 0, 0);
+    }
+  }
+  bool bad = false;
+  uint32_t kmax = 0;
+  // 2. general rows (RLE runs, the stream's end, a page's last partial row):
+  //    each key's 8 bytes, a row at a time (rare)
+#pragma unroll
+  for (int r = 0; r < EX_ROWS; r++) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) key[r][q] = 0;
+    const int32_t rl = v0 + r * EX_ROW, j0 = rl + 4 * lane;
+    if (rl >= lim || ((fastm >> r) & 1)) continue;
+    const int32_t s0 = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, ri[r]);
+    const uint32_t p0 = __builtin_amdgcn_readlane(W.prm, ri[r]), f0 = __builtin_amdgcn_readlane(W.rle, ri[r]);
+    const uint32_t p1 = __builtin_amdgcn_readlane(W.prm, ri[r] + 1), f1 = __builtin_amdgcn_readlane(W.rle, ri[r] + 1);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int32_t j = j0 + q;
+      const bool act = j < lim;
+      const bool sel = j >= s1[r];
+      const uint32_t pr = sel ? p1 : p0, fr = sel ? f1 : f0;
+      const int32_t sr = sel ? s1[r] : s0;
+      const int32_t bb = (int32_t)pr * 8 + (j - sr) * bw;  // stream bit of the key (pages < 256 MiB)
+      const u32x2 y = (fr || !act) ? u32x2{0, 0}
+                                   : __builtin_amdgcn_raw_buffer_load_b64(krs, ((uint32_t)(bb + ksh) >> 5) * 4, 0, 0);
+      uint32_t kv = __builtin_amdgcn_alignbit(y.y, y.x, (uint32_t)(bb + ksh) & 31) & mask;
+      const int32_t avail = slen * 8 - bb;  // zero-fill past the stream end (hybrid_decoder.go:133-141)
+      kv &= avail >= bw ? 0xffffffffu : avail <= 0 ? 0u : ((1u << avail) - 1);
+      kv = fr ? pr : kv;
+      bad |= act && kv >= rc.dict_n;
+      key[r][q] = act ? kv : 0u;
+    }
+  }
+  // 3. the fast rows' keys
+#pragma unroll
+  for (int r = 0; r < EX_ROWS; r++) {
+    if (!((fastm >> r) & 1)) continue;
+    const int32_t j0 = v0 + r * EX_ROW + 4 * lane;
+    const int32_t c0 = (int32_t)__builtin_amdgcn_readlane((uint32_t)w_c, ri[r]);
+    const int32_t c1 = (int32_t)__builtin_amdgcn_readlane((uint32_t)w_c, ri[r] + 1);
+    const uint32_t sh = (uint32_t)((j0 >= s1[r] ? c1 : c0) + j0 * bw) & 31;
+    if (bw <= 8) {
+      const uint32_t x = __builtin_amdgcn_alignbit(d[r].y, d[r].x, sh);
+#pragma unroll
+      for (int q = 0; q < 4; q++) key[r][q] = __builtin_amdgcn_ubfe(x, (uint32_t)(q * bw), (uint32_t)bw);
+    } else if (bw <= 16) {
+      const uint64_t x = ((uint64_t)__builtin_amdgcn_alignbit(d[r].z, d[r].y, sh) << 32) |
+                         __builtin_amdgcn_alignbit(d[r].y, d[r].x, sh);
+#pragma unroll
+      for (int q = 0; q < 4; q++) key[r][q] = (uint32_t)(x >> (q * bw)) & mask;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; q++) key[r][q] = bits_at(d[r], sh + (uint32_t)(q * bw)) & mask;
+    }
+    if (strow == r) {  // keys from the run starting at s1: bits of e
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if (j0 + q >= s1[r]) key[r][q] = bits_at(e, (lbs & 31) + (uint32_t)((j0 + q - s1[r]) * bw)) & mask;
+    }
+    kmax = max(kmax, max(max(key[r][0], key[r][1]), max(key[r][2], key[r][3])));
   }
   if (ballot(bad || kmax >= rc.dict_n)) {
     set_status(a.status, tj.page, ST_VALUES, E_DICT);  // type_dict.go:51-53
@@ -5202,155 +5317,258 @@ __device__ __forceinline__ int job_keys(const KArgs &a, const TileJob &tj, const
   return 0;
 }
 
-template <int WIDTH, int NW>
-__global__ __launch_bounds__(NW * 64) void k_expand_pass(KArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
-  constexpr int HR = EX_ROWS / 2;
-  typedef typename std::conditional<WIDTH == 4, uint32_t, uint64_t>::type VT;
-  const LdsGroup g = sload(a.lgroups + blockIdx.x);
-  const int wv = (int)ufirst(threadIdx.x >> 6);
+// the job's values, 16 / 32 contiguous bytes per lane per row (as expand_job)
+template <int WIDTH, class VT>
+__device__ __forceinline__ void store_rows(const TileJob &tj, int32_t v0, int32_t lim, const VT (&val)[EX_ROWS][4]) {
   const int lane = lane_id();
-  const int j = g.job0 + wv;
-  TileJob tj = {};
-  ExRec rc = {};
-  bool act = false;
-  uint32_t key[2][HR][4];
-  VT val[2][HR][4];
+  const __amdgpu_buffer_rsrc_t ors =
+      __builtin_amdgcn_make_buffer_rsrc((void *)tj.out, (short)0, (int)((uint32_t)lim * (uint32_t)WIDTH), 0x00020000);
+  const bool out_al = ((uintptr_t)tj.out & 15) == 0;
 #pragma unroll
-  for (int h = 0; h < 2; h++)
-#pragma unroll
-    for (int r = 0; r < HR; r++)
+  for (int r = 0; r < EX_ROWS; r++) {
+    const int32_t j0 = v0 + r * EX_ROW + 4 * lane;
+    const uint32_t off = (uint32_t)j0 * (uint32_t)WIDTH;
+    if (j0 + 4 <= lim && out_al) {
+      if (WIDTH == 4) {
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u32x4{(uint32_t)val[r][0], (uint32_t)val[r][1], (uint32_t)val[r][2], (uint32_t)val[r][3]}, ors, off, 0, 0);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u32x4{(uint32_t)val[r][0], (uint32_t)((uint64_t)val[r][0] >> 32), (uint32_t)val[r][1],
+                  (uint32_t)((uint64_t)val[r][1] >> 32)},
+            ors, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u32x4{(uint32_t)val[r][2], (uint32_t)((uint64_t)val[r][2] >> 32), (uint32_t)val[r][3],
+                  (uint32_t)((uint64_t)val[r][3] >> 32)},
+            ors, off + 16, 0, 0);
+      }
+    } else {
 #pragma unroll
       for (int q = 0; q < 4; q++) {
-        key[h][r][q] = 0;
-        val[h][r][q] = 0;
-      }
-  if (wv < g.njobs) {
-    tj = sload(a.tiles + j);
-    rc = sload(a.recs + j);
-    if (rec_live(rc.epoch, a.epoch) && rc.v0 < rc.lim) {
-      if (rc.bw < 0) {  // PLAIN (a dictionary chunk's fallback page): a copy of the job's bytes
-        copy_tile<EX_WAVE * 8 / 1024>(rc.vals + (int64_t)rc.v0 * WIDTH, tj.out + (int64_t)rc.v0 * WIDTH,
-                                      (int64_t)(rc.lim - rc.v0) * WIDTH, lane);
-      } else {
-        const int k = job_keys<WIDTH>(a, tj, rc, lds_dyn + wv * (g.kspan / 4), g.kspan, key);
-        if (k == 1) {  // outside the staged form: straight from HBM / L2
-          ExPage P;
-          P.nr = rc.nr;
-          P.bw = rc.bw;
-          P.val_len = rc.val_len;
-          P.dict_n = rc.dict_n;
-          P.vals = rc.vals;
-          P.dict = rc.dict;
-          P.runs = rc.runs;
-          for (int32_t c = rc.v0; c < rc.lim; c += 512)
-            expand_direct(a, P, tj.page, WIDTH, tj.out, c, min(c + 512, rc.lim),
-                          a.tile_info[tj.tf + (c - rc.v0) / RUN_TILE].x);
-        }
-        act = k == 0;
+        if (j0 + q >= lim) continue;
+        if (WIDTH == 4) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)val[r][q], ors, off + 4 * q, 0, 0);
+        else
+          __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)val[r][q], (uint32_t)((uint64_t)val[r][q] >> 32)}, ors,
+                                                off + 8 * q, 0, 0);
       }
     }
   }
-  // the chunk's dictionary (every job of the group has the same one): the
-  // group's first record (written by this decode's k_prepare), or the
-  // dictionary page itself when that job failed or is PLAIN
-  // (no __syncthreads_or here: its static LDS would not fit beside the
-  // launch's 160 KiB; a group whose waves all failed still streams the slices)
-  __syncthreads();  // every wave's staged keys are in registers: the LDS is the slices'
+}
+
+// a job outside the register form: keys and gathers straight from HBM / L2
+// (not inlined: rare, and its registers stay out of the kernel's allocation)
+__device__ __noinline__ void wg_direct(const KArgs &a, int page, uint8_t *out, int32_t tf, int32_t v0, int32_t lim,
+                                       const uint8_t *vals, const uint8_t *dict, const uint2 *runs, int32_t nr,
+                                       int32_t bw, int32_t val_len, uint32_t dict_n, int width) {
+  ExPage P;
+  P.nr = nr;
+  P.bw = bw;
+  P.val_len = val_len;
+  P.dict_n = dict_n;
+  P.vals = vals;
+  P.dict = dict;
+  P.runs = runs;
+  for (int32_t c = v0; c < lim; c += 512)
+    expand_direct(a, P, page, width, out, c, min(c + 512, lim), a.tile_info[tf + (c - v0) / RUN_TILE].x);
+}
+#define WG_DIRECT(tj, rc, W) \
+  wg_direct(a, (tj).page, (tj).out, (tj).tf, (rc).v0, (rc).lim, (rc).vals, (rc).dict, (rc).runs, (rc).nr, (rc).bw, \
+            (rc).val_len, (rc).dict_n, (W))
+
+// LDS <- dictionary bytes [b0, b0 + nbytes) (aligned dwords; an unaligned
+// dictionary is funnel-shifted), PF 16-byte pieces a thread in flight
+template <int NT, int PF>
+__device__ __forceinline__ void dict_to_lds(uint32_t *lds, const __amdgpu_buffer_rsrc_t rs, uint32_t dsh, uint32_t b0,
+                                            uint32_t nbytes) {
+  const uint32_t n16 = (nbytes + 15) / 16;
+  for (uint32_t i0 = threadIdx.x; i0 < n16; i0 += PF * NT) {
+    u32x4 x[PF];
+    uint32_t y[PF];
+#pragma unroll
+    for (int q = 0; q < PF; q++) {
+      const uint32_t i = i0 + q * NT;
+      x[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, b0 + 16 * i, 0, 0);  // out of range: zeros
+      y[q] = dsh ? __builtin_amdgcn_raw_buffer_load_b32(rs, b0 + 16 * i + 16, 0, 0) : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < PF; q++) {
+      const uint32_t i = i0 + q * NT;
+      if (i < n16)
+        *(u32x4 *)(lds + 4 * i) =
+            u32x4{__builtin_amdgcn_alignbyte(x[q].y, x[q].x, dsh), __builtin_amdgcn_alignbyte(x[q].z, x[q].y, dsh),
+                  __builtin_amdgcn_alignbyte(x[q].w, x[q].z, dsh), __builtin_amdgcn_alignbyte(y[q], x[q].w, dsh)};
+    }
+  }
+}
+
+// LDS <- dictionary bytes [0, nbytes) of a 16-byte aligned source by LDS-DMA
+// (1 KiB a wave instruction, every piece of the workgroup in flight at once);
+// the caller waits (vmcnt) and syncs
+__device__ __forceinline__ void dict_dma(uint32_t *lds, const uint8_t *src, uint32_t nbytes) {
+  const int lane = lane_id();
+  const uint32_t wv = ufirst(threadIdx.x >> 6);
+  for (uint32_t c = wv; c * 1024 < nbytes; c += WG_WAVES)
+    if (c * 1024 + 16 * lane < nbytes)
+      __builtin_amdgcn_global_load_lds((const void *)(src + c * 1024 + 16 * lane),
+                                       (__attribute__((address_space(3))) void *)(lds + c * 256), 16, 0, 0);
+}
+
+template <int WIDTH>
+__global__ __launch_bounds__(WG_WAVES * 64) void k_expand_wg(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
+  typedef typename std::conditional<WIDTH == 4, uint32_t, uint64_t>::type VT;
+  const LdsGroup g = sload(a.lgroups + blockIdx.x);
   if (g.njobs <= 0) return;  // an empty slot of the XCD dealing (block-uniform)
+  WSTAMP(0);
+  const int wv = (int)ufirst(threadIdx.x >> 6);
+  const int jend = g.job0 + g.njobs;
+  // this wave's first two jobs' descriptors, in flight during the dictionary copy
+  int j = g.job0 + wv;
+  uint32_t vcur = j < jend ? job_load(a, j) : 0u;
+  uint32_t vnext = j + WG_WAVES < jend ? job_load(a, j + WG_WAVES) : 0u;
+  // the chunk's dictionary: the group's first record (written by this decode's
+  // k_prepare), or the dictionary page itself when that job failed or is PLAIN
   const ExRec r0 = sload(a.recs + g.job0);
   const uint8_t *dict;
   uint32_t dn;
   if (rec_live(r0.epoch, a.epoch) && r0.dict) {
     dict = r0.dict;
     dn = r0.dict_n;
-  } else {  // a failed or PLAIN first page: the dictionary page itself (its size checked on the host)
-    if (page_status(a.status, g.dpage) != STATUS_OK) return;
+  } else {
+    if (page_status(a.status, g.dpage) != STATUS_OK) return;  // no record of the chunk was written
     const PageDesc dp = a.pages[g.dpage];
     dict = body_ptr(a, dp, g.dpage);
     dn = (uint32_t)max(dp.num_values, 0);
   }
-  const uint32_t SE = (uint32_t)(g.dict_bytes / WIDTH);  // entries per slice (the launch's LDS)
   const uint32_t dsh = (uint32_t)((uintptr_t)dict & 3);
+#if defined(PQ_WG_CHECK) || defined(PQ_WG_SIMPLE)
+  const bool dma = false;  // (analysis build: the register copy)
+#else
+  const bool dma = ((uintptr_t)dict & 15) == 0;
+#endif
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       (void *)((uintptr_t)dict & ~(uintptr_t)3), (short)0, (int)((dn * (uint32_t)WIDTH + dsh + 3) & ~3u), 0x00020000);
-  constexpr uint32_t T = NW * 64;
-  for (uint32_t base = 0; base < dn; base += SE) {
-    const uint32_t nbytes = min(dn - base, SE) * (uint32_t)WIDTH;
-    const uint32_t n16 = (nbytes + 15) / 16, b0 = base * (uint32_t)WIDTH;
-    if (base > 0) __syncthreads();  // the previous slice's gathers are done
-    for (uint32_t i0 = threadIdx.x; i0 < n16; i0 += 4 * T) {
-      u32x4 x[4];
-      uint32_t y[4];
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const uint32_t i = i0 + q * T;
-        x[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, b0 + 16 * i, 0, 0);  // out of range: zeros
-        y[q] = dsh ? __builtin_amdgcn_raw_buffer_load_b32(rs, b0 + 16 * i + 16, 0, 0) : 0u;
-      }
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const uint32_t i = i0 + q * T;
-        if (i < n16)
-          *(u32x4 *)(lds_dyn + 4 * i) =
-              u32x4{__builtin_amdgcn_alignbyte(x[q].y, x[q].x, dsh), __builtin_amdgcn_alignbyte(x[q].z, x[q].y, dsh),
-                    __builtin_amdgcn_alignbyte(x[q].w, x[q].z, dsh), __builtin_amdgcn_alignbyte(y[q], x[q].w, dsh)};
-      }
+  constexpr uint32_t SE = WG_SLICE / WIDTH;  // entries a slice
+  constexpr int NT = WG_WAVES * 64;
+  // (8-byte values: the host sends only dictionaries of one slice — a sliced
+  // round's 64 value registers a lane would not fit beside its keys)
+  const bool sliced = WIDTH == 4 && dn > SE;
+  if (!sliced) {  // resident: the whole dictionary, once
+    if (dma) {
+      dict_dma(lds_dyn, dict, min(dn, SE) * (uint32_t)WIDTH);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      dict_to_lds<NT, 4>(lds_dyn, rs, dsh, 0, min(dn, SE) * (uint32_t)WIDTH);
     }
     __syncthreads();
-    if (act) {
+  }
+  RunWin W;
+  if (j < jend && job_dict_live(a, vcur)) job_window(W, vcur);
+  WSTAMP(1);
+  // rounds of WG_WAVES jobs, one a wave (resident: each wave runs on through
+  // its jobs without waiting for the others; sliced: the dictionary streams
+  // through the LDS once a round).  Software-pipelined: while job j's keys load
+  // and gather, job j + WG_WAVES's run window and job j + 2 WG_WAVES's
+  // descriptors are in flight.
+  for (int j0 = g.job0; j0 < jend; j0 += WG_WAVES, j += WG_WAVES) {
+    const uint32_t vfar = j + 2 * WG_WAVES < jend ? job_load(a, j + 2 * WG_WAVES) : 0u;
+    RunWin Wn;
+    if (j + WG_WAVES < jend && job_dict_live(a, vnext)) job_window(Wn, vnext);
+    TileJob tj;
+    ExRec rc;
+    job_unpack(vcur, tj, rc);
+#ifdef PQ_WG_SIMPLE
+    // analysis build: plain scalar descriptor loads and the window loaded here
+    if (j < jend) {
+      tj = sload(a.tiles + j);
+      rc = sload(a.recs + j);
+      if (rec_live(rc.epoch, a.epoch) && rc.v0 < rc.lim && rc.bw >= 0) W.load(rc.runs, rc.nr, rc.first_run);
+    }
+#endif
+#ifdef PQ_WG_CHECK
+    // analysis build: the pipelined descriptors and window against the plain loads
+    if (j < jend) {
+      const TileJob tj2 = sload(a.tiles + j);
+      const ExRec rc2 = sload(a.recs + j);
+      const bool bad_t = tj2.out != tj.out || tj2.page != tj.page || tj2.tf != tj.tf;
+      const bool bad_r = rc2.vals != rc.vals || rc2.dict != rc.dict || rc2.runs != rc.runs || rc2.v0 != rc.v0 ||
+                         rc2.lim != rc.lim || rc2.bw != rc.bw || rc2.nr != rc.nr || rc2.first_run != rc.first_run ||
+                         rc2.epoch != rc.epoch || rc2.val_len != rc.val_len || rc2.dict_n != rc.dict_n;
+      bool bad_w = false;
+      if (rec_live(rc2.epoch, a.epoch) && rc2.v0 < rc2.lim && rc2.bw >= 0) {
+        RunWin W2;
+        W2.load(rc2.runs, rc2.nr, rc2.first_run);
+        bad_w = ballot(W2.start != W.start || W2.prm != W.prm || W2.rle != W.rle) != 0;
+      }
+      if (bad_t || bad_r || bad_w) {
+        if (lane_id() == 0)
+          printf("k_expand_wg check: block %d wave %d job %d: tile %d rec %d window %d (out %p/%p vals %p/%p runs %p/%p "
+                 "v0 %d/%d lim %d/%d bw %d/%d)\n",
+                 (int)blockIdx.x, wv, j, (int)bad_t, (int)bad_r, (int)bad_w, (void *)tj.out, (void *)tj2.out,
+                 (const void *)rc.vals, (const void *)rc2.vals, (const void *)rc.runs, (const void *)rc2.runs, rc.v0,
+                 rc2.v0, rc.lim, rc2.lim, rc.bw, rc2.bw);
+        tj = tj2;
+        rc = rc2;
+        rc.epoch = ~a.epoch & 0x7fffffffu;  // skipped
+      }
+    }
+#endif
+    int k = 3;  // 0 keys ready, 1 outside the register form, 2 failed, 3 nothing to do
+    uint32_t key[EX_ROWS][4];
+    WSTAMP(2);
+    if (j < jend && rec_live(rc.epoch, a.epoch) && rc.v0 < rc.lim) {  // (else: the page failed before k_prepare finished it)
+      if (rc.bw < 0)  // PLAIN (a dictionary chunk's fallback page): a copy of the job's bytes
+        copy_tile<EX_WAVE * 8 / 1024>(rc.vals + (int64_t)rc.v0 * WIDTH, tj.out + (int64_t)rc.v0 * WIDTH,
+                                      (int64_t)(rc.lim - rc.v0) * WIDTH, lane_id());
+      else
+        k = keys_direct(a, tj, rc, W, key);
+      if (k == 0 && !sliced && dn > SE) k = 1;  // (not sent by the host: a dictionary past the LDS)
+    }
+    WSTAMP(3);
+    VT val[EX_ROWS][4];
+    if (!sliced) {
+      if (k == 0) {
 #pragma unroll
-      for (int h = 0; h < 2; h++)
-#pragma unroll
-        for (int r = 0; r < HR; r++)
+        for (int r = 0; r < EX_ROWS; r++)
 #pragma unroll
           for (int q = 0; q < 4; q++) {
-            const uint32_t rel = key[h][r][q] - base;
-            if (rel < SE) {
-              if (WIDTH == 4) val[h][r][q] = lds_dyn[rel];
-              else val[h][r][q] = ((const uint64_t *)lds_dyn)[rel];
-            }
+            if (WIDTH == 4) val[r][q] = lds_dyn[key[r][q]];
+            else val[r][q] = ((const uint64_t *)lds_dyn)[key[r][q]];
           }
-    }
-  }
-  if (!act) return;
-  // stores: 16 / 32 contiguous bytes per lane per row (as expand_job)
-  const int32_t v0 = rc.v0, lim = rc.lim;
-  const __amdgpu_buffer_rsrc_t ors =
-      __builtin_amdgcn_make_buffer_rsrc((void *)tj.out, (short)0, (int)((uint32_t)lim * (uint32_t)WIDTH), 0x00020000);
-  const bool out_al = ((uintptr_t)tj.out & 15) == 0;
+      }
+    } else {
 #pragma unroll
-  for (int h = 0; h < 2; h++)
+      for (int r = 0; r < EX_ROWS; r++)
 #pragma unroll
-    for (int r = 0; r < HR; r++) {
-      const int32_t j0 = v0 + (h * HR + r) * EX_ROW + 4 * lane;
-      const uint32_t off = (uint32_t)j0 * (uint32_t)WIDTH;
-      if (j0 + 4 <= lim && out_al) {
-        if (WIDTH == 4) {
-          __builtin_amdgcn_raw_buffer_store_b128(
-              u32x4{(uint32_t)val[h][r][0], (uint32_t)val[h][r][1], (uint32_t)val[h][r][2], (uint32_t)val[h][r][3]},
-              ors, off, 0, 0);
+        for (int q = 0; q < 4; q++) val[r][q] = 0;
+      for (uint32_t base = 0; base < dn; base += SE) {
+        __syncthreads();  // the previous slice's gathers are done
+        if (dma) {
+          dict_dma(lds_dyn, dict + (size_t)base * WIDTH, min(dn - base, SE) * (uint32_t)WIDTH);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
-          __builtin_amdgcn_raw_buffer_store_b128(
-              u32x4{(uint32_t)val[h][r][0], (uint32_t)((uint64_t)val[h][r][0] >> 32), (uint32_t)val[h][r][1],
-                    (uint32_t)((uint64_t)val[h][r][1] >> 32)},
-              ors, off, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b128(
-              u32x4{(uint32_t)val[h][r][2], (uint32_t)((uint64_t)val[h][r][2] >> 32), (uint32_t)val[h][r][3],
-                    (uint32_t)((uint64_t)val[h][r][3] >> 32)},
-              ors, off + 16, 0, 0);
+          dict_to_lds<NT, 2>(lds_dyn, rs, dsh, base * (uint32_t)WIDTH, min(dn - base, SE) * (uint32_t)WIDTH);
         }
-      } else {
+        __syncthreads();
+        if (k == 0) {
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-          if (j0 + q >= lim) continue;
-          if (WIDTH == 4) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)val[h][r][q], ors, off + 4 * q, 0, 0);
-          else
-            __builtin_amdgcn_raw_buffer_store_b64(
-                u32x2{(uint32_t)val[h][r][q], (uint32_t)((uint64_t)val[h][r][q] >> 32)}, ors, off + 8 * q, 0, 0);
+          for (int r = 0; r < EX_ROWS; r++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+              const uint32_t rel = key[r][q] - base;
+              if (rel < SE) val[r][q] = lds_dyn[rel];
+            }
         }
       }
     }
+    WSTAMP(4);
+    if (k == 0) store_rows<WIDTH>(tj, rc.v0, rc.lim, val);
+    if (k == 1) WG_DIRECT(tj, rc, WIDTH);  // after the round: nothing of it live across the call
+    WSTAMP(5);
+    W = Wn;
+    vcur = vnext;
+    vnext = vfar;
+  }
 }
 
 // ===========================================================================
@@ -5456,20 +5674,6 @@ __global__ __launch_bounds__(LD_WAVES_H * 64) void k_expand_mix(KArgs a) {
   if (a.dbg && lane_id() == 0)  // the wave's end
     a.dbg[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + 6] = __builtin_amdgcn_s_memrealtime();
 #endif
-}
-
-// k_expand_big: one workgroup of BIG_WAVES waves per group of jobs whose
-// dictionary is too large for the mixed launch's LDS budget but fits a CU's
-// (host: dictionary + BIG_WAVES staged-key spans <= 160 KiB).  The dictionary
-// is copied once and shared by twice as many waves as in k_expand_mix, so one
-// resident workgroup per CU still keeps two waves per SIMD gathering from LDS
-// (measured on single-width files: bit widths 13-15 gather from L1/L2 at
-// 270-490 Gvalues/s, from LDS at 340-660 even with one 4-wave group per CU).
-template <int WIDTH>
-__global__ __launch_bounds__(BIG_WAVES * 64) void k_expand_big(KArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
-  const LdsGroup g = sload(a.lgroups + blockIdx.x);
-  mix_lds<WIDTH, BIG_WAVES>(a, g, lds_dyn);
 }
 
 // ===========================================================================
@@ -5802,47 +6006,25 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     hipLaunchKernelGGL(pq::k_copy, dim3(items < 4096 ? items : 4096), dim3(256), 0, s, k);
     return launch_status(which);
   }
-  if (which == 9 || which == 22 || which == 27) {  // k_expand_mix (9) / _big (22) / _pass (27): one workgroup per LdsGroup
+  if (which == 9 || which == 22) {  // k_expand_mix (9) / k_expand_wg (22): one workgroup per LdsGroup
     static bool attr = false;
     if (!attr) {
-      hipFuncSetAttribute((const void *)pq::k_expand_pass<4, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      hipFuncSetAttribute((const void *)pq::k_expand_pass<4, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      hipFuncSetAttribute((const void *)pq::k_expand_pass<8, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      hipFuncSetAttribute((const void *)pq::k_expand_pass<8, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       hipFuncSetAttribute((const void *)pq::k_expand_mix<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       hipFuncSetAttribute((const void *)pq::k_expand_mix<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      hipFuncSetAttribute((const void *)pq::k_expand_big<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      hipFuncSetAttribute((const void *)pq::k_expand_big<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      hipFuncSetAttribute((const void *)pq::k_expand_wg<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      hipFuncSetAttribute((const void *)pq::k_expand_wg<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr = true;
     }
-    if (which == 27) {
-      // k_expand_pass: groups after the mixed ones, absolute job indices; g.dict_bytes = slice bytes
-      const pq::LdsGroup *pg = (const pq::LdsGroup *)p->lgroups + p->ldn[0] + p->ldn[1] + p->ldn[2] + p->ldn[3];
-      const int nw = pq::pass_waves(4);
-      for (int w = 0; w < 2; w++) {
-        if (p->ldn[4 + w] <= 0) continue;
-        pq::KArgs kb = k;
-        kb.lgroups = pg + (w ? p->ldn[4] : 0);
-        const dim3 grid(p->ldn[4 + w]);
-        const size_t lds = (size_t)p->ldl[4 + w];
-        if (w == 0 && nw == 16) hipLaunchKernelGGL((pq::k_expand_pass<4, 16>), grid, dim3(16 * 64), lds, s, kb);
-        else if (w == 0) hipLaunchKernelGGL((pq::k_expand_pass<4, 8>), grid, dim3(8 * 64), lds, s, kb);
-        else if (nw == 16) hipLaunchKernelGGL((pq::k_expand_pass<8, 8>), grid, dim3(8 * 64), lds, s, kb);
-        else hipLaunchKernelGGL((pq::k_expand_pass<8, 4>), grid, dim3(4 * 64), lds, s, kb);
-      }
-      return launch_status(which);
-    }
     if (which == 22) {
-      // k_expand_big: big-dictionary groups after the mixed ones, absolute job indices
+      // k_expand_wg: its groups after the mixed ones, absolute job indices
       const pq::LdsGroup *bg = (const pq::LdsGroup *)p->lgroups + p->ldn[0] + p->ldn[1];
       for (int w = 0; w < 2; w++) {
-      if (p->ldn[2 + w] <= 0) continue;
-      pq::KArgs kb = k;
-      kb.lgroups = bg + (w ? p->ldn[2] : 0);
-      if (w == 0)
-        hipLaunchKernelGGL(pq::k_expand_big<4>, dim3(p->ldn[2]), dim3(pq::BIG_WAVES * 64), (size_t)p->ldl[2], s, kb);
-      else
-        hipLaunchKernelGGL(pq::k_expand_big<8>, dim3(p->ldn[3]), dim3(pq::BIG_WAVES * 64), (size_t)p->ldl[3], s, kb);
+        if (p->ldn[2 + w] <= 0) continue;
+        pq::KArgs kb = k;
+        kb.lgroups = bg + (w ? p->ldn[2] : 0);
+        const dim3 grid(p->ldn[2 + w]), blk(pq::WG_WAVES * 64);
+        if (w == 0) hipLaunchKernelGGL(pq::k_expand_wg<4>, grid, blk, (size_t)pq::WG_SLICE, s, kb);
+        else hipLaunchKernelGGL(pq::k_expand_wg<8>, grid, blk, (size_t)pq::WG_SLICE, s, kb);
       }
       return launch_status(which);
     }

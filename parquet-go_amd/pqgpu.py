@@ -90,7 +90,9 @@ class ColumnView(ctypes.Structure):
 class BatchStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in ("pages", "data_pages", "dict_pages", "snappy_pages",
                                               "host_inflated_pages", "input_bytes", "staged_bytes",
-                                              "output_bytes", "h2d_bytes", "snappy_in_bytes", "dict_bytes")]
+                                              "output_bytes", "h2d_bytes", "snappy_in_bytes", "dict_bytes")] + \
+        [(n, ctypes.c_double) for n in ("create_plan_ms", "create_alloc_ms", "create_upload_ms", "create_tables_ms",
+                                        "upload_gather_ms", "upload_wait_ms")]
 
 
 DECOMPRESS_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t,
