@@ -601,6 +601,22 @@ struct pqg_ctx {
 // DMAs are queued on `s` and the call returns without waiting for the last
 // ones (a later upload waits for a buffer's event before refilling it).
 static bool getenv_flag(const char *name);
+// Analysis knobs (A/B routes and tuning sweeps of DESIGN.md): read only in
+// the analysis build (`make -C parquet-go_amd/csrc analysis` ->
+// libpqgpu_analysis.so, -DPQ_ANALYSIS); the shipped library takes every
+// default, so each route it can take is one the GPU suite runs.
+static const char *knob(const char *name) {
+#ifdef PQ_ANALYSIS
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
+static bool knob_flag(const char *name) {
+  const char *v = knob(name);
+  return v && v[0] == '1';
+}
 template <class Layout>
 static int ring_upload(pqg_ctx *c, uint8_t *dst, const Layout &in, hipStream_t s, double *gather_ms = nullptr,
                        double *wait_ms = nullptr) {
@@ -632,7 +648,7 @@ static int ring_upload(pqg_ctx *c, uint8_t *dst, const Layout &in, hipStream_t s
     const int k = c->pin_next;
     const size_t m = std::min(pqg_ctx::kRingBytes, n - off);
     auto t0 = now();
-    static const bool poll = getenv_flag("PQG_RING_POLL");
+    static const bool poll = knob_flag("PQG_RING_POLL");
     if (c->pin_busy[k]) {
       if (poll) {  // (analysis: busy-poll the buffer's event instead of a blocking wait)
         hipError_t q;
@@ -1683,7 +1699,7 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
           d.body = d.src + (uint64_t)(lsize + lit);
           B->literal_pages++;
         } else if (C.codec == PQG_CODEC_SNAPPY && !(h.type == 2 && L.physical_type == T_BYTE_ARRAY) &&
-                   !getenv_flag("PQG_NO_TRAIN") &&
+                   !knob_flag("PQG_NO_TRAIN") &&
                    snappy_literal_train(f->data + w.payload + lsize, comp, body, train)) {
           // a train of literals: staged by k_copy from the plan (a BYTE_ARRAY
           // dictionary is read by k_dict_prepare before k_copy runs: k_snappy)
@@ -1739,7 +1755,7 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
       dict_idx = my_index;
       if (L.physical_type == T_BYTE_ARRAY) {
         B->dict_list.push_back(my_index);  // k_dict_prepare: the length-prefix walk
-        static const bool swd_off = getenv_flag("PQG_NO_SWALK");
+        static const bool swd_off = knob_flag("PQG_NO_SWALK");
         if (!swd_off && body >= SW_MIN && d.num_values > 0) {  // region-parallel (k_sw_*) before it
           const int32_t nreg = (int32_t)((body + SW_R - 1) / SW_R);
           B->pages.back().swalk = (int32_t)B->sw_dict.size();
@@ -1780,7 +1796,7 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
         B->lens_entries += 2 * (int64_t)std::max(d.num_values, 0);
         // a long page: its walk split over SW_R-byte regions (k_sw_*), when
         // its non-null count comes from k_levels (or every value is defined)
-        static const bool sw_off = getenv_flag("PQG_NO_SWALK");
+        static const bool sw_off = knob_flag("PQG_NO_SWALK");
         if (!sw_off && body >= SW_MIN && d.num_values > 0 && (L.max_def == 0 || B->pages.back().lvl_base >= 0)) {
           const int32_t nreg = (int32_t)((body + SW_R - 1) / SW_R);
           B->pages.back().swalk = (int32_t)B->sw_data.size();
@@ -1992,7 +2008,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
       const bool nest_fw = L.max_rep > 0 && (L.value_width == 4 || L.value_width == 8) &&
                            L.physical_type != T_BYTE_ARRAY && L.physical_type != T_BOOLEAN &&
                            !(cp.flags & COL_EMIT_LEVELS) && !fl_dba;
-      static const bool pstr_off = getenv("PQG_NO_PLAIN_STR") != nullptr;
+      static const bool pstr_off = knob("PQG_NO_PLAIN_STR") != nullptr;
       if (flat_ba && L.max_def == 0 && d.enc == ENC_PLAIN && d.lens_base >= 0 && !pstr_off) {
         // several waves per page (k_plain_str) over k_prepare's (offset, length) scratch
         for (int32_t v = 0; v < std::max(d.num_values, 0); v += PLAIN_STR_ITEM) {
@@ -2016,7 +2032,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     // a PLAIN page's k_expand records depend only on its header (flat and
     // required: the values section is the whole body): written by the host
     // once; a page too short for its values is left to k_prepare's check
-    static const bool srec_off = getenv_flag("PQG_NO_STATIC_RECORDS");
+    static const bool srec_off = knob_flag("PQG_NO_STATIC_RECORDS");
     if (d.enc == ENC_PLAIN && !srec_off && B->status0[(size_t)pi] == STATUS_OK &&
         (int64_t)n * L.value_width <= (int64_t)d.body_len)
       d.srec = 1;
@@ -2063,10 +2079,10 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   // interleaved by job count so that L2-bound gathers and LDS-bound ones share
   // the machine for the whole launch.
   B->ex_lds = (B->ex_lds + 255) & ~255;  // LDS-DMA pieces of 16 bytes per lane, the last one partial
-  const bool ld_off = getenv("PQG_NO_LDS_DICT") != nullptr;
+  const bool ld_off = knob("PQG_NO_LDS_DICT") != nullptr;
   std::vector<TileJob> slot_tiles, ld_tiles, big_tiles;
   std::vector<LdsGroup> big_groups[2];
-  const int64_t ld_max = getenv("PQG_LD_MAX_KB") ? 1024 * (int64_t)atoi(getenv("PQG_LD_MAX_KB")) : LD_MIX_MAX;
+  const int64_t ld_max = knob("PQG_LD_MAX_KB") ? 1024 * (int64_t)atoi(knob("PQG_LD_MAX_KB")) : LD_MIX_MAX;
   // which chunks fit the mixed launch's LDS groups (class 1), or k_expand_wg's
   // workgroup-a-CU form (class 2: the dictionary in at most WG_MAX_SLICES
   // slices of a CU's LDS), else the mixed launch's L1/L2 blocks
@@ -2083,7 +2099,8 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     const bool amortised = dbytes * 4 <= J * EX_WAVE_VALUES * W;
     if (amortised && dbytes + (int64_t)LD_WAVES_H * ks <= ld_max) return 1;
     // (8-byte values: one slice at most — k_expand_wg keeps no sliced form for them)
-    if (!wg_off && dbytes <= (int64_t)(W == 4 ? WG_MAX_SLICES : 1) * WG_SLICE && dbytes <= J * EX_WAVE_VALUES * W)
+    static const int64_t wg_slices = knob("PQG_WG_SLICES") ? std::max(1, atoi(knob("PQG_WG_SLICES"))) : WG_MAX_SLICES;
+    if (!wg_off && dbytes <= (W == 4 ? wg_slices : 1) * (int64_t)WG_SLICE && dbytes <= J * EX_WAVE_VALUES * W)
       return 2;
     return 0;
   };
@@ -2125,9 +2142,9 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
       if (cls) {
         const int64_t J = (int64_t)ct.size();
         if (cls == 1) {
-          const int64_t amort = getenv("PQG_LD_AMORT") ? atoi(getenv("PQG_LD_AMORT")) : 2;
+          const int64_t amort = knob("PQG_LD_AMORT") ? atoi(knob("PQG_LD_AMORT")) : 2;
           int64_t G = (dbytes * amort + (int64_t)EX_WAVE_VALUES * W - 1) / ((int64_t)EX_WAVE_VALUES * W);
-          const int64_t gmin = getenv("PQG_LD_GMIN") ? atoi(getenv("PQG_LD_GMIN")) : LD_WAVES_H;
+          const int64_t gmin = knob("PQG_LD_GMIN") ? atoi(knob("PQG_LD_GMIN")) : LD_WAVES_H;
           G = std::min<int64_t>(std::max<int64_t>((G + LD_WAVES_H - 1) / LD_WAVES_H * LD_WAVES_H, gmin), 128);
           const int64_t ng = (J + G - 1) / G;
           for (int64_t q = 0; q < ng; q++) ldg.push_back({&ct, q * J / ng, (q + 1) * J / ng, (int32_t)dbytes, ks});
@@ -2151,7 +2168,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     // gets the same number of L2-bound jobs (PQG_XCD_SPLIT_KB=0: whole chunks
     // only, least loaded first)
     {
-      static const int64_t split_max = getenv("PQG_XCD_SPLIT_KB") ? 1024 * (int64_t)atoi(getenv("PQG_XCD_SPLIT_KB"))
+      static const int64_t split_max = knob("PQG_XCD_SPLIT_KB") ? 1024 * (int64_t)atoi(knob("PQG_XCD_SPLIT_KB"))
                                                                   : (int64_t)1 << 20;
       auto dict_bytes_of = [&](const std::vector<TileJob> &ct) {
         return ct[0].dict >= 0 ? (int64_t)std::max(B->pages[(size_t)ct[0].dict].num_values, 0) * W : 0;
@@ -2160,7 +2177,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
       for (auto *ct : gchunks) (split_max > 0 && dict_bytes_of(*ct) <= split_max ? split : whole).push_back(ct);
       // a job of a whole (large-dictionary) chunk weighs PQG_XCD_WHOLE_W jobs
       // of the split ones (its gathers miss L2 more often)
-      static const double ww = getenv("PQG_XCD_WHOLE_W") ? atof(getenv("PQG_XCD_WHOLE_W")) : 1.0;
+      static const double ww = knob("PQG_XCD_WHOLE_W") ? atof(knob("PQG_XCD_WHOLE_W")) : 1.0;
       double load[8] = {};
       auto least = [&]() {
         size_t best = 0;
@@ -2199,7 +2216,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     while (gr < ngr || lr < nlr) {
       // the round kind that is behind in its share of the jobs goes next
       // (PQG_MIX_ORDER, analysis: 1 L1/L2 rounds first, 2 LDS rounds first)
-      static const int mix_order = getenv("PQG_MIX_ORDER") ? atoi(getenv("PQG_MIX_ORDER")) : 0;
+      static const int mix_order = knob("PQG_MIX_ORDER") ? atoi(knob("PQG_MIX_ORDER")) : 0;
       bool take_g = lr >= nlr || (gr < ngr && (double)gdone * (double)std::max<size_t>(ljobs, 1) <=
                                                   (double)ldone * (double)std::max<size_t>(gjobs, 1));
       if (mix_order == 1) take_g = gr < ngr;
@@ -2240,7 +2257,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
       // a chunk's groups go to one XCD residue (its dictionary stays in that
       // L2), chunks dealt to the least-loaded residue by their cost (jobs x
       // slices), largest first; then rounds of 8 blocks (block b on XCD b % 8)
-      static const int64_t wg_jobs = getenv("PQG_WG_JOBS") ? std::max(1, atoi(getenv("PQG_WG_JOBS"))) : WG_JOBS;
+      static const int64_t wg_jobs = knob("PQG_WG_JOBS") ? std::max(1, atoi(knob("PQG_WG_JOBS"))) : WG_JOBS;
       std::vector<std::vector<LdsGroup>> res(8);
       int64_t load[8] = {};
       auto slices = [&](int64_t db) { return (db + WG_SLICE - 1) / WG_SLICE; };
@@ -2301,7 +2318,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   // k_snappy takes pages in list order, one wave each: the longest bodies
   // first (longest-processing-time order), so that the long serial token
   // chains of big pages start with the launch instead of trailing it
-  if (!getenv("PQG_SNAPPY_LIST_ORDER")) {
+  if (!knob("PQG_SNAPPY_LIST_ORDER")) {
     std::stable_sort(B->snappy_list.begin(), B->snappy_list.end(), [&](int32_t x, int32_t y) {
       return B->pages[(size_t)x].body_len > B->pages[(size_t)y].body_len;
     });
@@ -2438,7 +2455,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     int64_t plen = env_part >= 0 ? env_part : std::max<int64_t>(4096, (tot / 16384 + 255) & ~(int64_t)255);
     if (plen > 0) plen = (plen + 255) & ~(int64_t)255;
     B->nest_parts.clear();
-    static const bool part_rescan = getenv_flag("PQG_PART_RESCAN");  // (analysis: parts count their own prefix)
+    static const bool part_rescan = knob_flag("PQG_PART_RESCAN");  // (analysis: parts count their own prefix)
     for (int32_t pg : B->general_nest) {
       const PageDesc &pd = B->pages[(size_t)pg];
       const int64_t n = std::max(pd.num_values, 0);
@@ -2868,7 +2885,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   // dictionary, k_levels needs nothing the Snappy phase writes and runs beside
   // it on a side stream (C3: its 0.73 ms left the critical path)
   // PQG_LEVELS_LATE=1 (analysis): k_levels back after the Snappy phase
-  static const bool lvl_late_env = getenv("PQG_LEVELS_LATE") != nullptr;
+  static const bool lvl_late_env = knob("PQG_LEVELS_LATE") != nullptr;
   const bool lvl_early = !resume && B->lvl_bytes > 0 && !B->lvl_late && !B->seg_times && !lvl_late_env;
   if (!resume) {
   mark(false);
@@ -2885,7 +2902,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     // from the start beside k_snappy's.  Measured on C3 (ms a step): full
     // grid 5.38, k = 1 6.52, 2 5.91, 4 5.43, 8 5.37 — resident waves beside
     // k_snappy's get too little issue; the full grid stays
-    static const int lv_cap = getenv("PQG_LEVELS_CAP") ? atoi(getenv("PQG_LEVELS_CAP")) : 0;
+    static const int lv_cap = knob("PQG_LEVELS_CAP") ? atoi(knob("PQG_LEVELS_CAP")) : 0;
     al.grid_cap = lv_cap > 0 ? lv_cap * B->ctx->cus : 0;
     e |= pq_launch(lv_id, &al, LN.side[2]);  // k_levels<-1>: every level page
     hipEventRecord(LN.join[2], LN.side[2]);
@@ -2917,7 +2934,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     // on the side stream was dispatched after the whole pages had taken the
     // CUs (PQG_WALK_SIDE=1 restores that order for comparison)
     static const bool walk_side = [] {
-      const char *v = getenv("PQG_WALK_SIDE");
+      const char *v = knob("PQG_WALK_SIDE");
       return v && v[0] == '1';
     }();
     hipStream_t ss = side && walk_side ? LN.side[0] : s;   // the serial chain
@@ -3084,7 +3101,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     a.nlist = (int32_t)B->tiles.size();
     // k_expand_wg (dictionaries that need a CU's LDS): after the mixed
     // launch, before it (PQG_BIG_ORDER=1) or beside it on a side stream (=2)
-    static const int big_order = getenv("PQG_BIG_ORDER") ? atoi(getenv("PQG_BIG_ORDER")) : 0;
+    static const int big_order = knob("PQG_BIG_ORDER") ? atoi(knob("PQG_BIG_ORDER")) : 0;
     const bool big = B->ldn[2] + B->ldn[3] > 0;
     if (big && big_order == 2) {
       hipEventRecord(LN.fork, s);
@@ -3097,11 +3114,11 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     // PLAIN: no level streams, no key-stream walk) gives k_level_check nothing
     // to find: k_expand_mix plans the next decode's statuses and the launch is
     // skipped (C1; PQG_LEVEL_CHECK=1 keeps it)
-    const bool plan_next = ndata > 0 && !getenv_flag("PQG_NO_STATUS_PLAN");
+    const bool plan_next = ndata > 0 && !knob_flag("PQG_NO_STATUS_PLAN");
     // (likewise a batch without level streams: the run walk sets its own
     // errors, k_level_check would only re-walk levels — C2)
     const bool skip_check = ((B->all_srec && ngen == 0 && B->dba_list.empty()) || B->no_levels) &&
-                            B->ldn[0] + B->ldn[1] > 0 && !getenv_flag("PQG_LEVEL_CHECK");
+                            B->ldn[0] + B->ldn[1] > 0 && !knob_flag("PQG_LEVEL_CHECK");
     if (skip_check && plan_next) {
       pq_launch_args ax = a;
       ax.status_next = B->d_status + ((a.epoch + 1) & 1) * npages;
@@ -3469,7 +3486,7 @@ int pqg_stream_open(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const i
   S->done.assign(S->slices.size(), 0);
   S->launched.assign(S->slices.size(), 0);
   S->lrc.assign(S->slices.size(), 0);
-  if (getenv("PQG_STREAM_LANES") && atoi(getenv("PQG_STREAM_LANES")) == 1) S->lanes = 1;
+  if (knob("PQG_STREAM_LANES") && atoi(knob("PQG_STREAM_LANES")) == 1) S->lanes = 1;
   const char *w = getenv("PQG_STREAM_WORKERS");
   const int nw = std::max(1, std::min({w ? atoi(w) : 3, depth, (int)std::max<size_t>(1, S->slices.size())}));
   for (int i = 0; i < nw; i++) S->workers.emplace_back(stream_worker, S);

@@ -195,9 +195,6 @@ __device__ __forceinline__ const uint8_t *body_ptr(const KArgs &a, const PageDes
 #ifndef SNAP_TOK_SHORT
 #define SNAP_TOK_SHORT 16  // token-parallel output: longer literals / near copies take the whole wave each
 #endif
-#ifndef PQ_SNAP_PAIR
-#define PQ_SNAP_PAIR 0  // medium tokens (SHORT..32 bytes) copied two per wave step
-#endif
 #ifndef PQ_FAR_DEFER
 #define PQ_FAR_DEFER 1  // k_snappy: short far copies' loads overlap the token tables (0: written at once)
 #endif
@@ -674,28 +671,7 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
         if (i < mylen) ring[(o + i) & RING_MASK] = b0;
         if (i + 1 < mylen) ring[(o + i + 1) & RING_MASK] = b1;
       }
-#if PQ_SNAP_PAIR
-      // tokens of up to 32 bytes two a step, a half wave each
-      for (uint64_t mm = ballot(indep && len > SNAP_TOK_SHORT && len <= 32); mm;) {
-        const int k1 = (int)__builtin_ctzll(mm);
-        mm &= mm - 1;
-        const bool two = mm != 0;
-        const int k2 = two ? (int)__builtin_ctzll(mm) : k1;
-        if (two) mm &= mm - 1;
-        const int64_t o1 = dpos + (int64_t)__builtin_amdgcn_readlane(out_rel, k1);
-        const int64_t o2 = dpos + (int64_t)__builtin_amdgcn_readlane(out_rel, k2);
-        const uint32_t l1 = (uint32_t)__builtin_amdgcn_readlane((int)len, k1), l2 = (uint32_t)__builtin_amdgcn_readlane((int)len, k2);
-        const uint32_t x1 = (uint32_t)__builtin_amdgcn_readlane((int)x, k1), x2 = (uint32_t)__builtin_amdgcn_readlane((int)x, k2);
-        const bool t1 = __builtin_amdgcn_readlane((int)lit, k1) != 0, t2 = __builtin_amdgcn_readlane((int)lit, k2) != 0;
-        const bool hi = lane >= 32;
-        const uint32_t j = (uint32_t)lane & 31u;
-        const int64_t oj = hi ? o2 : o1;
-        const uint32_t lj = hi ? (two ? l2 : 0u) : l1, xj = hi ? x2 : x1;
-        const bool tj = hi ? t2 : t1;
-        if (j < lj) ring[(oj + j) & RING_MASK] = tj ? winb[xj + j] : ring[(oj - xj + j) & RING_MASK];
-      }
-#endif
-      for (uint64_t lm = ballot(indep && len > (PQ_SNAP_PAIR ? 32u : 0u) && len > SNAP_TOK_SHORT); lm; lm &= lm - 1) {
+      for (uint64_t lm = ballot(indep && len > SNAP_TOK_SHORT); lm; lm &= lm - 1) {
         const int k = (int)__builtin_ctzll(lm);
         const int64_t ok = dpos + (int64_t)__builtin_amdgcn_readlane(out_rel, k);
         const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)len, k);
@@ -5992,8 +5968,12 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
   }
   if (which == 12) {  // k_prepare_copy: the prepare blocks, then the copy grid
     const uint32_t items = (k.max_jobs + (uint32_t)k.nhjobs) * pq::COPY_ITEMS;
-    // PQG_COPY_BLOCKS: the copy grid's cap (analysis)
+#ifdef PQ_ANALYSIS
+    // PQG_COPY_BLOCKS: the copy grid's cap (analysis build only)
     static const uint32_t cap = getenv("PQG_COPY_BLOCKS") ? (uint32_t)atoi(getenv("PQG_COPY_BLOCKS")) : 1024u;
+#else
+    constexpr uint32_t cap = 1024u;
+#endif
     const uint32_t cb = items < cap ? items : cap;
     const uint32_t pb = ((uint32_t)(k.nlist > 0 ? k.nlist : 0) + 3) / 4;
     if (pb + cb == 0) return 0;

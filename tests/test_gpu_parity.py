@@ -297,6 +297,41 @@ def test_tiled_big_dictionary_groups(bw):
             del os.environ[env]
 
 
+@pytest.mark.parametrize("bw", [13, 16])
+@pytest.mark.parametrize("comp", ["none", "snappy"])
+def test_tiled_wg_dictionary_layouts(bw, comp):
+    """k_expand_wg: a dictionary resident in a CU's LDS (bit width 13) and one
+    streamed through it in slices (16: two slices), INT32 and INT64 columns;
+    uncompressed dictionaries sit 16-byte aligned (copied by LDS-DMA), Snappy
+    single-literal ones are read in place at any alignment (register copy
+    with a funnel shift); every page's last rows take the general key path."""
+    rng = np.random.default_rng(300 + bw)
+    K = 1 << bw
+    rows = 3 * K + 777
+    d32 = rng.permutation(K).astype(np.int32) * 7 - 3
+    d64 = rng.permutation(K >> 2).astype(np.int64) * 0x10001 - (1 << 40)
+    t = _req_table({"a": d32[rng.integers(0, K, rows)], "b": d64[rng.integers(0, K >> 2, rows)]})
+    data = _pq_bytes(t, compression=comp, dictionary_pagesize_limit=1 << 30, row_group_size=rows // 2 + 5)
+    os.environ["PQG_BIG"] = "1"
+    try:
+        check_file(data, "wg bw%d %s" % (bw, comp))
+    finally:
+        del os.environ["PQG_BIG"]
+
+
+def test_segment_times_route():
+    """PQG_SEGMENT_TIMES=1 (bench.py's phase timing) launches k_copy, the
+    string walks, k_dict_prepare and k_prepare one by one instead of fused:
+    the same outputs on every config shape."""
+    os.environ["PQG_SEGMENT_TIMES"] = "1"
+    try:
+        for name in ("c1_int64_plain", "c2_dict_bw8", "c2_dict_bw12", "c3_delta_v2", "c4_list_str", "plain_strings",
+                     "gzip_int64"):
+            check_file(golden_bytes(name + ".parquet"), name + " segment times")
+    finally:
+        del os.environ["PQG_SEGMENT_TIMES"]
+
+
 def test_generated_nullable_mix():
     pa = pytest.importorskip("pyarrow")
     rng = np.random.default_rng(11)
