@@ -588,6 +588,7 @@ struct pqg_ctx {
   void *pin[kRingBufs] = {};
   hipEvent_t pin_ev[kRingBufs] = {};
   bool pin_busy[kRingBufs] = {};  // pin_ev recorded after a DMA that may still read the buffer
+  std::chrono::steady_clock::time_point pin_t[kRingBufs];  // when each buffer's last DMA was issued
   int pin_next = 0;
   std::mutex upload_mu;  // one ring_upload at a time per context
   GatherPool pool;       // PQG_UPLOAD_THREADS - 1 helper threads (started on first upload)
@@ -648,6 +649,7 @@ static int ring_upload(pqg_ctx *c, uint8_t *dst, const Layout &in, hipStream_t s
     const int k = c->pin_next;
     const size_t m = std::min(pqg_ctx::kRingBytes, n - off);
     auto t0 = now();
+    const bool was_busy = c->pin_busy[k];
     static const bool poll = knob_flag("PQG_RING_POLL");
     if (c->pin_busy[k]) {
       if (poll) {  // (analysis: busy-poll the buffer's event instead of a blocking wait)
@@ -659,7 +661,11 @@ static int ring_upload(pqg_ctx *c, uint8_t *dst, const Layout &in, hipStream_t s
       }
     }
     auto t1 = now();
-    t_wait += std::chrono::duration<double, std::milli>(t1 - t0).count();
+    const double w_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    t_wait += w_ms;
+    if (trace && was_busy && w_ms > 1.0)  // a long wait for a ring buffer's previous DMA
+      fprintf(stderr, "ring_upload: buffer %d (bytes %zu of %zu) waited %.2f ms for its DMA issued %.2f ms earlier\n", k,
+              off, n, w_ms, std::chrono::duration<double, std::milli>(t1 - c->pin_t[k]).count());
     c->pin_busy[k] = false;
     // gather [off, off + m) of the layout into the pinned buffer, in parts of >= 1 MiB
     uint8_t *pb = (uint8_t *)c->pin[k];
@@ -690,6 +696,7 @@ static int ring_upload(pqg_ctx *c, uint8_t *dst, const Layout &in, hipStream_t s
     else part(0);
     t_gather += std::chrono::duration<double, std::milli>(now() - t1).count();
     if (hipMemcpyAsync(dst + off, c->pin[k], m, hipMemcpyHostToDevice, s) != hipSuccess) return 1;
+    c->pin_t[k] = now();
     hipEventRecord(c->pin_ev[k], s);
     c->pin_busy[k] = true;
     off += m;

@@ -4831,12 +4831,10 @@ __device__ __forceinline__ void expand_job(const KArgs &a, const TileJob &tj, co
         __builtin_amdgcn_global_load_lds((const void *)(src + off),
                                          (__attribute__((address_space(3))) void *)(kspan + off / 4), 16, 0, 0);
   }
-  // every run meeting [v0, lim) must sit in lanes 0..62 (its end is the next lane's start),
-  // and no row of EX_ROW values may hold two run starts (rows meet at most two runs)
-  const int32_t rs = W.start > v0 && W.start < lim && ((W.start - v0) & (EX_ROW - 1)) ? (W.start - v0) / EX_ROW : -1 - lane;
-  const int32_t rs_next = (int32_t)shfl32((uint32_t)rs, min(lane + 1, 63));
-  const bool fits = staged && (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, 63) >= lim &&
-                    !ballot(lane < 63 && rs >= 0 && rs == rs_next);
+  // every run meeting [v0, lim) must sit in lanes 0..62 (its end is the next
+  // lane's start); rows meeting more than two runs (short RLE runs among
+  // bit-packed ones: bit width 1) take the general row path
+  const bool fits = staged && (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, 63) >= lim;
   STAMP(2);
   if (!fits) {
     for (int32_t c = v0; c < lim; c += 512)
@@ -4891,7 +4889,9 @@ __device__ __forceinline__ void expand_job(const KArgs &a, const TileJob &tj, co
       rs1[r] = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, ri + 1);
       rc0[r] = (int32_t)__builtin_amdgcn_readlane((uint32_t)w_c, ri);
       rc1[r] = (int32_t)__builtin_amdgcn_readlane((uint32_t)w_c, ri + 1);
-      all_fast &= rl < lim && rh - rl == EX_ROW && ((okm >> ri) & 1) && (rs1[r] >= rh || ((okm >> (ri + 1)) & 1));
+      const int32_t rs2 = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, min(ri + 2, 63));
+      all_fast &= rl < lim && rh - rl == EX_ROW && ((okm >> ri) & 1) &&
+                  (rs1[r] >= rh || (((okm >> (ri + 1)) & 1) && rs2 >= rh));
     }
     if (all_fast) {
       // straight-line: every row's LDS reads go out together.  The four keys of
@@ -4946,7 +4946,8 @@ __device__ __forceinline__ void expand_job(const KArgs &a, const TileJob &tj, co
       const int32_t s1 = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, ri + 1);
       const int32_t c0 = (int32_t)__builtin_amdgcn_readlane((uint32_t)w_c, ri);
       const bool one = s1 >= rh;  // the whole row inside run ri
-      const bool fast = ((okm >> ri) & 1) && (one || ((okm >> (ri + 1)) & 1)) && rh - rl == EX_ROW;
+      const bool two = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, min(ri + 2, 63)) >= rh;
+      const bool fast = ((okm >> ri) & 1) && (one || (((okm >> (ri + 1)) & 1) && two)) && rh - rl == EX_ROW;
       if (fast) {  // full row, bit-packed runs only, nothing past the stream end
         uint32_t lb0;
         if (one) {
@@ -4973,16 +4974,38 @@ __device__ __forceinline__ void expand_job(const KArgs &a, const TileJob &tj, co
         kmax = max(kmax, max(max(key[r][0], key[r][1]), max(key[r][2], key[r][3])));
         continue;
       }
-      const int32_t s0 = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, ri);
-      const uint32_t p0 = __builtin_amdgcn_readlane(W.prm, ri), f0 = __builtin_amdgcn_readlane(W.rle, ri);
-      const uint32_t p1 = __builtin_amdgcn_readlane(W.prm, ri + 1), f1 = __builtin_amdgcn_readlane(W.rle, ri + 1);
+      // general row: each value's run among every run meeting the row (the
+      // row's first run, then each run starting inside it, wave-uniform)
+      int32_t sq[4];
+      uint32_t pq[4], fq[4];
+      {
+        const int32_t s0 = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, ri);
+        const uint32_t p0 = __builtin_amdgcn_readlane(W.prm, ri), f0 = __builtin_amdgcn_readlane(W.rle, ri);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          sq[q] = s0;
+          pq[q] = p0;
+          fq[q] = f0;
+        }
+        for (int x = ri + 1; x < 64; x++) {
+          const int32_t ns = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, x);
+          if (ns >= rh) break;
+          const uint32_t px = __builtin_amdgcn_readlane(W.prm, x), fx = __builtin_amdgcn_readlane(W.rle, x);
+#pragma unroll
+          for (int q = 0; q < 4; q++)
+            if (j0 + q >= ns) {
+              sq[q] = ns;
+              pq[q] = px;
+              fq[q] = fx;
+            }
+        }
+      }
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const int32_t j = j0 + q;
         const bool act = j < lim;
-        const bool sel = j >= s1;
-        const uint32_t pr = sel ? p1 : p0, fr = sel ? f1 : f0;
-        const int32_t sr = sel ? s1 : s0;
+        const uint32_t pr = pq[q], fr = fq[q];
+        const int32_t sr = sq[q];
         const int32_t bb = (int32_t)pr * 8 + (j - sr) * bw;  // stream bit of the key (pages < 256 MiB)
         const uint32_t lb = (fr || !act) ? 0u : (uint32_t)(bb - (int32_t)lbase);
         const uint32_t *dw = kspan + (lb >> 5);
