@@ -2928,7 +2928,14 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
   }
   const int sz = (bw + 7) >> 3;  // RLE value bytes
   const uint8_t *nx_ab = nullptr;  // window the chain table was built for
-  bool chain = false;              // short runs seen lately: try chain mode
+  // bit width 1 streams alternate short RLE and bit-packed runs from the
+  // start (pyarrow: ~70 runs a 20k-value page): chain mode at once, no exact
+  // step (and its register-window load) first
+  bool chain = bw == 1;  // short runs seen lately: try chain mode
+  // the chain window's bytes (lane l: 16 bytes at 1024 h + 16 l) and the
+  // 1 KiB after it, loaded with it: a window that moves on by half its size
+  // takes its second half and the prefetched 1 KiB, no load in the chain
+  u32x4 cwv[CW / 1024], cpf = u32x4{0, 0, 0, 0};
   while (v < n) {
     // ---- chain mode ----
     if (chain) {
@@ -2945,11 +2952,20 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
       // window's first half (bit width 1 pages: 5 window steps with 1 KiB, 2
       // with 2 KiB)
       if (!nx_ab || ks + hpos < nx_ab || (ks + hpos) - nx_ab > CW / 2) {
-        nx_ab = (const uint8_t *)((uintptr_t)(ks + hpos) & ~(uintptr_t)15);
-        u32x4 wv[CW / 1024];
+        const uint8_t *want = (const uint8_t *)((uintptr_t)(ks + hpos) & ~(uintptr_t)15);
+        u32x4 *wv = cwv;
+        if (CW == 2048 && nx_ab && want >= nx_ab + 1024 && want < nx_ab + 2048) {
+          nx_ab += 1024;  // slide: [old + 1 KiB, old + 3 KiB) holds hpos in its first half
+          cwv[0] = cwv[CW / 1024 - 1];
+          cwv[CW / 1024 - 1] = cpf;
+        } else {
+          nx_ab = want;
 #pragma unroll
-        for (int h = 0; h < CW / 1024; h++)
-          wv[h] = *(const __attribute__((address_space(1))) u32x4 *)(nx_ab + 1024 * h + 16 * lane);
+          for (int h = 0; h < CW / 1024; h++)
+            wv[h] = *(const __attribute__((address_space(1))) u32x4 *)(nx_ab + 1024 * h + 16 * lane);
+        }
+        if (CW == 2048)  // the next 1 KiB, in flight while this window is walked
+          cpf = *(const __attribute__((address_space(1))) u32x4 *)(nx_ab + CW + 16 * lane);
 #pragma unroll
         for (int h = 0; h < CW / 1024; h++) {
           *(u32x4 *)(lbytes + 1024 * h + 16 * lane) = wv[h];
