@@ -3732,23 +3732,37 @@ __device__ __forceinline__ uint64_t pick4_64(const uint64_t (&v)[4], int j) {
 }
 
 // Bits of one step of a nested column (≤ 256 positions starting at global bit
-// b0; this lane's four at relative positions rel[k], set where on[k]) gathered
-// in LDS with ds_or, then written a word per lane: plain stores for the words
-// the step covers whole, atomicOr for the partial first/last word (shared with
-// the neighbouring step or page).  Replaces one global atomic per set bit.
-__device__ __forceinline__ void wave_bitmap(uint32_t *lw, uint32_t *gbm, int64_t b0, int total, const int (&rel)[4],
-                                            const bool (&on)[4]) {
+// b0): the produced entries (prod) hold the positions [0, total) in entry
+// order (rel[k]: entry k's position, an exclusive scan), each with bit on[k].
+// Every produced entry writes its bit as a byte of an LDS array (distinct
+// addresses: no atomics, no bank serialisation), then lane w packs the 32
+// bytes of word w (byte * 0x01020408 gathers a dword's four 0/1 bytes into
+// bits 24..27) and stores it: plain stores for the words the step covers
+// whole, atomicOr for the partial first/last word (shared with the
+// neighbouring step or page).  Replaces one global atomic per set bit and the
+// former LDS ds_or (up to 32 lanes on one word).
+__device__ __forceinline__ uint32_t pack_bytes16(const u32x4 &x) {
+  // (bytes outside the step hold stale LDS: each byte's low bit only, so no
+  // stale byte carries into a neighbour's bit)
+  const uint32_t m = 0x01020408u, b = 0x01010101u;
+  return (((x.x & b) * m) >> 24 & 15u) | ((((x.y & b) * m) >> 24 & 15u) << 4) |
+         ((((x.z & b) * m) >> 24 & 15u) << 8) | ((((x.w & b) * m) >> 24 & 15u) << 12);
+}
+__device__ __forceinline__ void wave_bitmap(uint8_t *lb, uint32_t *gbm, int64_t b0, int total, const int (&rel)[4],
+                                            const bool (&prod)[4], const bool (&on)[4]) {
   const int lane = lane_id();
   const int sh = (int)(b0 & 31);
   const int nw = (sh + total + 31) >> 5;  // <= 9
-  if (lane < 9) lw[lane] = 0;
-  wave_lds_sync();
 #pragma unroll
   for (int k = 0; k < 4; k++)
-    if (on[k]) atomicOr(&lw[(sh + rel[k]) >> 5], 1u << ((sh + rel[k]) & 31));
+    if (prod[k]) lb[sh + rel[k]] = on[k] ? 1 : 0;
   wave_lds_sync();
   if (lane < nw) {
-    const uint32_t wv = lw[lane];
+    const u32x4 x0 = *(const u32x4 *)(lb + 32 * lane), x1 = *(const u32x4 *)(lb + 32 * lane + 16);
+    uint32_t wv = pack_bytes16(x0) | (pack_bytes16(x1) << 16);
+    // only positions [sh, sh + total) of the step are its bits
+    const int lo = max(sh - 32 * lane, 0), hi = min(sh + total - 32 * lane, 32);
+    wv &= (hi >= 32 ? 0xffffffffu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
     uint32_t *g = gbm + (b0 >> 5) + lane;
     const bool edge = (lane == 0 && sh != 0) || (lane == nw - 1 && ((sh + total) & 31) != 0);
     if (!edge) *g = wv;
@@ -4015,8 +4029,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   }
   __shared__ BaLds ba_all[4];  // PLAIN BYTE_ARRAY length walk, one per wave
   BaLds &bl = ba_all[threadIdx.x >> 6];
-  __shared__ uint32_t bmw_all[4][12];  // nested-column bitmap words of a step
-  uint32_t *bmw = bmw_all[threadIdx.x >> 6];
+  __shared__ __attribute__((aligned(16))) uint8_t bmw_all[4][320];  // nested-column bitmap bytes of a step
+  uint8_t *bmw = bmw_all[threadIdx.x >> 6];
   // lists of 4/8-byte dictionary values (KIND 3): a dictionary of up to
   // DEC_DICT_LDS bytes is copied into the wave's LDS once, and the step's
   // gathers read it there instead of from L2 (one dependent global round trip
@@ -4185,10 +4199,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
       const int32_t rbase = wave_excl_scan32(nr, &mrows);
       int ri = 0, si = 0;
       int rrel[4];
-      bool lv[4];
+      bool lv[4], rp[4];
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         rrel[k] = rbase + ri;
+        rp[k] = act[k] && r[k] == 0;
         lv[k] = act[k] && r[k] == 0 && (int)dl[k] >= c.rep_def - 1;
         if (act[k] && r[k] == 0) {
           int64_t row = pi.row_base + row_run + rbase + ri;
@@ -4197,7 +4212,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
         }
         si += slot[k];
       }
-      if (c.list_validity) wave_bitmap(bmw, c.list_validity, pi.row_base + row_run, mrows, rrel, lv);
+      if (c.list_validity) wave_bitmap(bmw, c.list_validity, pi.row_base + row_run, mrows, rrel, rp, lv);
       row_run += mrows;
     }
 
@@ -4554,7 +4569,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
           sv[k] = slot[k] && valid[k];
           si += slot[k];
         }
-        wave_bitmap(bmw, c.validity, slot_base + slot_run, mslots, srel, sv);
+        wave_bitmap(bmw, c.validity, slot_base + slot_run, mslots, srel, slot, sv);
       }
     }
     slot_run += mslots;
