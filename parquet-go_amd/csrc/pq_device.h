@@ -43,43 +43,41 @@ template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
 }
+// v from the lane CTRL names, 0 where there is none (row_shr past the row
+// start) and in the rows outside ROWS: no lane masks, so no per-step
+// v_cndmask and no loop-invariant mask registers (k_snappy spilled them)
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t dpp_z(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, true);
+}
 template <bool MAX>
 __device__ __forceinline__ uint32_t wave_incl_dpp(uint32_t v) {
-  const int lane = lane_id(), rl = lane & 15;
-  uint32_t t;
-  t = dpp_mov<0x111>(v);  // row_shr:1
-  if (rl >= 1) v = MAX ? max(v, t) : v + t;
-  t = dpp_mov<0x112>(v);  // row_shr:2
-  if (rl >= 2) v = MAX ? max(v, t) : v + t;
-  t = dpp_mov<0x114>(v);  // row_shr:4
-  if (rl >= 4) v = MAX ? max(v, t) : v + t;
-  t = dpp_mov<0x118>(v);  // row_shr:8
-  if (rl >= 8) v = MAX ? max(v, t) : v + t;
-  t = dpp_mov<0x142>(v);  // row_bcast:15
-  if ((lane & 31) >= 16) v = MAX ? max(v, t) : v + t;
-  t = dpp_mov<0x143>(v);  // row_bcast:31
-  if (lane >= 32) v = MAX ? max(v, t) : v + t;
+  // (0 is the identity of both + and unsigned max)
+#define PQ_STEP(C, R)                \
+  do {                               \
+    const uint32_t t = dpp_z<C, R>(v); \
+    v = MAX ? max(v, t) : v + t;     \
+  } while (0)
+  PQ_STEP(0x111, 0xf);  // row_shr:1
+  PQ_STEP(0x112, 0xf);  // row_shr:2
+  PQ_STEP(0x114, 0xf);  // row_shr:4
+  PQ_STEP(0x118, 0xf);  // row_shr:8
+  PQ_STEP(0x142, 0xa);  // row_bcast:15 into rows 1 and 3
+  PQ_STEP(0x143, 0xc);  // row_bcast:31 into rows 2 and 3
+#undef PQ_STEP
   return v;
 }
-template <int CTRL>
-__device__ __forceinline__ uint64_t dpp_mov64(uint64_t v) {
-  return ((uint64_t)dpp_mov<CTRL>((uint32_t)(v >> 32)) << 32) | dpp_mov<CTRL>((uint32_t)v);
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint64_t dpp_z64(uint64_t v) {
+  return ((uint64_t)dpp_z<CTRL, ROWS>((uint32_t)(v >> 32)) << 32) | dpp_z<CTRL, ROWS>((uint32_t)v);
 }
 __device__ __forceinline__ uint64_t wave_incl_add64_dpp(uint64_t v) {
-  const int lane = lane_id(), rl = lane & 15;
-  uint64_t t;
-  t = dpp_mov64<0x111>(v);
-  if (rl >= 1) v += t;
-  t = dpp_mov64<0x112>(v);
-  if (rl >= 2) v += t;
-  t = dpp_mov64<0x114>(v);
-  if (rl >= 4) v += t;
-  t = dpp_mov64<0x118>(v);
-  if (rl >= 8) v += t;
-  t = dpp_mov64<0x142>(v);
-  if ((lane & 31) >= 16) v += t;
-  t = dpp_mov64<0x143>(v);
-  if (lane >= 32) v += t;
+  v += dpp_z64<0x111>(v);
+  v += dpp_z64<0x112>(v);
+  v += dpp_z64<0x114>(v);
+  v += dpp_z64<0x118>(v);
+  v += dpp_z64<0x142, 0xa>(v);
+  v += dpp_z64<0x143, 0xc>(v);
   return v;
 }
 __device__ __forceinline__ int32_t wave_incl_scan32_impl(int32_t v) { return (int32_t)wave_incl_dpp<false>((uint32_t)v); }

@@ -353,7 +353,7 @@ struct SnapLds {  // per wave
       uint4 tok[SB_TOK];        // {out_rel, len | literal << 31 | prefilled << 30, literal: window byte / copy: offset, 0}
       uint2 bmc[SB_OUT / 32];   // token-start bits, tokens starting in earlier words
     };
-    uint16_t jt[2][320];        // chain walk: jump tables J_b, J_b+1 over window positions 0..256
+    uint32_t jt[260];           // token chain: entry addresses of J_b over window positions 0..256
   };
 };
 
@@ -368,6 +368,8 @@ struct SnapLds {  // per wave
       L.tprev = t_;                                                \
     }                                                              \
   } while (0)
+#elif defined(PQ_SNAP_MARKS)
+#define SNAP_T(i) asm volatile(";SNAPMARK " #i)
 #else
 #define SNAP_T(i) \
   do {            \
@@ -410,14 +412,47 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// LDS byte addresses (address space 3): the chain table holds them, so a hop
+// is one ds_read_b32 with no address arithmetic, and byte copies add
+// immediate offsets to them.  (A workgroup's LDS addresses start at 0 and
+// k_snappy's stay below 64 KiB.)
+#define PQ_LDS __attribute__((address_space(3)))
+__device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(uintptr_t)(const PQ_LDS void *)p; }
+__device__ __forceinline__ uint32_t lds_u8(uint32_t a) { return *(const PQ_LDS uint8_t *)(uintptr_t)a; }
+__device__ __forceinline__ uint32_t lds_u32(uint32_t a) { return *(const PQ_LDS uint32_t *)(uintptr_t)a; }
+__device__ __forceinline__ void lds_st8(uint32_t a, uint32_t v) { *(PQ_LDS uint8_t *)(uintptr_t)a = (uint8_t)v; }
+__device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) { *(PQ_LDS uint32_t *)(uintptr_t)a = v; }
+
+// Tag tables of k_snappy (one per workgroup, LDS): [tag] the stream bytes of
+// a short token (a literal's tag and payload, a copy's header; 255 for a long
+// literal's tag), [256 + tag] its output length (0: long literal) —
+// decode_other.go:27-86's cases as two lookups instead of a branch per case.
+constexpr int SNAP_LUT = 512;
+__device__ __forceinline__ void snappy_lut_init(uint8_t *lut, int tag) {
+  const uint32_t t = (uint32_t)tag & 3, x = (uint32_t)tag >> 2;
+  uint32_t need, len;
+  if (t == 0) {
+    need = x >= 60 ? 255u : x + 2;
+    len = x >= 60 ? 0u : x + 1;
+  } else if (t == 1) {
+    need = 2;
+    len = 4 + (x & 7);
+  } else {
+    need = t == 2 ? 3u : 5u;
+    len = x + 1;
+  }
+  lut[tag] = (uint8_t)need;
+  lut[256 + tag] = (uint8_t)len;
+}
+
 // One batch starting at the short token at s.  Returns false on a corrupt
-// token (err set); advances s / dpos / F otherwise.
-__device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const uint8_t *src, int64_t slen, uint8_t *dst,
-                                             int64_t dl, int64_t seg_lo, bool write, int64_t &s, int64_t &dpos, int64_t &F,
-                                             uint32_t &err, const uint8_t *pend_src, int64_t pend_dpos,
-                                             int64_t &pend_len, int ndefer, int64_t def_dst, int64_t def_len,
-                                             uint64_t def_src, int lane, const uint8_t *in_end, int64_t &pf_s,
-                                             int64_t &pf_F, uint32_t &pg0, uint32_t &pg1, uint32_t &pg2) {
+// token (err set); advances s / dpos / F otherwise.  `lut`: the tag tables.
+__device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, uint32_t lut, const uint8_t *src, int64_t slen,
+                                             uint8_t *dst, int64_t dl, int64_t seg_lo, bool write, int64_t &s,
+                                             int64_t &dpos, int64_t &F, uint32_t &err, const uint8_t *pend_src,
+                                             int64_t pend_dpos, int64_t &pend_len, int ndefer, int64_t def_dst,
+                                             int64_t def_len, uint64_t def_src, int lane, const uint8_t *in_end,
+                                             int64_t &pf_s, int64_t &pf_F, uint32_t &pg0, uint32_t &pg1, uint32_t &pg2) {
   SNAP_T(-1);
   // 1. stage the window (aligned base; `sh` = position of byte s); the
   // previous batch prefetched it into pg0..pg2 when it ended at s
@@ -444,64 +479,79 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
   L.win[lane] = g0;
   L.win[lane + 64] = g1;
   if (lane < 4) L.win[lane + 128] = g2;
-  const uint32_t pk01 = snappy_tok_class(g0 & 0xff) | (snappy_tok_class((g0 >> 8) & 0xff) << 16);
-  const uint32_t pk23 = snappy_tok_class((g0 >> 16) & 0xff) | (snappy_tok_class(g0 >> 24) << 16);
-  SNAP_T(0);
-  // 2. the token chain over the first 256 window positions by pointer
-  // jumping: J_0(i) = i + size(i) (256: stop), J_b+1 = J_b o J_b; lane m
-  // applies J_b for the set bits b of m starting at sh, so it lands on the
-  // m-th token (no serial walk on the scalar unit)
-  const int64_t lim64 = (int64_t)sh + (slen - s) - 1;  // last position inside the block
-  const int lim = lim64 < 255 ? (int)lim64 : 255;
-  int pos = sh;
-  uint16_t *ja = L.jt[0], *jb = L.jt[1];
+  const uint32_t wb = lds_addr(L.win);     // window byte 0
+  const uint32_t tb = lds_addr(L.jt);   // chain table (dwords): the entry of position i at tb + 4 i
+  const uint32_t stop = tb + 4 * 256;      // position 256: the chain's end (its entry points at itself)
+  wave_lds_sync();
+  // J_0 of positions lane + 64 j: the entry address of the position after the
+  // token there (tag tables), or the end
+  uint32_t J[4];
 #pragma unroll
   for (int j = 0; j < 4; j++) {
-    const int i = 4 * lane + j;
-    const uint32_t w = j < 2 ? pk01 : pk23;
-    const uint32_t p = (j & 1) ? (w >> 16) : (w & 0xffff);
-    const int nx = i + (int)(p & 0xff);
-    ja[i] = (uint16_t)((p == 0 || i > lim || nx > 256) ? 256 : nx);
+    const uint32_t tag = lds_u8(wb + (uint32_t)lane + 64 * j);
+    J[j] = min(tb + 4 * ((uint32_t)lane + 64 * j) + 4 * lds_u8(lut + tag), stop);
   }
-  if (lane == 0) {
-    ja[256] = 256;
-    jb[256] = 256;
-  }
+#pragma unroll
+  for (int j = 0; j < 4; j++) lds_st32(tb + 4 * (uint32_t)lane + 256 * j, J[j]);
+  if (lane == 0) lds_st32(stop, stop);
+  SNAP_T(0);
+  // 2. the token chain by pointer jumping, in place: J_b+1 = J_b o J_b (a
+  // round's reads are all issued before its writes; the wave's LDS accesses
+  // run in order); lane m applies J_b for the set bits b of m starting at
+  // sh, so it lands on the m-th token
   wave_lds_sync();
+  uint32_t P = tb + 4 * (uint32_t)sh;
 #pragma unroll
   for (int b = 0; b < 6; b++) {
-    // every read of a round issued before its writes (the tables are both
-    // LDS: the compiler cannot reorder a read past a write that may alias
-    // it, and each read-modify-write pair cost an LDS round trip)
-    const int hop = ja[pos];
+    const uint32_t hop = lds_u32(P);
     if (b < 5) {
-      const uint2 q = *(const uint2 *)(ja + 4 * lane);  // J_b(4 lane .. 4 lane + 3)
-      const uint32_t n0 = ja[q.x & 0xffff], n1 = ja[q.x >> 16], n2 = ja[q.y & 0xffff], n3 = ja[q.y >> 16];
-      *(uint2 *)(jb + 4 * lane) = make_uint2(n0 | (n1 << 16), n2 | (n3 << 16));
+      uint32_t n[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) n[j] = lds_u32(J[j]);
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        J[j] = n[j];
+        lds_st32(tb + 4 * (uint32_t)lane + 256 * j, n[j]);
+      }
     }
-    if ((lane >> b) & 1) pos = hop;
-    if (b < 5) {
-      wave_lds_sync();
-      uint16_t *t = ja;
-      ja = jb;
-      jb = t;
-    }
+    if ((lane >> b) & 1) P = hop;
+    if (b < 5) wave_lds_sync();
   }
-  const uint32_t w01 = shfl32(pk01, (pos >> 2) & 63), w23 = shfl32(pk23, (pos >> 2) & 63);
-  const uint32_t wp = (pos & 2) ? w23 : w01;
-  const uint32_t pc = (pos & 1) ? (wp >> 16) : (wp & 0xffff);  // class of this lane's token
-  const bool valid = pos <= lim && pc != 0;
-  const int32_t incl = wave_incl_scan32(valid ? (int32_t)(pc >> 8) : 0);
-  // a prefix of the lanes: tokens that fit the batch and start before the end
-  // of the output (of the segment: a later token belongs to the next one)
-  const int64_t room = dl - dpos;
-  const int ntok = __builtin_popcountll(ballot(valid && incl <= SB_OUT && (int64_t)incl - (int64_t)(pc >> 8) < room));
+  // 3. decode token `lane` (its tag from the tables, its offset from the 5
+  // bytes at it) and check it (decode_other.go:14-101 order: header inside
+  // src, length <= remaining dst, 0 < offset <= d)
+  const int64_t lim64 = (int64_t)sh + (slen - s) - 1;  // last position inside the block
+  const uint32_t lim = lim64 < 255 ? (uint32_t)lim64 : 255u;
+  const uint32_t pos = (P - tb) >> 2;
+  const uint32_t pa = wb + pos;
+  const uint32_t tag = lds_u8(pa);
+  const uint32_t need = lds_u8(lut + tag), len0 = lds_u8(lut + 256 + tag);
+  const uint32_t d0 = lds_u32(pa & ~3u), d1 = lds_u32((pa & ~3u) + 4);
+  const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, pa & 3u), hi = __builtin_amdgcn_alignbyte(0u, d1, pa & 3u);
+  const uint32_t t = tag & 3;
+  const bool lit = t == 0;
+  const uint32_t c1 = ((tag >> 5) << 8) | ((lo >> 8) & 0xffu);  // tagCopy1
+  const uint32_t c2 = (lo >> 8) & 0xffffu;                      // tagCopy2
+  const uint32_t c4 = __builtin_amdgcn_alignbyte(hi, lo, 1u);   // tagCopy4
+  // literal: window position of its bytes / copy: offset
+  const uint32_t x = lit ? pos + 1 : t == 1 ? c1 : t == 2 ? c2 : c4;
+  const bool valid = P <= tb + 4 * lim && len0 != 0;
+  const int64_t rem64 = slen - s, room64 = dl - dpos;
+  const int32_t rem = rem64 < 0x40000000 ? (int32_t)rem64 : 0x40000000;  // stream bytes from s
+  const int32_t room = room64 < 0x40000000 ? (int32_t)room64 : 0x40000000;
+  const int32_t tend = (int32_t)pos - sh + (int32_t)need;  // the token's end, from s
+  const uint32_t vlen = valid ? len0 : 0u;
+  const int32_t incl = (int32_t)wave_incl_dpp<false>(vlen);
+  // the leading lanes: tokens that fit the batch and start before the end of
+  // the output (of the segment: a later token belongs to the next one)
+  const uint64_t okm = ballot(valid && incl <= SB_OUT && incl - (int32_t)vlen < room);
+  const int ntok = ~okm ? (int)__builtin_ctzll(~okm) : 64;
   if (ntok == 0) {  // output complete but tokens remain, or a token crosses the segment end
     err = E_SNAPPY;
     return false;
   }
   const int T = (int)__builtin_amdgcn_readlane(incl, ntok - 1);
-  const int cur = (int)__builtin_amdgcn_readlane(pos, ntok - 1) + (int)(__builtin_amdgcn_readlane(pc, ntok - 1) & 0xff);
+  const int cur = (int)__builtin_amdgcn_readlane(tend, ntok - 1) + sh;
   if (PQ_PF_EARLY) {
     // the next batch's window, prefetched as soon as this batch's end is
     // known: its loads overlap this batch's decode, far copies and output
@@ -515,53 +565,16 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
       pf_F = F;
     }
   }
-  const uint32_t tokpos = (uint32_t)pos;
-  wave_lds_sync();
   SNAP_T(1);
-  // 3. decode + check token `lane`
   const bool act = lane < ntok;
-  uint32_t len = 0, x = 0;
-  bool lit = false, bad = false;
-  if (act) {
-    const int pos = (int)tokpos;
-    uint64_t hv = (uint64_t)L.win[pos >> 2] | ((uint64_t)L.win[(pos >> 2) + 1] << 32);
-    hv >>= (pos & 3) * 8;
-    const uint32_t tag = (uint32_t)hv & 0xff;
-    const int64_t sabs = s + (pos - sh);  // stream position of the tag
-    if ((tag & 3) == 0) {
-      lit = true;
-      len = (tag >> 2) + 1;
-      x = (uint32_t)pos + 1;
-      bad = sabs + 1 + (int64_t)len > slen;
-    } else {
-      int hs;
-      if ((tag & 3) == 1) {
-        hs = 2;
-        len = 4 + ((tag >> 2) & 7);
-        x = ((tag & 0xe0) << 3) | (uint32_t)((hv >> 8) & 0xff);
-      } else if ((tag & 3) == 2) {
-        hs = 3;
-        len = 1 + (tag >> 2);
-        x = (uint32_t)((hv >> 8) & 0xffff);
-      } else {
-        hs = 5;
-        len = 1 + (tag >> 2);
-        x = (uint32_t)(hv >> 8);
-      }
-      bad = sabs + hs > slen;
-    }
-  }
-  int32_t total = 0;
-  const int32_t out_rel = wave_excl_scan32((int32_t)len, &total);
-  if (act) {
-    const int64_t d = dpos + out_rel;
-    bad |= (int64_t)len > dl - d;
-    if (!lit) bad |= x == 0 || (int64_t)x > d - seg_lo;  // a segment's copies stay inside it
-  }
-  if (ballot(act && bad)) {
+  const uint32_t len = act ? len0 : 0u;
+  const int32_t out_rel = incl - (int32_t)len;
+  const uint32_t back = (uint32_t)(dpos - seg_lo);  // output before the batch (< 2^31: a page's size is an int32)
+  if (ballot(act && (tend > rem || incl > room || (!lit && (x == 0 || x > back + (uint32_t)out_rel))))) {
     err = E_SNAPPY;
     return false;
   }
+  const int32_t total = T;
   SNAP_T(2);
   if (write) {
     if (pend_len) {  // the history must hold the last deferred literal's tail
@@ -573,16 +586,17 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
     // payload) is loaded by its own lane and written to the history at its
     // output position, all such loads in flight together
     const int64_t near_lo = dpos + T - RING;  // older bytes may be overwritten by this batch
-    const int64_t S = dpos + out_rel - (int64_t)x;  // copy: absolute source start
+    const uint32_t b32 = (uint32_t)dpos;      // (ring positions: low 32 bits suffice)
+    const bool far = act && !lit && x > (uint32_t)(out_rel + RING - T);  // source starts before near_lo
     bool pre = false, fdefer = false;
     uint64_t fq0 = 0, fq1 = 0;
     int fsh = 0;
-    if (ballot(act && !lit && S < near_lo)) {
+    if (ballot(far)) {
+      const int64_t S = dpos + out_rel - (int64_t)x;  // absolute source start
       // this wave's earlier staging stores must be visible to the loads below
       // (unless every source lies in output known written)
-      if (ballot(act && !lit && S < near_lo && S + (int64_t)len > F_safe))
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-      pre = act && !lit && x >= len && S + (int64_t)len <= near_lo;
+      if (ballot(far && S + (int64_t)len > F_safe)) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      pre = far && x >= len && S + (int64_t)len <= near_lo;
       uintptr_t fsrc = pre ? (uintptr_t)(dst + S) : 0;
       bool in_payload = false;
       for (int k2 = 0; k2 < ndefer; k2++) {  // every lane active: readlane of the deferred-literal table
@@ -603,8 +617,8 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
       }
       if (pre && PQ_FAR_DEFER && (int)(fsrc & 7) + (int)len <= 16) {
         // a short far copy (two aligned qwords): loads issued now, bytes
-        // written to the history after the token tables are built, so the
-        // round trip overlaps them
+        // written to the history with the short tokens', so the round trip
+        // overlaps the steps between
         const uintptr_t b8 = fsrc & ~(uintptr_t)7;
         const uint64_t *qp = (const uint64_t *)b8;
         fq0 = in_payload ? qp[0] : __hip_atomic_load(qp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -648,56 +662,72 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, const ui
     // Token-parallel output (PQ_SNAP_TOKEN): when every copy's source is
     // either already in the history (older than the batch: `near`), or was
     // prefilled / is being loaded (`pre`), or lies partly inside the batch
-    // (`dep`, at most SNAP_DEP_MAX of them), the tokens are written by their
-    // own lanes — literals from the window, near copies history to history,
-    // all at once — and then the dep copies one after another in token order,
-    // a byte a lane (an overlapping copy by pattern: byte r from
-    // S + r mod offset).  No token table, no start bitmap, no per-byte chase.
-    const bool nearc = act && !lit && !pre && S >= near_lo && S + (int64_t)len <= dpos;
-    const bool depc = act && !lit && !pre && S >= near_lo && S + (int64_t)len > dpos;
+    // (`dep`), the tokens are written by their own lanes — literals from the
+    // window, near copies history to history, short far copies from their
+    // loaded qwords, all at once — and then the dep copies one after another
+    // in token order, a byte a lane (an overlapping copy by pattern: byte r
+    // from S + r mod offset).  No token table, no start bitmap, no per-byte
+    // chase.
+    const bool nearc = act && !lit && !far && x >= (uint32_t)out_rel + len;
+    const bool depc = act && !lit && !far && x < (uint32_t)out_rel + len;
     const uint64_t depm = ballot(depc);
-    const bool fast = PQ_SNAP_TOKEN && !ballot(act && !lit && !pre && S < near_lo) && __popcll(depm) <= SNAP_DEP_MAX;
+    const bool fast = PQ_SNAP_TOKEN && !ballot(far && !pre);
     if (fast) {
-      const int64_t o = dpos + out_rel;
-      // tokens of up to SNAP_TOK_SHORT bytes by their own lanes, two bytes a
-      // step; longer ones (long literals) one after another by the whole wave
-      const bool indep = act && (lit || nearc);
-      const uint32_t mylen = indep && len <= SNAP_TOK_SHORT ? len : 0u;
-      const uint32_t maxlen = __builtin_amdgcn_readlane(wave_incl_dpp<true>(mylen), 63);
-      for (uint32_t i = 0; i < maxlen; i += 2) {
-        uint8_t b0 = 0, b1 = 0;
-        if (i < mylen) b0 = lit ? winb[x + i] : ring[(S + i) & RING_MASK];
-        if (i + 1 < mylen) b1 = lit ? winb[x + i + 1] : ring[(S + i + 1) & RING_MASK];
-        if (i < mylen) ring[(o + i) & RING_MASK] = b0;
-        if (i + 1 < mylen) ring[(o + i + 1) & RING_MASK] = b1;
+      const uint32_t rb = lds_addr(ring);
+      const uint32_t ro = (b32 + (uint32_t)out_rel) & RING_MASK;  // ring position of the token's output
+      // LDS address of the token's source bytes: the window, the history, or
+      // (a short far copy) its two qwords parked in the token-table area
+      uint32_t sa = lit ? wb + x : rb + ((b32 + (uint32_t)out_rel - x) & RING_MASK);
+      if (fdefer) {
+        L.tok[lane] = make_uint4((uint32_t)fq0, (uint32_t)(fq0 >> 32), (uint32_t)fq1, (uint32_t)(fq1 >> 32));
+        sa = lds_addr(&L.tok[lane]) + (uint32_t)fsh;
       }
-      for (uint64_t lm = ballot(indep && len > SNAP_TOK_SHORT); lm; lm &= lm - 1) {
+      // tokens of up to SNAP_TOK_SHORT bytes by their own lanes (all of a
+      // step's reads before its writes: one LDS round trip a step); longer
+      // ones (long literals) one after another by the whole wave
+      const bool shortc = act && (lit || nearc || fdefer) && len <= SNAP_TOK_SHORT;
+      const uint32_t mylen = shortc ? len : 0u;
+      const uint32_t da = rb + ro;
+      // a source or destination range that runs past the end of the ring
+      const bool wrap = shortc && (ro + len > RING || (!lit && !fdefer && (sa - rb) + len > RING));
+      if (!ballot(wrap)) {
+#pragma unroll
+        for (int h = 0; h < SNAP_TOK_SHORT / 8; h++) {
+          if (h > 0 && !ballot(mylen > 8u * h)) break;
+          uint32_t v[8];
+#pragma unroll
+          for (int i = 0; i < 8; i++) v[i] = lds_u8(sa + 8 * h + i);  // (bytes past the token: unused)
+#pragma unroll
+          for (int i = 0; i < 8; i++)
+            if (8u * h + i < mylen) lds_st8(da + 8 * h + i, v[i]);
+        }
+      } else {
+        for (uint32_t i = 0; i < SNAP_TOK_SHORT; i++) {
+          if (!ballot(i < mylen)) break;
+          if (i < mylen) {
+            const uint32_t sb = lit || fdefer ? sa + i : rb + ((sa - rb + i) & RING_MASK);
+            lds_st8(rb + ((ro + i) & RING_MASK), lds_u8(sb));
+          }
+        }
+      }
+      for (uint64_t lm = ballot(act && (lit || nearc) && len > SNAP_TOK_SHORT); lm; lm &= lm - 1) {
         const int k = (int)__builtin_ctzll(lm);
-        const int64_t ok = dpos + (int64_t)__builtin_amdgcn_readlane(out_rel, k);
+        const uint32_t ok = b32 + (uint32_t)__builtin_amdgcn_readlane(out_rel, k);
         const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)len, k);
         const uint32_t xk = (uint32_t)__builtin_amdgcn_readlane((int)x, k);
         const bool litk = __builtin_amdgcn_readlane((int)lit, k) != 0;
         if ((uint32_t)lane < lk) ring[(ok + lane) & RING_MASK] = litk ? winb[xk + lane] : ring[(ok - xk + lane) & RING_MASK];
       }
-      if (fdefer) {  // the deferred far copies' bytes
-#pragma unroll
-        for (int i2 = 0; i2 < 16; i2++) {
-          if (i2 >= (int)len) break;
-          const int bi = fsh + i2;
-          ring[(o + i2) & RING_MASK] = (uint8_t)((bi < 8 ? fq0 >> (8 * bi) : fq1 >> (8 * (bi - 8))) & 0xffu);
-        }
-      }
       wave_lds_sync();
       SNAP_T(4);
       for (uint64_t dm = depm; dm; dm &= dm - 1) {
         const int k = (int)__builtin_ctzll(dm);
-        const int64_t ok = dpos + (int64_t)__builtin_amdgcn_readlane(out_rel, k);
+        const uint32_t ok = b32 + (uint32_t)__builtin_amdgcn_readlane(out_rel, k);
         const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)len, k);
         const uint32_t xk = (uint32_t)__builtin_amdgcn_readlane((int)x, k);
-        if ((uint32_t)lane < lk) {
-          const int64_t sb = ok - (int64_t)xk + (int64_t)(xk >= lk ? (uint32_t)lane : (uint32_t)lane % xk);
-          ring[(ok + lane) & RING_MASK] = ring[sb & RING_MASK];
-        }
+        uint32_t r = (uint32_t)lane;
+        if (xk < lk) r = (uint32_t)lane % xk;  // (uniform branch) a repeated pattern
+        if ((uint32_t)lane < lk) ring[(ok + lane) & RING_MASK] = ring[(ok - xk + r) & RING_MASK];
         wave_lds_sync();
       }
     } else {
@@ -840,6 +870,9 @@ template <int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PQ_SNAPPY_WPE))) void k_snappy(KArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t ring_all[SNAPPY_WAVES][RING];
   __shared__ SnapLds sl_all[SNAPPY_WAVES];
+  __shared__ uint8_t snap_lut[SNAP_LUT];
+  snappy_lut_init(snap_lut, (int)threadIdx.x);  // (256 threads: one tag each)
+  __syncthreads();
   const int lane = lane_id();
   const int wv = (int)ufirst(threadIdx.x >> 6);  // wave-uniform (keeps per-wave state in SGPRs)
   const int wi = blockIdx.x * SNAPPY_WAVES + wv;
@@ -963,8 +996,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PQ_SNAPPY_W
     if ((tag & 3) != 0 || (tag >> 2) < 60) {
       // ---- short tokens (copies, literals <= 60 bytes): one batch of up to
       // SB_TOK tokens / SB_OUT output bytes per pass (snappy_batch)
-      if (!snappy_batch(L, ring, src, slen, dst, dl, seg_lo, write, s, dpos, F, err, pend_src, pend_dpos, pend_len, ndefer,
-                        def_dst, def_len, def_src, lane, a.in_end, pf_s, pf_F, pg0, pg1, pg2))
+      if (!snappy_batch(L, ring, lds_addr(snap_lut), src, slen, dst, dl, seg_lo, write, s, dpos, F, err, pend_src,
+                        pend_dpos, pend_len, ndefer, def_dst, def_len, def_src, lane, a.in_end, pf_s, pf_F, pg0, pg1, pg2))
         break;
       continue;
     }
@@ -2931,7 +2964,11 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
   // bit width 1 streams alternate short RLE and bit-packed runs from the
   // start (pyarrow: ~70 runs a 20k-value page): chain mode at once, no exact
   // step (and its register-window load) first
+#ifdef PQ_CHAIN_OFF
+  bool chain = false;  // (analysis build: the exact serial step only)
+#else
   bool chain = bw == 1;  // short runs seen lately: try chain mode
+#endif
   // the chain window's bytes (lane l: 16 bytes at 1024 h + 16 l) and the
   // 1 KiB after it, loaded with it: a window that moves on by half its size
   // takes its second half and the prefetched 1 KiB, no load in the chain
@@ -3099,7 +3136,9 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
       v = e;
       hpos += g * (int64_t)bw;
       if (v >= n) break;
+#ifndef PQ_CHAIN_OFF
       chain = hpos - h0 < 48;  // a short run: the next ones may chain
+#endif
       // a train?  only if the next header repeats this one (a uvarint's bytes
       // are fixed by its value and length)
       const int64_t stride = hl + g * (int64_t)bw;
@@ -3148,7 +3187,9 @@ __device__ void walk_runs(const KArgs &a, const PageDesc &d, PageInfo *pi, const
       const int64_t e = min<int64_t>(v + cr, (int64_t)n);
       R.emit(v, e, (uint32_t)v | RUN_RLE, val, hpos, -1);
       v = e;
+#ifndef PQ_CHAIN_OFF
       chain = true;
+#endif
     }
   }
   R.flush();
