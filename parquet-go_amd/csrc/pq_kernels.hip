@@ -353,7 +353,7 @@ struct SnapLds {  // per wave
       uint4 tok[SB_TOK];        // {out_rel, len | literal << 31 | prefilled << 30, literal: window byte / copy: offset, 0}
       uint2 bmc[SB_OUT / 32];   // token-start bits, tokens starting in earlier words
     };
-    uint32_t jt[260];           // token chain: entry addresses of J_b over window positions 0..256
+    uint16_t jt[264];           // token chain: entry addresses of J_b over window positions 0..256
   };
 };
 
@@ -413,14 +413,19 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // LDS byte addresses (address space 3): the chain table holds them, so a hop
-// is one ds_read_b32 with no address arithmetic, and byte copies add
+// is one ds_read_u16 with no address arithmetic, and byte copies add
 // immediate offsets to them.  (A workgroup's LDS addresses start at 0 and
 // k_snappy's stay below 64 KiB.)
 #define PQ_LDS __attribute__((address_space(3)))
 __device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(uintptr_t)(const PQ_LDS void *)p; }
 __device__ __forceinline__ uint32_t lds_u8(uint32_t a) { return *(const PQ_LDS uint8_t *)(uintptr_t)a; }
+__device__ __forceinline__ uint32_t lds_u16(uint32_t a) { return *(const PQ_LDS uint16_t *)(uintptr_t)a; }
 __device__ __forceinline__ uint32_t lds_u32(uint32_t a) { return *(const PQ_LDS uint32_t *)(uintptr_t)a; }
 __device__ __forceinline__ void lds_st8(uint32_t a, uint32_t v) { *(PQ_LDS uint8_t *)(uintptr_t)a = (uint8_t)v; }
+__device__ __forceinline__ void lds_st16(uint32_t a, uint32_t v) { *(PQ_LDS uint16_t *)(uintptr_t)a = (uint16_t)v; }
+__device__ __forceinline__ void lds_st64(uint32_t a, uint32_t lo, uint32_t hi) {  // a: 8-byte aligned
+  *(PQ_LDS uint64_t *)(uintptr_t)a = ((uint64_t)hi << 32) | lo;
+}
 __device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) { *(PQ_LDS uint32_t *)(uintptr_t)a = v; }
 
 // Tag tables of k_snappy (one per workgroup, LDS): [tag] the stream bytes of
@@ -479,40 +484,39 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, uint32_t
   L.win[lane] = g0;
   L.win[lane + 64] = g1;
   if (lane < 4) L.win[lane + 128] = g2;
-  const uint32_t wb = lds_addr(L.win);     // window byte 0
-  const uint32_t tb = lds_addr(L.jt);   // chain table (dwords): the entry of position i at tb + 4 i
-  const uint32_t stop = tb + 4 * 256;      // position 256: the chain's end (its entry points at itself)
-  wave_lds_sync();
-  // J_0 of positions lane + 64 j: the entry address of the position after the
-  // token there (tag tables), or the end
+  const uint32_t wb = lds_addr(L.win);  // window byte 0
+  const uint32_t tb = lds_addr(L.jt);   // chain table (u16): the entry of position i at tb + 2 i
+  const uint32_t stop = tb + 2 * 256;   // position 256: the chain's end (its entry points at itself)
+  // J_0 of this lane's positions 4 lane + j (the bytes of its window dword):
+  // the entry address of the position after a token starting there.  Token
+  // sizes SWAR over the 4 tags: a literal x + 2, copies 2 / 3 / 5 by a byte
+  // permute (a long literal's tag reads 62..65 here; the decode below cuts
+  // the batch at it)
+  const uint32_t t4 = g0 & 0x03030303u, x4 = (g0 >> 2) & 0x3f3f3f3fu;
+  const uint32_t mlit = __builtin_amdgcn_perm(0u, 0x000000ffu, t4);  // 0xff where a literal
+  const uint32_t need4 = ((x4 + 0x02020202u) & mlit) | (__builtin_amdgcn_perm(0u, 0x05030200u, t4) & ~mlit);
   uint32_t J[4];
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const uint32_t tag = lds_u8(wb + (uint32_t)lane + 64 * j);
-    J[j] = min(tb + 4 * ((uint32_t)lane + 64 * j) + 4 * lds_u8(lut + tag), stop);
-  }
-#pragma unroll
-  for (int j = 0; j < 4; j++) lds_st32(tb + 4 * (uint32_t)lane + 256 * j, J[j]);
-  if (lane == 0) lds_st32(stop, stop);
+  for (int j = 0; j < 4; j++) J[j] = tb + 2 * min(4 * (uint32_t)lane + j + ((need4 >> (8 * j)) & 0xffu), 256u);
+  lds_st64(tb + 8 * (uint32_t)lane, J[0] | (J[1] << 16), J[2] | (J[3] << 16));
+  if (lane == 0) lds_st16(stop, stop);
   SNAP_T(0);
   // 2. the token chain by pointer jumping, in place: J_b+1 = J_b o J_b (a
   // round's reads are all issued before its writes; the wave's LDS accesses
   // run in order); lane m applies J_b for the set bits b of m starting at
   // sh, so it lands on the m-th token
   wave_lds_sync();
-  uint32_t P = tb + 4 * (uint32_t)sh;
+  uint32_t P = tb + 2 * (uint32_t)sh;
 #pragma unroll
   for (int b = 0; b < 6; b++) {
-    const uint32_t hop = lds_u32(P);
+    const uint32_t hop = lds_u16(P);
     if (b < 5) {
       uint32_t n[4];
 #pragma unroll
-      for (int j = 0; j < 4; j++) n[j] = lds_u32(J[j]);
+      for (int j = 0; j < 4; j++) n[j] = lds_u16(J[j]);
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        J[j] = n[j];
-        lds_st32(tb + 4 * (uint32_t)lane + 256 * j, n[j]);
-      }
+      for (int j = 0; j < 4; j++) J[j] = n[j];
+      lds_st64(tb + 8 * (uint32_t)lane, n[0] | (n[1] << 16), n[2] | (n[3] << 16));
     }
     if ((lane >> b) & 1) P = hop;
     if (b < 5) wave_lds_sync();
@@ -522,7 +526,7 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, uint32_t
   // src, length <= remaining dst, 0 < offset <= d)
   const int64_t lim64 = (int64_t)sh + (slen - s) - 1;  // last position inside the block
   const uint32_t lim = lim64 < 255 ? (uint32_t)lim64 : 255u;
-  const uint32_t pos = (P - tb) >> 2;
+  const uint32_t pos = (P - tb) >> 1;
   const uint32_t pa = wb + pos;
   const uint32_t tag = lds_u8(pa);
   const uint32_t need = lds_u8(lut + tag), len0 = lds_u8(lut + 256 + tag);
@@ -535,7 +539,7 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, uint32_t
   const uint32_t c4 = __builtin_amdgcn_alignbyte(hi, lo, 1u);   // tagCopy4
   // literal: window position of its bytes / copy: offset
   const uint32_t x = lit ? pos + 1 : t == 1 ? c1 : t == 2 ? c2 : c4;
-  const bool valid = P <= tb + 4 * lim && len0 != 0;
+  const bool valid = P <= tb + 2 * lim && len0 != 0;
   const int64_t rem64 = slen - s, room64 = dl - dpos;
   const int32_t rem = rem64 < 0x40000000 ? (int32_t)rem64 : 0x40000000;  // stream bytes from s
   const int32_t room = room64 < 0x40000000 ? (int32_t)room64 : 0x40000000;
@@ -691,15 +695,17 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, uint32_t
       // a source or destination range that runs past the end of the ring
       const bool wrap = shortc && (ro + len > RING || (!lit && !fdefer && (sa - rb) + len > RING));
       if (!ballot(wrap)) {
+        // the source as aligned dwords, funnel-shifted (v_alignbyte) to the
+        // token's bytes; stored a byte at a time (ds_write_b8 / _d16_hi)
+        const uint32_t s4 = sa & ~3u;
 #pragma unroll
         for (int h = 0; h < SNAP_TOK_SHORT / 8; h++) {
           if (h > 0 && !ballot(mylen > 8u * h)) break;
-          uint32_t v[8];
-#pragma unroll
-          for (int i = 0; i < 8; i++) v[i] = lds_u8(sa + 8 * h + i);  // (bytes past the token: unused)
+          const uint32_t w0 = lds_u32(s4 + 8 * h), w1 = lds_u32(s4 + 8 * h + 4), w2 = lds_u32(s4 + 8 * h + 8);
+          const uint32_t r0 = __builtin_amdgcn_alignbyte(w1, w0, sa & 3u), r1 = __builtin_amdgcn_alignbyte(w2, w1, sa & 3u);
 #pragma unroll
           for (int i = 0; i < 8; i++)
-            if (8u * h + i < mylen) lds_st8(da + 8 * h + i, v[i]);
+            if (8u * h + i < mylen) lds_st8(da + 8 * h + i, (i < 4 ? r0 : r1) >> (8 * (i & 3)));
         }
       } else {
         for (uint32_t i = 0; i < SNAP_TOK_SHORT; i++) {

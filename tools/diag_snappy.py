@@ -48,8 +48,9 @@ ph = ph[:8 * npg].reshape(npg, 8).astype(np.float64)
 pg = pg[:4 * npg].reshape(npg, 4).astype(np.float64)  # per page: wave-cycles (all segments), longest wave, bytes out, in
 names = [c["name"] for c in r.Columns()]
 print("%s: %d pages; longest wave %.0f kcycles" % (cfg, npg, pg[:, 1].max() / 1e3))
-steps = (["window", "chain", "decode", "far", "tables", "bytes", "flush"] if os.environ.get("PQG_SNAPPY_V1") == "1"
-         else ["window", "chain", "decode", "table", "longlit", "bytes", "flush"])  # k_snappy_wg
+# k_snappy's batch steps (PQ_SNAP_STAMPS marks -1..6); k_snappy_wg's with PQG_SNAPPY_WG=1
+steps = (["window", "chain", "decode", "table", "longlit", "bytes", "flush"] if os.environ.get("PQG_SNAPPY_WG") == "1"
+         else ["tables", "chain", "check", "far", "short", "dep", "flush"])
 print("%-16s %6s %8s %8s %9s | %s | %s" % ("column", "pages", "batches", "MB out", "kcyc/pg", " ".join("%7s" % s for s in steps),
                                            "cyc/batch"))
 for ci in sorted(set((pc >> 8).tolist())):
