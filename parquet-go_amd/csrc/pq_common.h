@@ -51,6 +51,11 @@ __host__ __device__ inline uint32_t make_status(uint32_t stage, uint32_t code) {
 // (k_prepare) is set at once with this bit, so that a dictionary-index error
 // k_expand finds among the values before it (same stage, plain code) wins the
 // atomicMin; the host masks it off (STATUS_CODE)
+// Kernels that decode a tiled page's values after the run walk (k_expand_mix,
+// k_expand_wg) must therefore gate on the DICTIONARY page's status, never on
+// the data page's own: a data page already holding an E_LATE status still has
+// its values before the bad header decoded, so an earlier dictionary-index
+// error can win (tests/test_gpu_parity.py::test_dict_index_error_before_bad_header)
 constexpr uint32_t E_LATE = 0x4000u;
 constexpr uint32_t STATUS_CODE = 0x3fffu;
 constexpr uint32_t STATUS_OK = 0xFFFFFFFFu;

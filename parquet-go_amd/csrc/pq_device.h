@@ -52,6 +52,12 @@ __device__ __forceinline__ uint32_t dpp_z(uint32_t v) {
 }
 template <bool MAX>
 __device__ __forceinline__ uint32_t wave_incl_dpp(uint32_t v) {
+#ifdef PQ_SNAP_GUARD
+  // a lane outside EXEC would read as 0 and cut the prefix at it: the guard
+  // build reports any call from a partial wave (tests/test_gpu_guard.py)
+  if (__builtin_amdgcn_read_exec() != ~0ull && lane_id() == (int)__builtin_ctzll(__builtin_amdgcn_read_exec()))
+    printf("PQ_CHK scan: exec %llx\n", (unsigned long long)__builtin_amdgcn_read_exec());
+#endif
   // (0 is the identity of both + and unsigned max)
 #define PQ_STEP(C, R)                \
   do {                               \
@@ -72,6 +78,10 @@ __device__ __forceinline__ uint64_t dpp_z64(uint64_t v) {
   return ((uint64_t)dpp_z<CTRL, ROWS>((uint32_t)(v >> 32)) << 32) | dpp_z<CTRL, ROWS>((uint32_t)v);
 }
 __device__ __forceinline__ uint64_t wave_incl_add64_dpp(uint64_t v) {
+#ifdef PQ_SNAP_GUARD
+  if (__builtin_amdgcn_read_exec() != ~0ull && lane_id() == (int)__builtin_ctzll(__builtin_amdgcn_read_exec()))
+    printf("PQ_CHK scan64: exec %llx\n", (unsigned long long)__builtin_amdgcn_read_exec());
+#endif
   v += dpp_z64<0x111>(v);
   v += dpp_z64<0x112>(v);
   v += dpp_z64<0x114>(v);

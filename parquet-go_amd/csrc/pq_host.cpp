@@ -1304,9 +1304,13 @@ double pqg_file_row_group_cost(const pqg_file *f, int rg) {
     const ColumnChunkMeta &c = f->rgs[(size_t)rg].cols[li];
     ns += (double)std::max<int64_t>(c.total_uncompressed, 0) / 2000.0;  // bytes / (2 TB/s) in ns
     if (c.codec == PQG_CODEC_SNAPPY) ns += (double)std::max<int64_t>(c.total_compressed, 0) / 400.0;
-    if (!c.has_dict_off || c.dict_page_offset <= 0 || c.dict_page_offset >= c.data_page_offset) continue;
-    if ((uint64_t)c.dict_page_offset >= f->len) continue;
-    TReader t(f->data + c.dict_page_offset, f->len - (size_t)c.dict_page_offset);
+    // the dictionary page: at dictionary_page_offset when it is set before the
+    // data pages, else (writers that leave it unset) possibly the chunk's
+    // first page, at data_page_offset
+    const bool at_dict = c.has_dict_off && c.dict_page_offset > 0 && c.dict_page_offset < c.data_page_offset;
+    const int64_t off = at_dict ? c.dict_page_offset : c.data_page_offset;
+    if (off <= 0 || (uint64_t)off >= f->len) continue;
+    TReader t(f->data + off, f->len - (size_t)off);
     PageHeader h;
     read_page_header(t, h);
     if (t.err || h.type != 2 || !h.has_dict || h.dict_num_values <= 0) continue;

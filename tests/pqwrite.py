@@ -209,12 +209,15 @@ def write_column(pages, ptype=1, encoding=5, optional=False, type_length=0, dict
     return bytes(out)
 
 
-def write_row_groups(row_groups, ptype=1, encoding=8, optional=False):
+def write_row_groups(row_groups, ptype=1, encoding=8, optional=False, dict_offset_field=True):
     """One leaf `v` (parquet.Type `ptype`), several row groups, V1
     uncompressed pages: row_groups = [{"pages": [(num_values, def_levels or
     None, values_section_bytes)], "dict_page": bytes or None, "dict_count":
     n}].  Values sections are given as they are stored (for RLE_DICTIONARY:
-    the bit-width byte and the hybrid key stream).  Returns the file bytes."""
+    the bit-width byte and the hybrid key stream).  Without
+    `dict_offset_field` the chunk metadata leaves dictionary_page_offset unset
+    and data_page_offset points at the dictionary page (as some writers do).
+    Returns the file bytes."""
     elems = [_S().str(4, "schema").i32(5, 1), _S().i32(1, ptype).i32(3, 1 if optional else 0).str(4, "v")]
     out = bytearray(b"PAR1")
     rgs = []
@@ -240,6 +243,8 @@ def write_row_groups(row_groups, ptype=1, encoding=8, optional=False):
             out += _S().i32(1, 0).i32(2, len(b)).i32(3, len(b)).struct(5, dph).done() + b
             n_rg += n
         size = len(out) - first
+        if dict_off is not None and not dict_offset_field:
+            data_off, dict_off = dict_off, None
         meta = (_S().i32(1, ptype).list(2, T_I32, [0, 3, encoding]).list(3, T_BINARY, ["v"]).i32(4, 0).i64(5, n_rg)
                 .i64(6, size).i64(7, size).i64(9, data_off))
         if dict_off is not None:

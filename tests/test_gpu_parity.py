@@ -982,3 +982,52 @@ def test_crash_inputs_gpu(case):
         assert ei.value.code == res
         return
     check_file(data, case["test"])
+
+
+def test_dictionary_page_at_data_page_offset():
+    """A chunk whose metadata leaves dictionary_page_offset unset, with the
+    dictionary page first at data_page_offset (some writers do): decoded
+    from there, bit-exact against the oracle, RLE runs and bit-packed keys."""
+    import pqwrite
+    rng = np.random.default_rng(45)
+    for dn, bw in ((5, 3), (3000, 12), (20000, 15)):
+        keys = rng.integers(0, dn, 50000)
+        dvals = rng.integers(-2**31, 2**31, dn).astype("<i4").tobytes()
+        body = bytes([bw]) + pqwrite.hybrid_bitpacked(keys, bw)
+        rgs = [{"dict_page": dvals, "dict_count": dn, "pages": [(50000, None, body), (50000, None, body)]}]
+        check_file(pqwrite.write_row_groups(rgs, ptype=1, encoding=8, dict_offset_field=False),
+                   "dictionary at data_page_offset, %d entries" % dn)
+
+
+def test_dict_index_error_before_bad_header():
+    """The tiled path's error order in a batch without level streams (C2's
+    shape, no k_level_check): the run walk sets a corrupt run header's error
+    at once (with E_LATE), and a dictionary-index error k_expand finds among
+    the values before that header must still win, as in the reference
+    (keys read before a stream error are range-checked first,
+    type_dict.go:44-53).  The status is the oracle's in every layout."""
+    import pqwrite
+    dn, bw = 3, 2  # key 3 is out of range
+    good = [0, 1, 2, 1, 0, 2, 1, 0] * 8
+    bad = list(good)
+    bad[13] = 3
+    rle = lambda v, cnt: pqwrite._uvar(cnt << 1) + bytes([v])
+    cases = {
+        # a bad key, then a run header past the stream (bit-packed groups beyond it)
+        "bad key, then truncated run": pqwrite.hybrid_bitpacked(bad, bw) + pqwrite._uvar((40 << 1) | 1) + b"\x00",
+        # a bad key, then an empty RLE run
+        "bad key, then empty run": pqwrite.hybrid_bitpacked(bad, bw) + b"\x00",
+        # good keys, then the bad header alone
+        "truncated run alone": pqwrite.hybrid_bitpacked(good, bw) + pqwrite._uvar((40 << 1) | 1) + b"\x00",
+        # a bad RLE key after good runs, then the bad header
+        "bad RLE key, then empty run": pqwrite.hybrid_bitpacked(good, bw) + rle(3, 8) + b"\x00",
+    }
+    dvals = np.array([7, -9, 11], "<i4").tobytes()
+    for name, keys in cases.items():
+        n = 64 + 64
+        body = bytes([bw]) + keys
+        rgs = [{"dict_page": dvals, "dict_count": dn, "pages": [(n, None, body)]}]
+        data = pqwrite.write_row_groups(rgs, ptype=1, encoding=8)
+        with pytest.raises(oracle.OracleError):
+            oracle.File(data).decode(0)
+        check_file(data, name)

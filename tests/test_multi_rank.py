@@ -74,6 +74,31 @@ def test_cost_balanced_shards_c2_shape(tmp_path):
         assert by_cost[0][0] == 0 and by_cost[-1][1] == n
 
 
+def test_cost_prices_dictionary_at_data_page_offset():
+    """A writer that leaves dictionary_page_offset unset puts the dictionary
+    page at data_page_offset: RowGroupCost still finds it there and prices
+    the gathers by its bit width (the same cost as with the field set), and
+    both layouts decode alike on the oracle."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle
+    import pqgpu
+    import pqwrite
+    rng = np.random.default_rng(44)
+    dn, n = 20000, 200000  # bit width 15: L2 gathers
+    keys = rng.integers(0, dn, n)
+    dvals = rng.integers(-2**31, 2**31, dn).astype("<i4").tobytes()
+    rg = {"dict_page": dvals, "dict_count": dn, "pages": [(n, None, bytes([15]) + pqwrite.hybrid_bitpacked(keys, 15))]}
+    with_field = pqwrite.write_row_groups([rg], ptype=1, encoding=8)
+    without = pqwrite.write_row_groups([rg], ptype=1, encoding=8, dict_offset_field=False)
+    c1 = pqgpu.FileReader(with_field).RowGroupCost(0)
+    c2 = pqgpu.FileReader(without).RowGroupCost(0)
+    assert c1 > 0 and abs(c1 - c2) < 1e-6 * c1, (c1, c2)
+    assert c1 > len(with_field) / 2000.0 * 1.5  # the gathers, not only the bytes
+    a = oracle.File(with_field).decode(0)["values"].view(np.int32)
+    b = oracle.File(without).decode(0)["values"].view(np.int32)
+    assert np.array_equal(a, b) and np.array_equal(a, np.frombuffer(dvals, "<i4")[keys])
+
+
 def _rank_main(rank, world, port, path, out_dir):
     import torch
     import torch.distributed as dist
