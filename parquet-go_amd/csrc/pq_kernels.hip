@@ -376,6 +376,23 @@ struct SnapLds {  // per wave
   } while (0)
 #endif
 
+// diagnostic build (-DPQ_DEC_STAMPS, tools/diag_decode.py): k_decode<2>'s
+// shader cycles per step phase, accumulated per wave, added to dbg2 per page
+#ifdef PQ_DEC_STAMPS
+#define DEC_T(i)                                               \
+  do {                                                         \
+    if (KIND == 2) {                                           \
+      const uint64_t t_ = __builtin_amdgcn_s_memtime();        \
+      if ((i) >= 0) dacc[(i) < 0 ? 0 : (i)] += t_ - dprev;     \
+      dprev = t_;                                              \
+    }                                                          \
+  } while (0)
+#else
+#define DEC_T(i) \
+  do {           \
+  } while (0)
+#endif
+
 #ifdef PQ_SNAP_GUARD
 #define PQ_CHK(c, id, u, v, onfail)                                                                   \
   do {                                                                                                \
@@ -4204,7 +4221,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
     return (uint64_t)pr | ((uint64_t)pd << 32);
   };
   uint64_t lv_next = PQ_LV_AHEAD ? lv_load(e0) : 0;
+#ifdef PQ_DEC_STAMPS
+  uint64_t dacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t dprev = __builtin_amdgcn_s_memtime();
+  const uint64_t dt0 = dprev;
+#endif
   while (e0 < e_end) {
+    DEC_T(-1);
     const int cnt = step_cnt(e0);
     uint32_t r[4] = {0, 0, 0, 0}, dl[4] = {0, 0, 0, 0};
     const uint64_t lv = PQ_LV_AHEAD ? lv_next : lv_load(e0);
@@ -4280,6 +4303,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
       row_run += mrows;
     }
 
+    DEC_T(0);  // levels, counts, scans
     // ---- the m dense values of this step, in dense order (value j: lane j>>2, element j&3) ----
     uint64_t v[4] = {0, 0, 0, 0};
     int64_t soff[4] = {0, 0, 0, 0}, slen[4] = {0, 0, 0, 0};
@@ -4341,6 +4365,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
         }
         uint32_t kk[4];
         err = keys.next4(m, kk);
+        DEC_T(1);  // the key stream
         if (err) {
           // decodeValues checks each key as it reads it (type_dict.go:44-53): an
           // out-of-range key among those read before the stream error comes first
@@ -4539,6 +4564,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
       }
     }
 
+    DEC_T(2);  // key checks, dictionary entries
     // ---- outputs ----
     if (is_ba) {
       int64_t ll[4], tot = 0;
@@ -4603,6 +4629,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
         }
       }
     }
+    DEC_T(3);  // string / value outputs
     if (c.max_def > 0) {
       if (flat) {
         // 4 bits per lane -> 32-bit words owned by lanes 8q (this step covers 256 aligned slots
@@ -4638,8 +4665,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
     }
     slot_run += mslots;
     nn_run += m;
+    DEC_T(4);  // validity bitmaps, counters
     e0 += cnt;
   }
+#ifdef PQ_DEC_STAMPS
+  if (KIND == 2 && a.dbg2 && lane < 8) {
+    const uint64_t mine = lane == 0 ? dacc[0] : lane == 1 ? dacc[1] : lane == 2 ? dacc[2] : lane == 3 ? dacc[3]
+                                                                      : lane == 4 ? dacc[4] : 0ull;
+    atomicAdd((unsigned long long *)&a.dbg2[(size_t)page * 8 + lane], (unsigned long long)mine);
+  }
+  if (KIND == 2 && a.dbg2 && lane == 0) atomicAdd((unsigned long long *)&a.dbg2[(size_t)page * 8 + 7], 1ull);
+  if (KIND == 2 && a.dbg && lane == 0) {
+    atomicAdd((unsigned long long *)&a.dbg[(size_t)page * 4 + 0], (unsigned long long)(__builtin_amdgcn_s_memtime() - dt0));
+    atomicMax((unsigned long long *)&a.dbg[(size_t)page * 4 + 1], (unsigned long long)(__builtin_amdgcn_s_memtime() - dt0));
+    a.dbg[(size_t)page * 4 + 2] = (uint64_t)n;
+    a.dbg[(size_t)page * 4 + 3] = (uint64_t)e0;
+  }
+#endif
   // a later-found level error can outrank this one: k_level_check re-walks
   // the earlier level streams (the reference decodes all rep levels, then all
   // def levels, then the values, page_v1.go:37-52)
