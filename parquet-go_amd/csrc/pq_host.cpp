@@ -764,9 +764,10 @@ struct pqg_batch {
   uint32_t *d_seg_flag = nullptr;
   std::vector<int32_t> general_list;  // data pages for k_decode (wave per page): k_decode<0> pages, then
   std::vector<int32_t> general_flat;  // k_decode<1> pages (appended to general_list after planning)
+  std::vector<int32_t> general_str4;  // k_decode<4> pages (flat required RLE_DICTIONARY BYTE_ARRAY), first of the strings
   std::vector<int32_t> general_str;   // k_decode<2> pages (flat BYTE_ARRAY), appended after those
   std::vector<int32_t> general_nest;  // k_decode<3> pages (lists of fixed-width values), appended last
-  int32_t ngen_flat = 0, ngen_str = 0, ngen_nest = 0;
+  int32_t ngen_flat = 0, ngen_str = 0, ngen_str4 = 0, ngen_nest = 0;  // (ngen_str counts <4>'s pages too)
   std::vector<int32_t> dba_list;      // DELTA_BYTE_ARRAY pages: value bytes by k_dba
   std::vector<int32_t> nest_parts;    // k_decode<3> waves: (page, first level, end level) triplets
   std::vector<int32_t> pstr_items;    // k_plain_str: (page, first value) pairs of flat required PLAIN strings
@@ -2028,7 +2029,12 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
         }
         continue;
       }
+      // flat required dictionary strings: k_decode<4> (the dictionary path of
+      // <2> alone, 8 waves a SIMD instead of 3; PQG_NO_DEC4=1, analysis: <2>)
+      static const bool dec4_off = knob_flag("PQG_NO_DEC4");
+      const bool str4 = flat_ba && L.max_def == 0 && d.enc == ENC_RLE_DICT && !dec4_off;
       (flat_fw   ? B->general_flat
+       : str4    ? B->general_str4
        : flat_ba ? B->general_str
        : nest_fw ? B->general_nest
                  : B->general_list)
@@ -2446,8 +2452,11 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   B->ngen_flat = (int32_t)B->general_flat.size();
   B->general_list.insert(B->general_list.end(), B->general_flat.begin(), B->general_flat.end());
   B->general_flat.clear();
-  B->ngen_str = (int32_t)B->general_str.size();
+  B->ngen_str4 = (int32_t)B->general_str4.size();
+  B->ngen_str = (int32_t)(B->general_str4.size() + B->general_str.size());
+  B->general_list.insert(B->general_list.end(), B->general_str4.begin(), B->general_str4.end());
   B->general_list.insert(B->general_list.end(), B->general_str.begin(), B->general_str.end());
+  B->general_str4.clear();
   B->general_str.clear();
   B->ngen_nest = (int32_t)B->general_nest.size();
   {
@@ -3075,8 +3084,11 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
         e |= pq_launch(23, &a, LN.side[1]);
       }
       a.list = B->d_lists + ns + nd + ndata + ng0 + B->ngen_flat;
-      a.nlist = B->ngen_str;
-      e |= pq_launch(15, &a, LN.side[1]);  // k_decode<2>: flat BYTE_ARRAY pages
+      a.nlist = B->ngen_str4;
+      e |= pq_launch(31, &a, LN.side[1]);  // k_decode<4>: flat required dictionary strings
+      a.list += B->ngen_str4;
+      a.nlist = B->ngen_str - B->ngen_str4;
+      e |= pq_launch(15, &a, LN.side[1]);  // k_decode<2>: the other flat BYTE_ARRAY pages
       hipEventRecord(LN.join[1], LN.side[1]);
     }
     if (B->ngen_nest > 0) {

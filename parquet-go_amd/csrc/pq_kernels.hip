@@ -376,6 +376,10 @@ struct SnapLds {  // per wave
   } while (0)
 #endif
 
+#ifndef PQ_K4_WPE
+#define PQ_K4_WPE 8  // k_decode<4> (flat required dictionary strings): waves per SIMD
+#endif
+
 // diagnostic build (-DPQ_DEC_STAMPS, tools/diag_decode.py): k_decode<2>'s
 // shader cycles per step phase, accumulated per wave, added to dbg2 per page
 #ifdef PQ_DEC_STAMPS
@@ -3886,6 +3890,24 @@ __device__ __forceinline__ void copy_str(const uint8_t *sp, uint8_t *op, int64_t
   }
 }
 
+// L bytes LDS -> LDS (byte addresses; the ranges of different lanes are
+// disjoint): head bytes up to a dword-aligned destination, whole dwords from
+// two aligned source dwords each (v_alignbyte), the tail a byte at a time.
+__device__ __forceinline__ void lds_copy_bytes(uint32_t src, uint32_t dst, int L) {
+  const int h = min((int)((4u - (dst & 3u)) & 3u), L);
+#pragma unroll
+  for (int b = 0; b < 3; b++)
+    if (b < h) lds_st8(dst + b, lds_u8(src + b));
+  int pos = h;
+  for (; pos + 4 <= L; pos += 4) {
+    const uint32_t q = (src + pos) & ~3u;
+    lds_st32(dst + pos, __builtin_amdgcn_alignbyte(lds_u32(q + 4), lds_u32(q), (src + pos) & 3u));
+  }
+#pragma unroll
+  for (int b = 0; b < 3; b++)
+    if (pos + b < L) lds_st8(dst + pos + b, lds_u8(src + pos + b));
+}
+
 // ===========================================================================
 // k_plain_str: flat required PLAIN BYTE_ARRAY pages (type_bytearray.go:13-55)
 // in items of PS_ITEM values, several waves per page.  k_prepare's length walk
@@ -4036,7 +4058,7 @@ __global__ __launch_bounds__(256) void k_plain_str(KArgs a) {
 // aligned to 256 output slots so each lane owns a 16-byte-aligned slice of
 // the values and whole validity words.
 template <int KIND>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ? 5 : KIND == 2 ? 3 : KIND == 3 ? 2 : 1))) void k_decode(KArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ? 5 : KIND == 2 ? 3 : KIND == 3 ? 2 : KIND == 4 ? PQ_K4_WPE : 1))) void k_decode(KArgs a) {
   const int gi = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
   if (gi >= a.nlist) return;
   const int lane = lane_id();
@@ -4075,10 +4097,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   const int w = c.width;
   // KIND (the host routes pages by column class, none with level output but
   // KIND 0): 1 flat fixed-width (4/8-byte, non-BOOLEAN), 2 flat BYTE_ARRAY,
-  // 3 nested (lists) of fixed-width values, 0 everything else.  The other
+  // 3 nested (lists) of fixed-width values, 4 flat REQUIRED RLE_DICTIONARY
+  // BYTE_ARRAY (<2>'s dictionary path alone: a fraction of its registers, so
+  // more of these one-wave pages in flight), 0 everything else.  The other
   // paths drop out of each instance and its register budget.
-  const bool flat = KIND == 1 || KIND == 2 || (KIND == 0 && c.max_rep == 0);
-  const bool is_ba = KIND == 2 || (KIND == 0 && c.ptype == T_BYTE_ARRAY);
+  const bool flat = KIND == 1 || KIND == 2 || KIND == 4 || (KIND == 0 && c.max_rep == 0);
+  const bool is_ba = KIND == 2 || KIND == 4 || (KIND == 0 && c.ptype == T_BYTE_ARRAY);
   const bool is_bool = KIND == 0 && c.ptype == T_BOOLEAN;
   const bool emit_lv = KIND == 0 && (c.flags & COL_EMIT_LEVELS);
 
@@ -4099,7 +4123,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
       dict_n = dp->num_values;
       dict_base = dp->dict_base;
     }
-  } else if (KIND != 2 && d.enc == ENC_DELTA_BP) {
+  } else if (KIND != 2 && KIND != 4 && d.enc == ENC_DELTA_BP) {
     dz.init(vals, vlen, c.ptype == T_INT32);
     delta_prev = (uint64_t)dz.first;
   } else if (d.enc == ENC_RLE && is_bool) {
@@ -4117,17 +4141,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   // gathers read it there instead of from L2 (one dependent global round trip
   // less a step; C4's 2,001-entry INT32 dictionaries)
   // (KIND 2, dictionary strings: the entries' (offset, length) pairs)
-  constexpr int DLW = (KIND == 3 || KIND == 2) && PQ_DEC_DICT_LDS >= 8 ? PQ_DEC_DICT_LDS / 4 : 1;
+  constexpr int DLW = (KIND == 3 || KIND == 2 || KIND == 4) && PQ_DEC_DICT_LDS >= 8 ? PQ_DEC_DICT_LDS / 4 : 1;
   __shared__ uint32_t dlds_all[4][DLW];
   uint32_t *dlds = dlds_all[threadIdx.x >> 6];
-  const int64_t dlb = KIND == 2 ? dict_n * 8 : dict_n * (int64_t)w;  // bytes staged
-  const bool dict_lds = (KIND == 3 || KIND == 2) && DLW > 1 && dp && d.enc == ENC_RLE_DICT &&
-                        (KIND == 2 || w == 4 || w == 8) && dlb <= (int64_t)DLW * 4;
+  const int64_t dlb = KIND == 2 || KIND == 4 ? dict_n * 8 : dict_n * (int64_t)w;  // bytes staged
+  const bool dict_lds = (KIND == 3 || KIND == 2 || KIND == 4) && DLW > 1 && dp && d.enc == ENC_RLE_DICT &&
+                        (KIND == 2 || KIND == 4 || w == 4 || w == 8) && dlb <= (int64_t)DLW * 4;
+  // (<4>: when the dictionary page's values fit beside the entry table they
+  // are staged too, and a step's string bytes are assembled in the rest of
+  // the area and stored as whole 16-byte chunks; see the outputs)
+  const int64_t sb_off = (dlb + 15) & ~(int64_t)15;  // staged values' byte offset in dlds
+  const int64_t dvb = KIND == 4 && dp ? (int64_t)dp->body_len : 0;
+  const int64_t stg_off = (sb_off + dvb + 32 + 15) & ~(int64_t)15;  // the step's output bytes
+  const bool str_lds = KIND == 4 && dict_lds && dvb > 0 && stg_off + 1024 <= (int64_t)DLW * 4;
+  const uint32_t str_lb = lds_addr(dlds) + (uint32_t)sb_off, stg_lb = lds_addr(dlds) + (uint32_t)stg_off;
+  const int64_t stg_cap = (int64_t)DLW * 4 - stg_off - 32;
   if (dict_lds) {
     const int nw = (int)((dlb + 3) >> 2);
-    if (KIND == 2) {
+    if (KIND == 2 || KIND == 4) {
       const uint32_t *ent = (const uint32_t *)(a.dict_ent + dict_base);
       for (int i = lane; i < nw; i += 64) dlds[i] = ent[i];
+      if (str_lds)
+        for (int i = lane; i < (int)((dvb + 3) >> 2) + 2; i += 64)
+          dlds[sb_off / 4 + i] = load_u32_unaligned(dict_vals + 4 * (int64_t)i);
     } else {
       for (int i = lane; i < nw; i += 64) dlds[i] = load_u32_unaligned(dict_vals + 4 * (int64_t)i);
     }
@@ -4139,7 +4175,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   // FIXED_LEN_BYTE_ARRAY DELTA_BYTE_ARRAY (KIND 0 only): slots zeroed here,
   // the values written by k_dba
   const bool fl_dba = KIND == 0 && c.ptype == T_FLBA && d.enc == ENC_DELTA_BA && d.lens_base >= 0;
-  const bool dstr = (is_ba && (d.enc == ENC_DELTA_LBA || d.enc == ENC_DELTA_BA) && d.lens_base >= 0) || fl_dba;
+  const bool dstr = (KIND != 4 && is_ba && (d.enc == ENC_DELTA_LBA || d.enc == ENC_DELTA_BA) && d.lens_base >= 0) || fl_dba;
   const bool defer_bytes = dstr && d.enc == ENC_DELTA_BA;
   int64_t dpos = pi.str_data;
 
@@ -4241,7 +4277,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
         r[k] = (uint32_t)(lv >> (8 * k)) & 0xffu;
         dl[k] = (uint32_t)(lv >> (32 + 8 * k)) & 0xffu;
       }
-    } else {
+    } else if (KIND != 4) {  // (<4>: required, no levels)
       if (!flat) {
         err = rep.next4(cnt, r);
         if (err) {
@@ -4414,7 +4450,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
             }
           }
         sbase_ptr = dict_vals;
-      } else if (KIND != 2 && d.enc == ENC_DELTA_BP) {
+      } else if (KIND != 2 && KIND != 4 && d.enc == ENC_DELTA_BP) {
         uint64_t dv[4];
         err = dz.template next4<KIND != 3>(m, dv);  // <3> is register-bound
         if (err) {
@@ -4485,7 +4521,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
           vi += valid[k];
         }
         sbase_ptr = vals;
-      } else if (d.enc == ENC_PLAIN && is_ba && d.lens_base >= 0) {
+      } else if (KIND != 4 && d.enc == ENC_PLAIN && is_ba && d.lens_base >= 0) {
         // offsets and lengths left by k_prepare's walk (which validated the
         // whole chain); dense value nn_run + j -> lane j>>2, element j&3
         const int32_t nvp = max(n, 0);
@@ -4520,7 +4556,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
           vi += valid[k];
         }
         sbase_ptr = vals;
-      } else if (d.enc == ENC_PLAIN && is_ba) {
+      } else if (KIND != 4 && d.enc == ENC_PLAIN && is_ba) {
         // length chain (type_bytearray.go:24-45) by pointer jumping, 64 entries a
         // batch; entry j of the step goes to lane j>>2, element j&3
         uint32_t eo[4] = {0, 0, 0, 0}, el[4] = {0, 0, 0, 0};
@@ -4576,16 +4612,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
       int64_t incl = wave_incl_scan64(tot);
       int64_t start = str_run + incl - tot;
       int si = 0;
+      const int64_t T = (int64_t)shfl64((uint64_t)incl, 63);  // the step's string bytes
+      if (KIND == 4 && str_lds && T <= stg_cap) {
+        // Small dictionary staged in LDS: each lane assembles its values'
+        // bytes in the LDS stage (LDS to LDS), then the step's output goes
+        // out as whole 16-byte chunks, a chunk a lane.  Storing each string
+        // a byte / dword at a time from its lane took ~10 scattered store
+        // requests a value, which bounded C5's dictionary-string pages.
+        const int64_t P0 = str_run;
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        if (slot[k]) {
-          start += ll[k];
-          c.str_offsets[slot_base + slot_run + sbase + si + 1] = start;
-          if (valid[k] && !defer_bytes) copy_str(sbase_ptr + soff[k], c.values + start - ll[k], ll[k]);
-          si++;
+        for (int k = 0; k < 4; k++) {
+          if (slot[k]) {
+            if (valid[k] && ll[k] > 0) lds_copy_bytes(str_lb + (uint32_t)soff[k], stg_lb + (uint32_t)(start - P0), (int)ll[k]);
+            start += ll[k];
+            c.str_offsets[slot_base + slot_run + sbase + si + 1] = start;
+            si++;
+          }
+        }
+        wave_lds_sync();
+        uint8_t *ov = c.values;
+        const int64_t P1 = P0 + T;
+        const int64_t q0 = (int64_t)(((uintptr_t)(ov + P0)) & ~(uintptr_t)15) - (int64_t)(uintptr_t)ov;
+        for (int64_t q = q0 + 16 * (int64_t)lane; q < P1; q += 1024) {
+          const int32_t pr0 = (int32_t)(q - P0);  // step-relative start of this chunk (> -16)
+          const uint32_t sa = stg_lb + (uint32_t)(pr0 + 16) - 16u;  // (the stage has 16 bytes before it)
+          const uint32_t s4 = sa & ~3u;
+          uint32_t w[5];
+#pragma unroll
+          for (int i = 0; i < 5; i++) w[i] = lds_u32(s4 + 4 * i);
+          uint32_t x[4];
+#pragma unroll
+          for (int i = 0; i < 4; i++) x[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sa & 3u);
+          if (pr0 >= 0 && pr0 + 16 <= (int32_t)T) {
+            *(uint4 *)(ov + q) = make_uint4(x[0], x[1], x[2], x[3]);
+          } else {  // an edge chunk: only the step's own bytes
+            for (int b = 0; b < 16; b++) {
+              const int32_t pb = pr0 + b;
+              if (pb >= 0 && pb < (int32_t)T) ov[q + b] = (uint8_t)(x[b >> 2] >> (8 * (b & 3)));
+            }
+          }
+        }
+        wave_lds_sync();
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          if (slot[k]) {
+            start += ll[k];
+            c.str_offsets[slot_base + slot_run + sbase + si + 1] = start;
+            if (valid[k] && !defer_bytes) copy_str(sbase_ptr + soff[k], c.values + start - ll[k], ll[k]);
+            si++;
+          }
         }
       }
-      str_run += (int64_t)shfl64((uint64_t)incl, 63);
+      str_run += T;
     } else if (flat && (w == 4 || w == 8)) {
       const int64_t s0 = slot_base + slot_run + 4 * lane;  // my four slots
       uint64_t o[4];
@@ -4630,7 +4709,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
       }
     }
     DEC_T(3);  // string / value outputs
-    if (c.max_def > 0) {
+    if (KIND != 4 && c.max_def > 0) {
       if (flat) {
         // 4 bits per lane -> 32-bit words owned by lanes 8q (this step covers 256 aligned slots
         // except a page's first/last step, which share words with neighbouring pages)
@@ -6225,6 +6304,7 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     case 3: hipLaunchKernelGGL(pq::k_decode<0>, grid, block, 0, s, k); break;
     case 14: hipLaunchKernelGGL(pq::k_decode<1>, grid, block, 0, s, k); break;
     case 15: hipLaunchKernelGGL(pq::k_decode<2>, grid, block, 0, s, k); break;
+    case 31: hipLaunchKernelGGL(pq::k_decode<4>, grid, block, 0, s, k); break;
     case 16: hipLaunchKernelGGL(pq::k_decode<3>, grid, block, 0, s, k); break;
     case 5: hipLaunchKernelGGL(pq::k_level_check, grid, block, 0, s, k); break;
     case 10: hipLaunchKernelGGL(pq::k_dba, grid, block, 0, s, k); break;
