@@ -3100,7 +3100,8 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
         pq_launch_args ap = a;
         ap.parts = B->d_parts;
         ap.nlist = nparts;
-        e |= pq_launch(16, &ap, LN.side[2]);  // k_decode<3>: parts of list pages of fixed-width values
+        static const bool k5_off = knob_flag("PQG_NO_DEC5");  // (analysis: the parts on <3>)
+        e |= pq_launch(k5_off ? 16 : 32, &ap, LN.side[2]);  // k_decode<5>: parts of list pages of fixed-width values
         ap = a;
         ap.redo = 1;
         e |= pq_launch(16, &ap, LN.side[2]);  // k_decode<3>: pages whose later parts failed, whole

@@ -376,6 +376,9 @@ struct SnapLds {  // per wave
   } while (0)
 #endif
 
+#ifndef PQ_K5_WPE
+#define PQ_K5_WPE 3  // k_decode<5> (parts of list pages: level scratch, PLAIN / dictionary values): waves per SIMD
+#endif
 #ifndef PQ_K4_WPE
 #define PQ_K4_WPE 8  // k_decode<4> (flat required dictionary strings): waves per SIMD
 #endif
@@ -4058,7 +4061,7 @@ __global__ __launch_bounds__(256) void k_plain_str(KArgs a) {
 // aligned to 256 output slots so each lane owns a 16-byte-aligned slice of
 // the values and whole validity words.
 template <int KIND>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ? 5 : KIND == 2 ? 3 : KIND == 3 ? 2 : KIND == 4 ? PQ_K4_WPE : 1))) void k_decode(KArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ? 5 : KIND == 2 ? 3 : KIND == 3 ? 2 : KIND == 4 ? PQ_K4_WPE : KIND == 5 ? PQ_K5_WPE : 1))) void k_decode(KArgs a) {
   const int gi = blockIdx.x * 4 + (int)ufirst(threadIdx.x >> 6);
   if (gi >= a.nlist) return;
   const int lane = lane_id();
@@ -4068,7 +4071,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   // k_levels' level bytes, the key stream is skipped to the part's first
   // value.  A part after the first that meets an error marks the page
   // ST_REDO, and the redo launch decodes it whole for the reference's status.
-  const bool part = KIND == 3 && a.parts != nullptr;
+  const bool part = (KIND == 3 && a.parts != nullptr) || KIND == 5;
   int page;
   int64_t e_lo = 0, e_hi = 0x7fffffffffffll;
   if (part) {
@@ -4097,7 +4100,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   const int w = c.width;
   // KIND (the host routes pages by column class, none with level output but
   // KIND 0): 1 flat fixed-width (4/8-byte, non-BOOLEAN), 2 flat BYTE_ARRAY,
-  // 3 nested (lists) of fixed-width values, 4 flat REQUIRED RLE_DICTIONARY
+  // 3 nested (lists) of fixed-width values (5: the parts of such pages, whose
+  // levels are always in k_levels' scratch and whose values are PLAIN or
+  // dictionary: no serial level walk, no DELTA), 4 flat REQUIRED RLE_DICTIONARY
   // BYTE_ARRAY (<2>'s dictionary path alone: a fraction of its registers, so
   // more of these one-wave pages in flight), 0 everything else.  The other
   // paths drop out of each instance and its register budget.
@@ -4123,7 +4128,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
       dict_n = dp->num_values;
       dict_base = dp->dict_base;
     }
-  } else if (KIND != 2 && KIND != 4 && d.enc == ENC_DELTA_BP) {
+  } else if (KIND != 2 && KIND != 4 && KIND != 5 && d.enc == ENC_DELTA_BP) {
     dz.init(vals, vlen, c.ptype == T_INT32);
     delta_prev = (uint64_t)dz.first;
   } else if (d.enc == ENC_RLE && is_bool) {
@@ -4141,11 +4146,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   // gathers read it there instead of from L2 (one dependent global round trip
   // less a step; C4's 2,001-entry INT32 dictionaries)
   // (KIND 2, dictionary strings: the entries' (offset, length) pairs)
-  constexpr int DLW = (KIND == 3 || KIND == 2 || KIND == 4) && PQ_DEC_DICT_LDS >= 8 ? PQ_DEC_DICT_LDS / 4 : 1;
+  constexpr int DLW = (KIND == 3 || KIND == 2 || KIND == 4 || KIND == 5) && PQ_DEC_DICT_LDS >= 8 ? PQ_DEC_DICT_LDS / 4 : 1;
   __shared__ uint32_t dlds_all[4][DLW];
   uint32_t *dlds = dlds_all[threadIdx.x >> 6];
   const int64_t dlb = KIND == 2 || KIND == 4 ? dict_n * 8 : dict_n * (int64_t)w;  // bytes staged
-  const bool dict_lds = (KIND == 3 || KIND == 2 || KIND == 4) && DLW > 1 && dp && d.enc == ENC_RLE_DICT &&
+  const bool dict_lds = (KIND == 3 || KIND == 2 || KIND == 4 || KIND == 5) && DLW > 1 && dp && d.enc == ENC_RLE_DICT &&
                         (KIND == 2 || KIND == 4 || w == 4 || w == 8) && dlb <= (int64_t)DLW * 4;
   // (<4>: when the dictionary page's values fit beside the entry table they
   // are staged too, and a step's string bytes are assembled in the rest of
@@ -4277,7 +4282,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
         r[k] = (uint32_t)(lv >> (8 * k)) & 0xffu;
         dl[k] = (uint32_t)(lv >> (32 + 8 * k)) & 0xffu;
       }
-    } else if (KIND != 4) {  // (<4>: required, no levels)
+    } else if (KIND != 4 && KIND != 5) {  // (<4>: required, no levels; <5>: level scratch always)
       if (!flat) {
         err = rep.next4(cnt, r);
         if (err) {
@@ -4450,7 +4455,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
             }
           }
         sbase_ptr = dict_vals;
-      } else if (KIND != 2 && KIND != 4 && d.enc == ENC_DELTA_BP) {
+      } else if (KIND != 2 && KIND != 4 && KIND != 5 && d.enc == ENC_DELTA_BP) {
         uint64_t dv[4];
         err = dz.template next4<KIND != 3>(m, dv);  // <3> is register-bound
         if (err) {
@@ -6305,6 +6310,7 @@ int pq_launch(int which, const pq_launch_args *p, hipStream_t s) {
     case 14: hipLaunchKernelGGL(pq::k_decode<1>, grid, block, 0, s, k); break;
     case 15: hipLaunchKernelGGL(pq::k_decode<2>, grid, block, 0, s, k); break;
     case 31: hipLaunchKernelGGL(pq::k_decode<4>, grid, block, 0, s, k); break;
+    case 32: hipLaunchKernelGGL(pq::k_decode<5>, grid, block, 0, s, k); break;
     case 16: hipLaunchKernelGGL(pq::k_decode<3>, grid, block, 0, s, k); break;
     case 5: hipLaunchKernelGGL(pq::k_level_check, grid, block, 0, s, k); break;
     case 10: hipLaunchKernelGGL(pq::k_dba, grid, block, 0, s, k); break;
