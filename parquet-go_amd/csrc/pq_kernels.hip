@@ -388,7 +388,7 @@ struct SnapLds {  // per wave
 #ifdef PQ_DEC_STAMPS
 #define DEC_T(i)                                               \
   do {                                                         \
-    if (KIND == 2) {                                           \
+    if (KIND == 2 || KIND == 4 || KIND == 5) {                 \
       const uint64_t t_ = __builtin_amdgcn_s_memtime();        \
       if ((i) >= 0) dacc[(i) < 0 ? 0 : (i)] += t_ - dprev;     \
       dprev = t_;                                              \
@@ -4753,13 +4753,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
     e0 += cnt;
   }
 #ifdef PQ_DEC_STAMPS
-  if (KIND == 2 && a.dbg2 && lane < 8) {
+  if ((KIND == 2 || KIND == 4 || KIND == 5) && a.dbg2 && lane < 8) {
     const uint64_t mine = lane == 0 ? dacc[0] : lane == 1 ? dacc[1] : lane == 2 ? dacc[2] : lane == 3 ? dacc[3]
                                                                       : lane == 4 ? dacc[4] : 0ull;
     atomicAdd((unsigned long long *)&a.dbg2[(size_t)page * 8 + lane], (unsigned long long)mine);
   }
-  if (KIND == 2 && a.dbg2 && lane == 0) atomicAdd((unsigned long long *)&a.dbg2[(size_t)page * 8 + 7], 1ull);
-  if (KIND == 2 && a.dbg && lane == 0) {
+  if ((KIND == 2 || KIND == 4 || KIND == 5) && a.dbg2 && lane == 0) atomicAdd((unsigned long long *)&a.dbg2[(size_t)page * 8 + 7], 1ull);
+  if ((KIND == 2 || KIND == 4 || KIND == 5) && a.dbg && lane == 0) {
     atomicAdd((unsigned long long *)&a.dbg[(size_t)page * 4 + 0], (unsigned long long)(__builtin_amdgcn_s_memtime() - dt0));
     atomicMax((unsigned long long *)&a.dbg[(size_t)page * 4 + 1], (unsigned long long)(__builtin_amdgcn_s_memtime() - dt0));
     a.dbg[(size_t)page * 4 + 2] = (uint64_t)n;
