@@ -388,7 +388,7 @@ struct SnapLds {  // per wave
 #ifdef PQ_DEC_STAMPS
 #define DEC_T(i)                                               \
   do {                                                         \
-    if (KIND == 2 || KIND == 4 || KIND == 5) {                 \
+    if (KIND == 1 || KIND == 2 || KIND == 4 || KIND == 5) {                 \
       const uint64_t t_ = __builtin_amdgcn_s_memtime();        \
       if ((i) >= 0) dacc[(i) < 0 ? 0 : (i)] += t_ - dprev;     \
       dprev = t_;                                              \
@@ -720,17 +720,29 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, uint32_t
       const bool wrap = shortc && (ro + len > RING || (!lit && !fdefer && (sa - rb) + len > RING));
       if (!ballot(wrap)) {
         // the source as aligned dwords, funnel-shifted (v_alignbyte) to the
-        // token's bytes; stored a byte at a time (ds_write_b8 / _d16_hi)
-        const uint32_t s4 = sa & ~3u;
+        // token's bytes and again to the destination's 2-byte alignment; a
+        // head byte to an even address, then byte pairs (ds_write_b16 /
+        // _d16_hi), then a tail byte: at most 10 store steps a token
+        // instead of 16 byte stores
+        const uint32_t s4 = sa & ~3u, hb = da & 1u;
+        uint32_t w[6];
 #pragma unroll
-        for (int h = 0; h < SNAP_TOK_SHORT / 8; h++) {
-          if (h > 0 && !ballot(mylen > 8u * h)) break;
-          const uint32_t w0 = lds_u32(s4 + 8 * h), w1 = lds_u32(s4 + 8 * h + 4), w2 = lds_u32(s4 + 8 * h + 8);
-          const uint32_t r0 = __builtin_amdgcn_alignbyte(w1, w0, sa & 3u), r1 = __builtin_amdgcn_alignbyte(w2, w1, sa & 3u);
+        for (int i = 0; i < 6; i++) w[i] = lds_u32(s4 + 4 * i);  // (bytes past the token: unused)
+        const uint32_t tail = lds_u8(sa + (mylen ? mylen - 1 : 0));
+        uint32_t r[5], v[4];
 #pragma unroll
-          for (int i = 0; i < 8; i++)
-            if (8u * h + i < mylen) lds_st8(da + 8 * h + i, (i < 4 ? r0 : r1) >> (8 * (i & 3)));
+        for (int i = 0; i < 5; i++) r[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sa & 3u);  // token bytes 4 i ..
+#pragma unroll
+        for (int i = 0; i < 4; i++) v[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], hb);  // token bytes hb + 4 i ..
+        if (hb && mylen) lds_st8(da, r[0]);
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          if (h > 0 && !ballot(mylen > hb + 8u)) break;
+#pragma unroll
+          for (int p = 4 * h; p < 4 * h + 4; p++)
+            if (hb + 2u * p + 2u <= mylen) lds_st16(da + hb + 2 * p, (p & 1) ? v[p >> 1] >> 16 : v[p >> 1]);
         }
+        if (mylen > hb && ((mylen - hb) & 1u)) lds_st8(da + mylen - 1, tail);
       } else {
         for (uint32_t i = 0; i < SNAP_TOK_SHORT; i++) {
           if (!ballot(i < mylen)) break;
@@ -4146,11 +4158,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   // gathers read it there instead of from L2 (one dependent global round trip
   // less a step; C4's 2,001-entry INT32 dictionaries)
   // (KIND 2, dictionary strings: the entries' (offset, length) pairs)
-  constexpr int DLW = (KIND == 3 || KIND == 2 || KIND == 4 || KIND == 5) && PQ_DEC_DICT_LDS >= 8 ? PQ_DEC_DICT_LDS / 4 : 1;
+  constexpr int DLW = (KIND == 3 || KIND == 1 || KIND == 2 || KIND == 4 || KIND == 5) && PQ_DEC_DICT_LDS >= 8 ? PQ_DEC_DICT_LDS / 4 : 1;
   __shared__ uint32_t dlds_all[4][DLW];
   uint32_t *dlds = dlds_all[threadIdx.x >> 6];
   const int64_t dlb = KIND == 2 || KIND == 4 ? dict_n * 8 : dict_n * (int64_t)w;  // bytes staged
-  const bool dict_lds = (KIND == 3 || KIND == 2 || KIND == 4 || KIND == 5) && DLW > 1 && dp && d.enc == ENC_RLE_DICT &&
+  const bool dict_lds = (KIND == 3 || KIND == 1 || KIND == 2 || KIND == 4 || KIND == 5) && DLW > 1 && dp && d.enc == ENC_RLE_DICT &&
                         (KIND == 2 || KIND == 4 || w == 4 || w == 8) && dlb <= (int64_t)DLW * 4;
   // (<4>: when the dictionary page's values fit beside the entry table they
   // are staged too, and a step's string bytes are assembled in the rest of
@@ -4753,13 +4765,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
     e0 += cnt;
   }
 #ifdef PQ_DEC_STAMPS
-  if ((KIND == 2 || KIND == 4 || KIND == 5) && a.dbg2 && lane < 8) {
+  if ((KIND == 1 || KIND == 2 || KIND == 4 || KIND == 5) && a.dbg2 && lane < 8) {
     const uint64_t mine = lane == 0 ? dacc[0] : lane == 1 ? dacc[1] : lane == 2 ? dacc[2] : lane == 3 ? dacc[3]
                                                                       : lane == 4 ? dacc[4] : 0ull;
     atomicAdd((unsigned long long *)&a.dbg2[(size_t)page * 8 + lane], (unsigned long long)mine);
   }
-  if ((KIND == 2 || KIND == 4 || KIND == 5) && a.dbg2 && lane == 0) atomicAdd((unsigned long long *)&a.dbg2[(size_t)page * 8 + 7], 1ull);
-  if ((KIND == 2 || KIND == 4 || KIND == 5) && a.dbg && lane == 0) {
+  if ((KIND == 1 || KIND == 2 || KIND == 4 || KIND == 5) && a.dbg2 && lane == 0) atomicAdd((unsigned long long *)&a.dbg2[(size_t)page * 8 + 7], 1ull);
+  if ((KIND == 1 || KIND == 2 || KIND == 4 || KIND == 5) && a.dbg && lane == 0) {
     atomicAdd((unsigned long long *)&a.dbg[(size_t)page * 4 + 0], (unsigned long long)(__builtin_amdgcn_s_memtime() - dt0));
     atomicMax((unsigned long long *)&a.dbg[(size_t)page * 4 + 1], (unsigned long long)(__builtin_amdgcn_s_memtime() - dt0));
     a.dbg[(size_t)page * 4 + 2] = (uint64_t)n;

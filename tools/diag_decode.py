@@ -48,7 +48,7 @@ pg = pg[:4 * npg].reshape(npg, 4).astype(np.float64)
 names = [c["name"] for c in r.Columns()]
 steps = ["levels", "keys", "dict", "outputs", "bitmaps"]
 m_all = ph[:, 7] > 0
-print("%s: %d k_decode<2>/<4>/<5> pages; longest wave %.0f kcycles" % (cfg, m_all.sum(), pg[:, 1].max() / 1e3))
+print("%s: %d k_decode<1>/<2>/<4>/<5> pages; longest wave %.0f kcycles" % (cfg, m_all.sum(), pg[:, 1].max() / 1e3))
 print("%-16s %6s %9s %9s | %s | %s" % ("column", "pages", "values", "kcyc/pg", " ".join("%8s" % s for s in steps), "cyc/256"))
 for ci in sorted(set((pc >> 8).tolist())):
     m = ((pc >> 8) == ci) & m_all
