@@ -473,7 +473,7 @@ def timed_batch_parity(batch, reader, rg0, rg1, threads):
     and compared bit-exactly with the oracle's decode of the same row-group
     range (oracle/pqref.c; type_dict.go:39-59, chunk_reader.go:380-402).  The
     per-row-group batches of parity_check take other kernel routes (a lone
-    row group's big dictionary runs k_expand_big, the XCD dealing differs),
+    row group's big dictionary may run k_expand_wg, the XCD dealing differs),
     so this is the check that pins the headline's own bytes.  Oracle decodes
     run on `threads` host threads, a few leaves ahead of the GPU copies.
     Returns (ok, text)."""

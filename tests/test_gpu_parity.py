@@ -279,9 +279,10 @@ def test_generated_dictionary_widths(bw):
 
 @pytest.mark.parametrize("bw", [13, 14, 15])
 def test_tiled_big_dictionary_groups(bw):
-    """k_expand_big: dictionaries of 2^13..2^15 entries copied once per
-    8-wave workgroup into LDS (PQG_BIG=1), INT32 and INT64 columns side by
-    side, against the oracle; and with the L1/L2 path (PQG_NO_BIG=1)."""
+    """Wide dictionaries (2^13..2^15 entries): k_expand_wg, a CU's workgroup
+    holding the dictionary in LDS (PQG_BIG=1), INT32 and INT64 columns side
+    by side, against the oracle; and the mixed launch's L1/L2 path
+    (PQG_NO_BIG=1)."""
     rng = np.random.default_rng(200 + bw)
     K = 1 << bw
     rows = 600000
