@@ -192,6 +192,9 @@ __device__ __forceinline__ const uint8_t *body_ptr(const KArgs &a, const PageDes
 #ifndef SNAP_DEP_MAX
 #define SNAP_DEP_MAX 64  // copies overlapping their own batch written one after another (more: per-byte chase)
 #endif
+#ifndef PQ_SNAP_B16
+#define PQ_SNAP_B16 1  // k_snappy: short tokens stored as byte pairs (0: a byte at a time)
+#endif
 #ifndef SNAP_TOK_SHORT
 #define SNAP_TOK_SHORT 16  // token-parallel output: longer literals / near copies take the whole wave each
 #endif
@@ -719,6 +722,7 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, uint32_t
       // a source or destination range that runs past the end of the ring
       const bool wrap = shortc && (ro + len > RING || (!lit && !fdefer && (sa - rb) + len > RING));
       if (!ballot(wrap)) {
+#if PQ_SNAP_B16
         // the source as aligned dwords, funnel-shifted (v_alignbyte) to the
         // token's bytes and again to the destination's 2-byte alignment; a
         // head byte to an even address, then byte pairs (ds_write_b16 /
@@ -743,6 +747,19 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, uint32_t
             if (hb + 2u * p + 2u <= mylen) lds_st16(da + hb + 2 * p, (p & 1) ? v[p >> 1] >> 16 : v[p >> 1]);
         }
         if (mylen > hb && ((mylen - hb) & 1u)) lds_st8(da + mylen - 1, tail);
+#else
+        // (analysis build PQ_SNAP_B16=0: the byte stores this replaced)
+        const uint32_t s4 = sa & ~3u;
+#pragma unroll
+        for (int h = 0; h < SNAP_TOK_SHORT / 8; h++) {
+          if (h > 0 && !ballot(mylen > 8u * h)) break;
+          const uint32_t w0 = lds_u32(s4 + 8 * h), w1 = lds_u32(s4 + 8 * h + 4), w2 = lds_u32(s4 + 8 * h + 8);
+          const uint32_t r0 = __builtin_amdgcn_alignbyte(w1, w0, sa & 3u), r1 = __builtin_amdgcn_alignbyte(w2, w1, sa & 3u);
+#pragma unroll
+          for (int i = 0; i < 8; i++)
+            if (8u * h + i < mylen) lds_st8(da + 8 * h + i, (i < 4 ? r0 : r1) >> (8 * (i & 3)));
+        }
+#endif
       } else {
         for (uint32_t i = 0; i < SNAP_TOK_SHORT; i++) {
           if (!ballot(i < mylen)) break;
@@ -4158,11 +4175,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   // gathers read it there instead of from L2 (one dependent global round trip
   // less a step; C4's 2,001-entry INT32 dictionaries)
   // (KIND 2, dictionary strings: the entries' (offset, length) pairs)
-  constexpr int DLW = (KIND == 3 || KIND == 1 || KIND == 2 || KIND == 4 || KIND == 5) && PQ_DEC_DICT_LDS >= 8 ? PQ_DEC_DICT_LDS / 4 : 1;
+  constexpr int DLW = (KIND == 3 || KIND == 2 || KIND == 4 || KIND == 5) && PQ_DEC_DICT_LDS >= 8 ? PQ_DEC_DICT_LDS / 4 : 1;
   __shared__ uint32_t dlds_all[4][DLW];
   uint32_t *dlds = dlds_all[threadIdx.x >> 6];
   const int64_t dlb = KIND == 2 || KIND == 4 ? dict_n * 8 : dict_n * (int64_t)w;  // bytes staged
-  const bool dict_lds = (KIND == 3 || KIND == 1 || KIND == 2 || KIND == 4 || KIND == 5) && DLW > 1 && dp && d.enc == ENC_RLE_DICT &&
+  const bool dict_lds = (KIND == 3 || KIND == 2 || KIND == 4 || KIND == 5) && DLW > 1 && dp && d.enc == ENC_RLE_DICT &&
                         (KIND == 2 || KIND == 4 || w == 4 || w == 8) && dlb <= (int64_t)DLW * 4;
   // (<4>: when the dictionary page's values fit beside the entry table they
   // are staged too, and a step's string bytes are assembled in the rest of
