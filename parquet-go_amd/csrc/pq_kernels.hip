@@ -3940,6 +3940,57 @@ __device__ __forceinline__ void lds_copy_bytes(uint32_t src, uint32_t dst, int L
     if (pos + b < L) lds_st8(dst + pos + b, lds_u8(src + pos + b));
 }
 
+// A lane's four strings (device memory) -> an LDS stage (byte addresses
+// dst[k]; disjoint ranges): the short ones (<= 16 bytes) from six aligned
+// dwords each (global loads cannot alias the LDS stores, so the compiler
+// may hoist them); longer ones a dword at a time.  Head bytes to an aligned LDS dword, whole dwords, tail bytes.
+#define PQ_GLB1 __attribute__((address_space(1)))
+__device__ __forceinline__ void copy_str4_to_lds(const uint8_t *const (&sp)[4], const uint32_t (&dst)[4],
+                                                 const int (&ln)[4]) {
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int L = ln[k];
+    if (L <= 0) continue;
+    const uint32_t d = dst[k];
+    const int h = min((int)((4u - (d & 3u)) & 3u), L);
+    if (L <= 16) {
+      const PQ_GLB1 uint32_t *q = (const PQ_GLB1 uint32_t *)((uintptr_t)sp[k] & ~(uintptr_t)3);
+      uint32_t w[6];
+#pragma unroll
+      for (int i = 0; i < 6; i++) w[i] = q[i];
+      const uint32_t sk = (uint32_t)((uintptr_t)sp[k] & 3);
+      uint32_t r[5];
+#pragma unroll
+      for (int i = 0; i < 5; i++) r[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sk);  // string bytes 4 i ..
+#pragma unroll
+      for (int b = 0; b < 3; b++)
+        if (b < h) lds_st8(d + b, r[0] >> (8 * b));
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        const int pos = h + 4 * t;
+        const uint32_t u = __builtin_amdgcn_alignbyte(r[t + 1], r[t], (uint32_t)h);
+        if (pos + 4 <= L) {
+          lds_st32(d + pos, u);
+        } else if (pos < L) {
+#pragma unroll
+          for (int b = 0; b < 3; b++)
+            if (pos + b < L) lds_st8(d + pos + b, u >> (8 * b));
+        }
+      }
+    } else {
+      const PQ_GLB1 uint8_t *sb = (const PQ_GLB1 uint8_t *)(uintptr_t)sp[k];
+      for (int b = 0; b < h; b++) lds_st8(d + b, sb[b]);
+      int pos = h;
+      for (; pos + 4 <= L; pos += 4) {
+        const uintptr_t a = (uintptr_t)(sp[k] + pos);
+        const PQ_GLB1 uint32_t *q = (const PQ_GLB1 uint32_t *)(a & ~(uintptr_t)3);
+        lds_st32(d + pos, __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3)));
+      }
+      for (; pos < L; pos++) lds_st8(d + pos, sb[pos]);
+    }
+  }
+}
+
 // ===========================================================================
 // k_plain_str: flat required PLAIN BYTE_ARRAY pages (type_bytearray.go:13-55)
 // in items of PS_ITEM values, several waves per page.  k_prepare's length walk
@@ -4647,7 +4698,55 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
       int64_t start = str_run + incl - tot;
       int si = 0;
       const int64_t T = (int64_t)shfl64((uint64_t)incl, 63);  // the step's string bytes
-      if (KIND == 4 && str_lds && T <= stg_cap) {
+      constexpr int64_t BA_STG = (int64_t)sizeof(BaLds) - 32;  // <2>'s stage: the PLAIN walk's LDS, free on this path
+      if (KIND == 2 && d.enc == ENC_RLE_DICT && !defer_bytes && T <= BA_STG) {
+        // Dictionary strings (any dictionary size, nulls allowed): each lane
+        // copies its values' bytes from the dictionary into an LDS stage,
+        // then the step's output is stored as whole 16-byte chunks (C4's
+        // 1,000-word dictionary column: its per-string byte / dword stores
+        // were 54 % of a step, tools/diag_decode.py)
+        const int64_t P0 = str_run;
+        const uint32_t stg = lds_addr(&bl);
+        const uint8_t *cs[4];
+        uint32_t cd[4];
+        int cl[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          cs[k] = sbase_ptr + (valid[k] ? soff[k] : 0);
+          cd[k] = stg + (uint32_t)(start - P0);
+          cl[k] = slot[k] && valid[k] ? (int)ll[k] : 0;
+          if (slot[k]) {
+            start += ll[k];
+            c.str_offsets[slot_base + slot_run + sbase + si + 1] = start;
+            si++;
+          }
+        }
+        copy_str4_to_lds(cs, cd, cl);
+        wave_lds_sync();
+        uint8_t *ov = c.values;
+        const int64_t P1 = P0 + T;
+        const int64_t q0 = (int64_t)(((uintptr_t)(ov + P0)) & ~(uintptr_t)15) - (int64_t)(uintptr_t)ov;
+        for (int64_t q = q0 + 16 * (int64_t)lane; q < P1; q += 1024) {
+          const int32_t pr0 = (int32_t)(q - P0);
+          const uint32_t sa = stg + (uint32_t)(pr0 + 16) - 16u;
+          const uint32_t s4 = sa & ~3u;
+          uint32_t w[5];
+#pragma unroll
+          for (int i = 0; i < 5; i++) w[i] = lds_u32(s4 + 4 * i);
+          uint32_t x[4];
+#pragma unroll
+          for (int i = 0; i < 4; i++) x[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sa & 3u);
+          if (pr0 >= 0 && pr0 + 16 <= (int32_t)T) {
+            *(uint4 *)(ov + q) = make_uint4(x[0], x[1], x[2], x[3]);
+          } else {
+            for (int b = 0; b < 16; b++) {
+              const int32_t pb = pr0 + b;
+              if (pb >= 0 && pb < (int32_t)T) ov[q + b] = (uint8_t)(x[b >> 2] >> (8 * (b & 3)));
+            }
+          }
+        }
+        wave_lds_sync();
+      } else if (KIND == 4 && str_lds && T <= stg_cap) {
         // Small dictionary staged in LDS: each lane assembles its values'
         // bytes in the LDS stage (LDS to LDS), then the step's output goes
         // out as whole 16-byte chunks, a chunk a lane.  Storing each string
