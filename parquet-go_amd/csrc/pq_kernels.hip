@@ -3947,17 +3947,28 @@ __device__ __forceinline__ void lds_copy_bytes(uint32_t src, uint32_t dst, int L
 #define PQ_GLB1 __attribute__((address_space(1)))
 __device__ __forceinline__ void copy_str4_to_lds(const uint8_t *const (&sp)[4], const uint32_t (&dst)[4],
                                                  const int (&ln)[4]) {
+  // the loads of a pair of strings go out together, before either one's
+  // stores (a wave per page has no other wave to hide their latency)
+  uint32_t w2[2][6];
 #pragma unroll
   for (int k = 0; k < 4; k++) {
+    if ((k & 1) == 0) {
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const PQ_GLB1 uint32_t *q = (const PQ_GLB1 uint32_t *)((uintptr_t)sp[k + j] & ~(uintptr_t)3);
+        const bool sh = ln[k + j] > 0 && ln[k + j] <= 16;
+#pragma unroll
+        for (int i = 0; i < 6; i++) w2[j][i] = sh ? q[i] : 0u;
+      }
+    }
     const int L = ln[k];
     if (L <= 0) continue;
     const uint32_t d = dst[k];
     const int h = min((int)((4u - (d & 3u)) & 3u), L);
     if (L <= 16) {
-      const PQ_GLB1 uint32_t *q = (const PQ_GLB1 uint32_t *)((uintptr_t)sp[k] & ~(uintptr_t)3);
       uint32_t w[6];
 #pragma unroll
-      for (int i = 0; i < 6; i++) w[i] = q[i];
+      for (int i = 0; i < 6; i++) w[i] = w2[k & 1][i];
       const uint32_t sk = (uint32_t)((uintptr_t)sp[k] & 3);
       uint32_t r[5];
 #pragma unroll
