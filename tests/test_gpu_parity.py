@@ -481,6 +481,27 @@ def test_tiled_dictionary_fallback_to_plain_strings():
                              data_page_version=ver), "string dict fallback v" + ver)
 
 
+@pytest.mark.parametrize("maxlen", [16, 40, 300])
+def test_nullable_dictionary_strings_staged(maxlen):
+    """Nullable RLE_DICTIONARY BYTE_ARRAY pages on k_decode<2> (type_bytearray.go:
+    57-80 dictionary lookups; chunk_reader.go:206-283): a step's strings go
+    through the wave's LDS stage when its bytes fit (empty strings, <= 16-byte
+    strings from six dwords, longer ones a dword at a time) and the per-string
+    copies when they do not (maxlen 300: ~38 KB steps); nulls every density."""
+    pa = pytest.importorskip("pyarrow")
+    rng = np.random.default_rng(31 + maxlen)
+    rows = 60000
+    lens = rng.integers(0, maxlen + 1, 700)
+    vocab = ["".join(chr(97 + int(c)) for c in rng.integers(0, 26, n)) for n in lens]
+    idx = rng.integers(0, len(vocab), rows)
+    words = [vocab[i] for i in idx]
+    t = pa.table({"a": pa.array(words, mask=rng.random(rows) < 0.3),
+                  "b": pa.array(words, mask=rng.random(rows) < 0.97)})
+    for ver in ("1.0", "2.0"):
+        check_file(_pq_bytes(t, compression="snappy", row_group_size=25000, data_page_version=ver),
+                   "nullable dict strings maxlen %d v%s" % (maxlen, ver))
+
+
 def _c5_bytes(tmp_path, rows, rg_rows, **kw):
     import synth
     path = str(tmp_path / "c5_small.parquet")
