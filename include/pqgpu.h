@@ -41,7 +41,10 @@
 extern "C" {
 #endif
 
-#define PQGPU_ABI_VERSION 1
+/* 2: pqg_batch_stats_get takes the caller's sizeof(pqg_batch_stats) (the
+ *    struct grew six doubles in version 1's lifetime; a size-less call could
+ *    overrun an older caller's struct). */
+#define PQGPU_ABI_VERSION 2
 
 /* Status / error classes (same numbering as the oracle, oracle/pqref.h). */
 typedef enum {
@@ -209,7 +212,10 @@ int pqg_batch_error_location(const pqg_batch *b, int *rg, int *leaf, int *page);
 int pqg_batch_column(const pqg_batch *b, int i, pqg_column_view *out);
 /* Copy one output buffer of selected column i to host memory. */
 int pqg_batch_copy(pqg_batch *b, int i, int buf_id, void *dst, size_t cap, size_t *nbytes);
-int pqg_batch_stats_get(const pqg_batch *b, pqg_batch_stats *out);
+/* Fills min(size, sizeof(pqg_batch_stats)) bytes of *out (pass sizeof(*out));
+ * bytes past the library's struct are zeroed.  size must cover at least the
+ * eleven int64 counters (the version-1 prefix): else PQG_ERR_ARG. */
+int pqg_batch_stats_get(const pqg_batch *b, pqg_batch_stats *out, size_t size);
 /* Device time (ms) per timed segment, averaged over the decodes issued since
  * the previous call (up to 64), from HIP events on the context stream.  By
  * default one segment brackets the decode phase (k_decode + k_expand); with

@@ -6,6 +6,7 @@
 // run are produced 64 at a time, one per lane.  Kernels give each page to one
 // wave and keep many pages in flight per CU to hide the serial header walks.
 #pragma once
+#include <type_traits>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -23,6 +24,29 @@ __device__ __forceinline__ int64_t ufirst64(int64_t x) {
   uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)x);
   uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
   return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+// 64-bit values rebuilt from readlane words.  __builtin_amdgcn_readlane
+// returns int: OR-ing a low word whose bit 31 is set into a 64-bit value
+// without going through uint32_t sign-extends it over the high word (the
+// round-1 deferred-literal fault and the round-5 k_expand_wg run-table fault).
+// Every site that rebuilds a pointer or an int64 from lane words uses these.
+// readlane_u64(v, lo_lane, hi_lane): v a 32-bit lane word, the value's low word
+// in lane lo_lane and its high word in lane hi_lane (a lane-distributed record)
+template <class T>
+__device__ __forceinline__ uint64_t readlane_u64(T v, int lo_lane, int hi_lane) {
+  static_assert(std::is_same<T, uint32_t>::value, "lane words are uint32_t");
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)v, lo_lane);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)v, hi_lane);
+  return ((uint64_t)hi << 32) | (uint64_t)lo;
+}
+// readlane64(v, lane): lane `lane`'s value of a 64-bit per-lane register
+template <class T>
+__device__ __forceinline__ uint64_t readlane64(T v, int lane) {
+  static_assert(sizeof(T) == 8 && (std::is_integral<T>::value || std::is_pointer<T>::value), "a 64-bit operand");
+  const uint64_t x = (uint64_t)v;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, lane);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), lane);
+  return ((uint64_t)hi << 32) | (uint64_t)lo;
 }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ int rank_in(uint64_t mask) {  // number of set bits below this lane

@@ -3309,8 +3309,13 @@ int pqg_batch_copy(pqg_batch *B, int i, int buf, void *dst, size_t cap, size_t *
   return PQG_OK;
 }
 
-int pqg_batch_stats_get(const pqg_batch *B, pqg_batch_stats *o) {
-  if (!B || !o) return PQG_ERR_ARG;
+// ABI 2: the caller passes sizeof its struct; only that many bytes are
+// written, so a caller built against an older (shorter) header is never
+// overrun, and a newer one sees zeros in fields this library lacks.
+int pqg_batch_stats_get(const pqg_batch *B, pqg_batch_stats *out, size_t size) {
+  if (!B || !out || size < offsetof(pqg_batch_stats, create_plan_ms)) return PQG_ERR_ARG;
+  pqg_batch_stats full;
+  pqg_batch_stats *o = &full;
   memset(o, 0, sizeof(*o));
   o->pages = (int64_t)B->pages.size();
   o->data_pages = (int64_t)B->data_list.size();
@@ -3344,6 +3349,8 @@ int pqg_batch_stats_get(const pqg_batch *B, pqg_batch_stats *o) {
     if (cp.str_offsets) bout += (int64_t)cp.str_off_bytes;
   }
   o->output_bytes = bout;
+  memset(out, 0, size);
+  memcpy(out, o, std::min(size, sizeof(full)));
   return PQG_OK;
 }
 

@@ -631,12 +631,9 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, uint32_t
       uintptr_t fsrc = pre ? (uintptr_t)(dst + S) : 0;
       bool in_payload = false;
       for (int k2 = 0; k2 < ndefer; k2++) {  // every lane active: readlane of the deferred-literal table
-        const int64_t kd =
-            (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)def_dst >> 32), k2) << 32) |
-                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)def_dst, k2));
+        const int64_t kd = (int64_t)readlane64(def_dst, k2);
         const int64_t kl = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)def_len, k2);
-        const uint64_t ks = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(def_src >> 32), k2) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)def_src, k2);
+        const uint64_t ks = readlane64(def_src, k2);
         if (pre && S < kd + kl && S + (int64_t)len > kd) {
           if (S >= kd && S + (int64_t)len <= kd + kl) {
             fsrc = (uintptr_t)ks + (uintptr_t)(S - kd);
@@ -854,15 +851,10 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, uint32_t
             uintptr_t from = (p >= 0 && p < F) ? (uintptr_t)(dst + p) : 0;
             bool payload = false;
             for (int k2 = 0; k2 < ndefer; k2++) {
-              const int64_t kd = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
-                                                (int)(uint32_t)((uint64_t)def_dst >> 32), k2)
-                                            << 32) |
-                                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)def_dst, k2));
+              const int64_t kd = (int64_t)readlane64(def_dst, k2);
               const int64_t kl = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)def_len, k2);
               if (p >= kd && p < kd + kl) {
-                const uint64_t ks =
-                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(def_src >> 32), k2) << 32) |
-                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)def_src, k2);
+                const uint64_t ks = readlane64(def_src, k2);
                 from = (uintptr_t)ks + (uintptr_t)(p - kd);
                 payload = true;
               }
@@ -4180,6 +4172,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   }
   const PageDesc d = a.pages[page];
   if (d.dict >= 0 && page_status(a.status, d.dict) != STATUS_OK) return;
+  if (KIND == 5 && (d.lvl_base < 0 || (d.enc != ENC_RLE_DICT && d.enc != ENC_PLAIN))) {
+    // a page the host left whole (no level scratch, or DELTA values) rides in
+    // the part list of a batch where other list pages were split: <5> has
+    // neither the serial level walk nor the DELTA path, so the redo launch
+    // (k_decode<3>, whole pages) decodes it
+    set_status(a.status, page, ST_REDO, 0);
+    return;
+  }
   const ColDesc c = a.cols[d.col];
   const PageInfo pi = a.info[page];
   const int n = d.num_values;
@@ -4709,7 +4709,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
       int64_t start = str_run + incl - tot;
       int si = 0;
       const int64_t T = (int64_t)shfl64((uint64_t)incl, 63);  // the step's string bytes
-      constexpr int64_t BA_STG = (int64_t)sizeof(BaLds) - 32;  // <2>'s stage: the PLAIN walk's LDS, free on this path
+      // <2>'s stage: the PLAIN walk's LDS, free on this path, from 16 bytes in
+      // (a chunk's first read reaches up to 15 bytes before the step's bytes)
+      constexpr int64_t BA_STG = (int64_t)sizeof(BaLds) - 48;
       if (KIND == 2 && d.enc == ENC_RLE_DICT && !defer_bytes && T <= BA_STG) {
         // Dictionary strings (any dictionary size, nulls allowed): each lane
         // copies its values' bytes from the dictionary into an LDS stage,
@@ -4717,7 +4719,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
         // 1,000-word dictionary column: its per-string byte / dword stores
         // were 54 % of a step, tools/diag_decode.py)
         const int64_t P0 = str_run;
-        const uint32_t stg = lds_addr(&bl);
+        const uint32_t stg = lds_addr(&bl) + 16u;
         const uint8_t *cs[4];
         uint32_t cd[4];
         int cl[4];
@@ -5527,8 +5529,7 @@ __device__ __forceinline__ bool job_dict_live(const KArgs &a, uint32_t v) {
   return rec_live(ep, a.epoch) && v0 < lim && bw >= 0;
 }
 __device__ __forceinline__ void job_window(RunWin &W, uint32_t v) {
-  // (readlane returns int: each word through uint32_t, or a low word with bit 31 set sign-extends)
-  const uint64_t rp = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(v, 5) << 32) | (uint32_t)__builtin_amdgcn_readlane(v, 4);
+  const uint64_t rp = readlane_u64(v, 4, 5);
   W.load((const uint2 *)rp, (int32_t)__builtin_amdgcn_readlane(v, 9), (int32_t)__builtin_amdgcn_readlane(v, 10));
 }
 

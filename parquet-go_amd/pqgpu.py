@@ -43,6 +43,9 @@ CompressionCodec_UNCOMPRESSED, CompressionCodec_SNAPPY, CompressionCodec_GZIP, C
 Type_BOOLEAN, Type_INT32, Type_INT64, Type_INT96, Type_FLOAT, Type_DOUBLE, Type_BYTE_ARRAY, \
     Type_FIXED_LEN_BYTE_ARRAY = range(8)
 
+# include/pqgpu.h PQGPU_ABI_VERSION this mirror's structs and signatures follow
+ABI_VERSION = 2
+
 BUF_VALUES, BUF_VALIDITY, BUF_LIST_OFFSETS, BUF_LIST_VALIDITY, BUF_STR_OFFSETS, BUF_DEF, BUF_REP = range(7)
 BATCH_LEVELS = 1
 
@@ -134,7 +137,7 @@ def lib():
                 "pqg_batch_row_groups": (i32, [vp, P(ctypes.c_int), P(ctypes.c_int)]),
                 "pqg_batch_column": (i32, [vp, i32, P(ColumnView)]),
                 "pqg_batch_copy": (i32, [vp, i32, i32, vp, sz, P(sz)]),
-                "pqg_batch_stats_get": (i32, [vp, P(BatchStats)]),
+                "pqg_batch_stats_get": (i32, [vp, P(BatchStats), sz]),
                 "pqg_batch_kernel_times": (i32, [vp, P(ctypes.c_char_p), P(ctypes.c_float), i32]),
                 "pqg_batch_set_timing": (i32, [vp, i32]),
                 "pqg_batch_destroy": (None, [vp]),
@@ -148,6 +151,9 @@ def lib():
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args
+            if L.pqg_abi_version() != ABI_VERSION:
+                raise RuntimeError("%s has ABI version %d, this module follows %d (rebuild the library)"
+                                   % (os.path.basename(_LIB_PATH), L.pqg_abi_version(), ABI_VERSION))
             _LIB = L
         return _LIB
 
@@ -306,7 +312,7 @@ class Batch:
 
     def stats(self):
         s = BatchStats()
-        _check(lib().pqg_batch_stats_get(self._h, ctypes.byref(s)))
+        _check(lib().pqg_batch_stats_get(self._h, ctypes.byref(s), ctypes.sizeof(s)))
         return {f: getattr(s, f) for f, _ in s._fields_}
 
     def set_timing(self, every):

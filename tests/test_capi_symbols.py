@@ -1,9 +1,11 @@
 """CPU tests of the C ABI boundary: libpqgpu.so loads, exports every symbol
 include/pqgpu.h declares, agrees with the oracle on error numbering, and its
 host planner (footer / schema parse) agrees with the oracle.  No compute calls."""
+import ctypes
 import json
 import os
 import re
+import subprocess
 
 import pytest
 
@@ -27,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     L = pqgpu.lib()
     for name in header_functions():
         assert hasattr(L, name), name
-    assert L.pqg_abi_version() == 1
+    assert L.pqg_abi_version() == pqgpu.ABI_VERSION == 2
 
 
 def test_status_numbering_matches_oracle():
@@ -113,3 +115,50 @@ def test_open_many_footers_in_parallel(tmp_path):
     bad.write_bytes(b"PAR1" + b"\0" * 20 + b"PAR1")
     with pytest.raises(pqgpu.PqgError):
         pqgpu.OpenFiles(paths[:2] + [str(bad)])
+
+
+def _c_layout(tmp_path, structs):
+    """sizeof / offsetof of each (struct, [fields]) as the C compiler lays them
+    out from include/pqgpu.h (a probe compiled with gcc, the reference's cgo
+    toolchain would see the same)."""
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "pqgpu.h"', "int main(void) {"]
+    for st, fields in structs:
+        lines.append('printf("%s sizeof %%zu\\n", sizeof(%s));' % (st, st))
+        for f in fields:
+            lines.append('printf("%s %s %%zu\\n", offsetof(%s, %s));' % (st, f, st, f))
+    lines.append("return 0; }")
+    src = tmp_path / "probe.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "probe"
+    subprocess.check_call(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src),
+                           "-o", str(exe)])
+    out = {}
+    for ln in subprocess.check_output([str(exe)]).decode().split("\n"):
+        if ln:
+            st, f, v = ln.split()
+            out[(st, f)] = int(v)
+    return out
+
+
+@pytest.mark.parametrize("cname,pyname", [("pqg_batch_stats", "BatchStats"), ("pqg_column_view", "ColumnView"),
+                                          ("pqg_column_info", "ColumnInfo")])
+def test_struct_layout_matches_ctypes_mirror(tmp_path, cname, pyname):
+    """The header's structs and pqgpu.py's ctypes mirrors agree field by field
+    (offsets) and in size, so neither side reads or writes past the other."""
+    cls = getattr(pqgpu, pyname)
+    fields = [f for f, _ in cls._fields_]
+    lay = _c_layout(tmp_path, [(cname, fields)])
+    assert lay[(cname, "sizeof")] == ctypes.sizeof(cls)
+    for f in fields:
+        assert lay[(cname, f)] == getattr(cls, f).offset, (cname, f)
+
+
+def test_stats_get_argument_contract():
+    """pqg_batch_stats_get(b, out, size) (ABI 2): a null batch or a size short
+    of the version-1 prefix (the eleven int64 counters) is PQG_ERR_ARG.  The
+    prefix rule on a real batch: tests/test_gpu_parity.py
+    test_stats_get_old_caller_size."""
+    L = pqgpu.lib()
+    s = pqgpu.BatchStats()
+    assert L.pqg_batch_stats_get(None, ctypes.byref(s), ctypes.sizeof(s)) == pqgpu.ERR_ARG
+    assert pqgpu.BatchStats.create_plan_ms.offset == 11 * 8

@@ -68,6 +68,43 @@ def test_deferred_literal_payload_high_low_word():
     _check(data, "deferred literal")
 
 
+@pytest.mark.parametrize("family", ["k_dba", "k_plain_str", "k_sw"])
+def test_string_kernels_high_low_word(family):
+    """The high-low-word input layout (every page address's low word has bit
+    31 set) through one file per string kernel family: k_dba (DELTA_BYTE_ARRAY
+    values rebuilt in order), k_plain_str (flat required PLAIN string pages in
+    items) and k_sw_regions / _link / _emit (the region-parallel length walk of
+    >= 64 KiB PLAIN pages and string dictionaries).  Bit-exact against the
+    oracle, as with the ordinary layout."""
+    from test_gpu_parity import _pq_bytes, _plain_string_cases
+    rng = np.random.default_rng(62)
+    if family == "k_dba":
+        files = [("delta_strings", open(os.path.join(GOLDEN, "delta_strings.parquet"), "rb").read())]
+        pa = pytest.importorskip("pyarrow")
+        words = ["prefix_%06d_%s" % (i // 3, "x" * int(k)) for i, k in enumerate(rng.integers(0, 40, 30000))]
+        t = pa.table({"s": pa.array(words)})
+        files.append(("dba generated", _pq_bytes(t, compression="snappy", use_dictionary=False,
+                                                 column_encoding={"s": "DELTA_BYTE_ARRAY"})))
+    else:
+        cases = _plain_string_cases(rng)
+        t = cases["text"]
+        if family == "k_plain_str":  # flat required PLAIN pages, Snappy and not
+            files = [("text %s" % c, _pq_bytes(t, compression=c, use_dictionary=False, data_page_size=1 << 20,
+                                               row_group_size=40000)) for c in ("none", "snappy")]
+        else:  # nullable long pages and a >= 64 KiB string dictionary: the region walk
+            files = [("blob nullable", _pq_bytes(cases["blob_nullable"], compression="snappy", use_dictionary=False,
+                                                 data_page_size=1 << 20, row_group_size=40000)),
+                     ("text dictionary", _pq_bytes(t, compression="none", use_dictionary=True,
+                                                   dictionary_pagesize_limit=1 << 30, data_page_size=1 << 20,
+                                                   row_group_size=40000))]
+    os.environ["PQG_DEBUG_INPUT_HIGH_WORD"] = "1"
+    try:
+        for name, data in files:
+            _check(data, "%s %s high low word" % (family, name))
+    finally:
+        del os.environ["PQG_DEBUG_INPUT_HIGH_WORD"]
+
+
 _GUARD_SCRIPT = r"""
 import glob, os, sys
 sys.path[:0] = [os.path.join(ROOT, "tests"), os.path.join(ROOT, "parquet-go_amd"), os.path.join(ROOT, "oracle")]

@@ -128,6 +128,29 @@ def test_golden_fixture_parity(name, manifest):
             assert np.array_equal(g[k], exp[ek].view(np.uint8).ravel()), (name, key, k)
 
 
+def test_stats_get_old_caller_size():
+    """ABI 2: a caller whose pqg_batch_stats is the version-1 struct (eleven
+    int64 counters, 88 bytes) passes that size and gets exactly those bytes —
+    the same counters as a full-size call — and nothing past them is written;
+    a size short of the prefix is PQG_ERR_ARG."""
+    import ctypes
+    data = golden_bytes("c4_list_str.parquet")
+    r = pqgpu.FileReader(data)
+    b = r.batch(0, r.RowGroupCount(), list(range(len(r.Columns()))), 0)
+    try:
+        full = b.stats()
+        L = pqgpu.lib()
+        buf = (ctypes.c_uint8 * 160)(*([0xAB] * 160))
+        assert L.pqg_batch_stats_get(b._h, ctypes.cast(buf, ctypes.POINTER(pqgpu.BatchStats)), 88) == 0
+        got = np.frombuffer(bytes(buf), np.int64, 11)
+        names = [f for f, _ in pqgpu.BatchStats._fields_][:11]
+        assert list(got) == [full[k] for k in names]
+        assert bytes(buf)[88:] == b"\xab" * 72
+        assert L.pqg_batch_stats_get(b._h, ctypes.cast(buf, ctypes.POINTER(pqgpu.BatchStats)), 80) == pqgpu.ERR_ARG
+    finally:
+        b.close()
+
+
 def test_row_group_subsets():
     data = golden_bytes("c4_list_str.parquet")
     check_file(data, "c4 rg1", 1, 2)
@@ -433,6 +456,46 @@ def test_list_page_parts(part):
         assert len(outcomes) >= 2, outcomes
     finally:
         del os.environ["PQG_NEST_PART"]
+
+
+@pytest.mark.parametrize("part", ["256", ""])
+def test_list_parts_beside_unsplit_pages(part):
+    """A batch where one list column's pages are split into k_decode<5> parts
+    and another list column's pages stay whole because the planner does not
+    split them: DELTA_BINARY_PACKED list<int64> / list<int32> values
+    (deltabp_decoder.go), which <5> has no path for.  Those pages ride in the
+    part list unsplit, are handed to the whole-page redo launch
+    (k_decode<3>) and decode bit-exact against the oracle, V1 and V2, with and
+    without nulls; a corrupted DELTA list page reports the oracle's error."""
+    pa = pytest.importorskip("pyarrow")
+    pq = pytest.importorskip("pyarrow.parquet")
+    rng = np.random.default_rng(61)
+    n = 40000
+    lists = [None if rng.random() < 0.05 else [None if rng.random() < 0.05 else int(v)
+                                                for v in rng.integers(-3000, 3000, rng.poisson(4))] for _ in range(n)]
+    z64 = [None if x is None else [None if v is None else v * 1000003 + 7 for v in x] for x in lists]
+    z32 = [None if x is None else [None if v is None else v * 13 for v in x] for x in lists]
+    t = pa.table({"d": pa.array(lists, pa.list_(pa.int32())), "z": pa.array(z64, pa.list_(pa.int64())),
+                  "y": pa.array(z32, pa.list_(pa.int32()))})
+    if part:
+        os.environ["PQG_NEST_PART"] = part
+    try:
+        for ver in ("1.0", "2.0"):
+            check_file(_pq_bytes(t, compression="snappy", row_group_size=20000, data_page_version=ver,
+                                 use_dictionary=["d"], column_encoding={"z": "DELTA_BINARY_PACKED",
+                                                                        "y": "DELTA_BINARY_PACKED"}),
+                       "delta lists beside parts %s v%s" % (part, ver))
+        base = _pq_bytes(t, compression="none", row_group_size=n, use_dictionary=["d"], data_page_size=16 << 10,
+                         column_encoding={"z": "DELTA_BINARY_PACKED", "y": "DELTA_BINARY_PACKED"})
+        cc = pq.ParquetFile(io.BytesIO(base)).metadata.row_group(0).column(1)
+        lo, hi = cc.data_page_offset, cc.data_page_offset + cc.total_compressed_size
+        for trial in range(6):
+            data = bytearray(base)
+            p = int(rng.integers(lo + 32, hi))
+            data[p] ^= int(rng.integers(1, 256))
+            check_file(bytes(data), "delta lists beside parts %s corrupt %d" % (part, trial))
+    finally:
+        os.environ.pop("PQG_NEST_PART", None)
 
 
 def _req_table(cols):
