@@ -6,6 +6,8 @@ analysis tools import this; the decoder never does.
 
   c1  required INT64, PLAIN, uncompressed, V1                      (configs[0])
   c2  required INT32 dictionary, index bit width 1..20, Snappy, V1  (configs[1])
+  c2runs  the same with run-heavy keys: runs of one key, geometric
+          length with mean 16 (SURVEY.md §8(d) C2's run-heavy variant)
   c3  DELTA_BINARY_PACKED INT64 ts + optional DOUBLE, V2, Snappy    (configs[2])
   c4  LIST<INT32> + dictionary STRING with rep/def levels, V1       (configs[3])
   c5  TPC-H lineitem-shaped, 16 columns, Snappy, V1                 (configs[4])
@@ -20,6 +22,7 @@ import numpy as np
 DEFAULTS = {
     "c1": (10_000_000, 1 << 20),
     "c2": (100_000_000, 1 << 20),
+    "c2runs": (100_000_000, 1 << 20),
     "c3": (100_000_000, 1 << 20),
     "c4": (20_000_000, 1 << 20),
     "c5": (45_300_000, 1_415_625),
@@ -28,12 +31,14 @@ DEFAULTS = {
 DESCR = {
     "c1": "C1: INT64 PLAIN, uncompressed, V1, %d rows, %d-row row groups",
     "c2": "C2: INT32 RLE_DICTIONARY bw 1-20, Snappy, V1, %d rows, %d-row row groups",
+    "c2runs": "C2 run-heavy: INT32 RLE_DICTIONARY bw 1-20, keys in runs of geometric length (mean 16), Snappy, V1, "
+              "%d rows, %d-row row groups",
     "c3": "C3: DELTA_BINARY_PACKED INT64 ts + optional DOUBLE (10%% nulls), V2, Snappy, %d rows, %d-row row groups",
     "c4": "C4: LIST<INT32> (maxD 3, maxR 1) + dictionary STRING (10%% nulls), V1, Snappy, %d rows, %d-row row groups",
     "c5": "C5: TPC-H lineitem-shaped 16 columns, Snappy, V1, %d rows, %d-row row groups (one GPU's 32 of 256 RGs)",
 }
 
-DTYPE = {"c1": "int64", "c2": "int32", "c3": "int64+f64 bits", "c4": "int32+bytes", "c5": "int64/int32/f64 bits/bytes"}
+DTYPE = {"c1": "int64", "c2": "int32", "c2runs": "int32", "c3": "int64+f64 bits", "c4": "int32+bytes", "c5": "int64/int32/f64 bits/bytes"}
 
 
 def _write(path, schema, gen, rows, rg_rows, **kw):
@@ -75,6 +80,26 @@ def make(cfg, path, rows, rg_rows, fixed_bw=0, **writer_kw):
             K = 1 << bw
             dvals = (rng.permutation(K).astype(np.int64) * 2654435761 % (1 << 32) - (1 << 31)).astype(np.int32)
             return pa.table({"v": pa.array(dvals[rng.integers(0, K, n)])}, schema=schema)
+        _write(path, schema, gen, rows, rg_rows, compression="snappy", use_dictionary=True,
+               data_page_version="1.0", dictionary_pagesize_limit=1 << 30)
+
+    elif cfg == "c2runs":
+        # every row group: runs of one dictionary key, run lengths geometric
+        # with mean 16 (pyarrow's hybrid encoder makes RLE runs of the runs of
+        # 8 or more, bit-packed groups of the rest), so the pages take the
+        # run-table path of the expand and compress under Snappy
+        rng = np.random.default_rng(22)
+        schema = pa.schema([pa.field("v", pa.int32(), nullable=False)])
+
+        def gen(i, d, n):
+            bw = fixed_bw if fixed_bw else 1 + (i % 20)
+            K = 1 << bw
+            dvals = (rng.permutation(K).astype(np.int64) * 2654435761 % (1 << 32) - (1 << 31)).astype(np.int32)
+            lens = rng.geometric(1.0 / 16, n // 8 + 64)
+            while lens.sum() < n:
+                lens = np.concatenate([lens, rng.geometric(1.0 / 16, n // 8 + 64)])
+            keys = np.repeat(rng.integers(0, K, len(lens)), lens)[:n]
+            return pa.table({"v": pa.array(dvals[keys])}, schema=schema)
         _write(path, schema, gen, rows, rg_rows, compression="snappy", use_dictionary=True,
                data_page_version="1.0", dictionary_pagesize_limit=1 << 30)
 
