@@ -93,6 +93,8 @@ struct PageDesc {
                          // suffix / prefix lengths; PLAIN (offset, length) per value from k_prepare's walk
   int32_t sidx;          // index in the Snappy page list (-1: not decoded by k_snappy)
   int32_t swalk;         // long PLAIN BYTE_ARRAY page: index in the region-parallel length walk (-1: none)
+  int64_t sp_base;       // flat dictionary-string page split into k_decode<2> parts: first entry of its
+                         // string-byte prefix table (k_prepare: bytes of values [0, 256 s)); -1: none
   int64_t lvl_base;      // page with levels on k_prepare's count path: byte offset of its decoded
                          // levels in the level scratch (rep bytes if max_rep > 0, then def bytes,
                          // num_values each); -1: k_decode reads the level streams itself
@@ -154,6 +156,7 @@ constexpr uint32_t WG_SLICE = 160 * 1024;  // LDS bytes of a slice (the CU's LDS
 constexpr int WG_MAX_SLICES = 4;
 constexpr int WG_JOBS = 64;
 constexpr int PLAIN_STR_ITEM = 2048;      // k_plain_str: values per work item
+constexpr int STR_PART = 2048;            // k_decode<2>: level entries per part of a split dictionary-string page
 struct LdsGroup {
   int32_t job0, njobs;   // jobs [job0, job0 + njobs) of the launch order
   int32_t dpage;         // the chunk's dictionary page; -1: one job per wave, L1/L2 gathers

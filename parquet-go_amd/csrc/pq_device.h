@@ -122,6 +122,9 @@ __device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) { return wave
 __device__ __forceinline__ int32_t wave_sum32(int32_t v) {
   return (int32_t)__builtin_amdgcn_readlane(wave_incl_dpp<false>((uint32_t)v), 63);
 }
+__device__ __forceinline__ int64_t wave_sum64(int64_t v) {
+  return (int64_t)readlane64(wave_incl_add64_dpp((uint64_t)v), 63);
+}
 // exclusive wave prefix sum; *total receives the wave total (uniform)
 __device__ __forceinline__ int32_t wave_excl_scan32(int32_t v, int32_t *total) {
   int32_t incl = wave_incl_scan32_impl(v);

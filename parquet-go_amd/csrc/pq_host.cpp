@@ -82,8 +82,9 @@ struct pq_launch_args {
   const int32_t *walk, *seg_base;
   int64_t *segs;
   uint32_t *seg_flag;
-  const int32_t *parts;  // k_decode<3>: (page, first level, end level) triplets instead of `list`
-  int32_t redo;          // k_decode<3>: decode again (whole) the pages whose parts failed
+  const int32_t *parts;  // k_decode<3> / <2>: (page, first level, end level) triplets instead of `list`
+  int32_t redo;          // k_decode<3> / <2>: decode again (whole) the pages whose parts failed
+  int64_t *str_pre;      // k_prepare -> k_decode<2> parts: string bytes before every 256 values of a page
   const int64_t *hjobs;
   int32_t nhjobs;
   int32_t grid_cap;  // k_levels<-1>: at most this many workgroups (grid-stride loop)
@@ -799,6 +800,11 @@ struct pqg_batch {
   uint64_t *d_dict = nullptr;
   int32_t *d_lists = nullptr;
   int32_t *d_parts = nullptr;  // nest_parts on the device
+  std::vector<int32_t> str_parts;  // k_decode<2> waves: (page, first level, end level) triplets
+  int64_t str_pre_entries = 0;     // prefix-table entries of the split pages (PageDesc::sp_base)
+  bool str_split = false;          // some k_decode<2> page is split
+  int32_t *d_str_parts = nullptr;
+  int64_t *d_str_pre = nullptr;
   int32_t *d_part_pre = nullptr;  // per part: counts before it (k_levels -> k_decode<3>)
   void *d_jobs = nullptr;        // deferred long-literal copy jobs (k_snappy -> k_copy)
   uint32_t *d_njobs = nullptr;   // per Snappy page: jobs written
@@ -1634,6 +1640,7 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
     d.lens_base = -1;
     d.lvl_base = -1;
     d.part0 = -1;
+    d.sp_base = -1;
     d.sidx = -1;
     d.swalk = -1;
     d.col = ci;
@@ -2454,6 +2461,40 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   B->general_flat.clear();
   B->ngen_str4 = (int32_t)B->general_str4.size();
   B->ngen_str = (int32_t)(B->general_str4.size() + B->general_str.size());
+  {
+    // k_decode<2>'s flat dictionary-string pages (nullable: C4's strings;
+    // ~20,000 entries a page, one wave each left most of the GPU idle) in
+    // parts of ~STR_PART entries, a wave each.  Part boundaries sit on 256-slot
+    // steps of the column (the validity words a step writes are its own); a
+    // part counts the values before it from k_levels' level scratch and takes
+    // their string bytes from k_prepare's per-256-value prefix table
+    // (PageDesc::sp_base), then seeks the key stream.  PQG_STR_PART (analysis):
+    // entries a part, 0: whole pages.
+    B->str_parts.clear();
+    B->str_pre_entries = 0;
+    B->str_split = false;
+    static const int64_t spart = knob("PQG_STR_PART") ? atoll(knob("PQG_STR_PART")) : STR_PART;
+    for (int32_t pg : B->general_str) {
+      PageDesc &pd = B->pages[(size_t)pg];
+      const int64_t n = std::max(pd.num_values, 0);
+      pd.sp_base = -1;
+      const bool can = spart > 0 && pd.enc == ENC_RLE_DICT && pd.dict >= 0 && (pd.lvl_bits || pd.lvl_base >= 0) &&
+                       n >= 2 * spart;
+      if (!can) {
+        B->str_parts.insert(B->str_parts.end(), {pg, 0, (int32_t)n});
+        continue;
+      }
+      pd.sp_base = B->str_pre_entries;
+      B->str_pre_entries += n / 256 + 2;
+      B->str_split = true;
+      for (int64_t lo = 0; lo < n;) {
+        int64_t hi = ((pd.level_base + lo + spart + 255) & ~(int64_t)255) - pd.level_base;
+        if (n - hi < spart / 2) hi = n;
+        B->str_parts.insert(B->str_parts.end(), {pg, (int32_t)lo, (int32_t)hi});
+        lo = hi;
+      }
+    }
+  }
   B->general_list.insert(B->general_list.end(), B->general_str4.begin(), B->general_str4.end());
   B->general_list.insert(B->general_list.end(), B->general_str.begin(), B->general_str.end());
   B->general_str4.clear();
@@ -2519,6 +2560,8 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     tab.put((void **)&B->d_lists, lists.data(), sizeof(int32_t) * lists.size());
     tab.put((void **)&B->d_parts, B->nest_parts.data(), sizeof(int32_t) * B->nest_parts.size());
     tab.put((void **)&B->d_part_pre, nullptr, sizeof(int32_t) * 4 * (B->nest_parts.size() / 3 + 1));
+    tab.put((void **)&B->d_str_parts, B->str_parts.data(), sizeof(int32_t) * B->str_parts.size());
+    tab.put((void **)&B->d_str_pre, nullptr, sizeof(int64_t) * (size_t)(B->str_pre_entries + 1));
     tab.put((void **)&B->d_lgroups, B->lgroups.data(), sizeof(LdsGroup) * (B->lgroups.size() + 1));
     tab.put((void **)&B->d_page_jobs, pj.data(), sizeof(int32_t) * pj.size());
     tab.put((void **)&B->d_sitems, B->snap_items.data(), 4 * B->snap_items.size());
@@ -2846,6 +2889,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   a.lvl = B->d_lvl;
   a.part_tab = B->d_parts;
   a.part_pre = B->d_part_pre;
+  a.str_pre = B->d_str_pre;
   a.status0 = B->d_status0;
   a.zr = B->d_zr;
   a.nzr = upto_scan ? 0 : B->nzr;  // the bitmaps are written by the decode kernels only
@@ -3088,7 +3132,17 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
       e |= pq_launch(31, &a, LN.side[1]);  // k_decode<4>: flat required dictionary strings
       a.list += B->ngen_str4;
       a.nlist = B->ngen_str - B->ngen_str4;
-      e |= pq_launch(15, &a, LN.side[1]);  // k_decode<2>: the other flat BYTE_ARRAY pages
+      if (B->str_split) {
+        pq_launch_args ap = a;
+        ap.parts = B->d_str_parts;
+        ap.nlist = (int32_t)(B->str_parts.size() / 3);
+        e |= pq_launch(15, &ap, LN.side[1]);  // k_decode<2>: the other flat BYTE_ARRAY pages, in parts
+        ap = a;
+        ap.redo = 1;
+        e |= pq_launch(15, &ap, LN.side[1]);  // k_decode<2>: pages whose later parts failed, whole
+      } else {
+        e |= pq_launch(15, &a, LN.side[1]);  // k_decode<2>: the other flat BYTE_ARRAY pages
+      }
       hipEventRecord(LN.join[1], LN.side[1]);
     }
     if (B->ngen_nest > 0) {
@@ -3633,6 +3687,7 @@ static int device_snappy_block(pqg_ctx *ctx, const uint8_t *src, size_t n, uint8
     PageDesc d;
     memset(&d, 0, sizeof(d));
     d.part0 = -1;
+    d.sp_base = -1;
     d.kind = PAGE_DICT;
     d.comp_len = (int32_t)n;
     d.body_len = (int32_t)expect;

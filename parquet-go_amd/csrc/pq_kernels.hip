@@ -98,8 +98,9 @@ struct KArgs {
   const int32_t *seg_base;  // per Snappy-list position: first entry in segs (nseg = next - this)
   int64_t *segs;          // per segment: stream offset of its first token (k_snappy_walk)
   uint32_t *seg_flag;     // per Snappy-list position: 0 segments ok, 1 serial fallback, 2 nothing to do
-  const int32_t *parts;   // k_decode<3>: (page, first level, end level) per wave, instead of `list`
-  int32_t redo;           // k_decode<3>: the pages left at ST_REDO by their parts, decoded whole
+  const int32_t *parts;   // k_decode<3> / <2>: (page, first level, end level) per wave, instead of `list`
+  int32_t redo;           // k_decode<3> / <2>: the pages left at ST_REDO by their parts, decoded whole
+  int64_t *str_pre;       // split k_decode<2> pages: string bytes before every 256 values (k_prepare)
   const int32_t *part_tab;  // list-page parts (as `parts`), for k_levels
   int32_t *part_pre;        // per part: rows, slots, values before it (4 ints; PageDesc::part0)
 };
@@ -217,6 +218,22 @@ constexpr int SNAPPY_WAVES = 4;
 // chunks (1 KiB per wave instruction); the source is read as aligned dwords
 // and funnel-shifted (v_alignbyte) by the uniform source/destination skew.
 // Only the last RING bytes also enter the LDS history.
+// A far copy reads back this wave's own staged output.  Stores of the same CU
+// are visible to its loads through the CU's L1 once complete (the workgroup
+// fence before the far copies waits for them; a workgroup acquire needs no L1
+// invalidate), so the loads are plain global loads — served by L1 / the XCD's
+// L2 — instead of device-scope ones, which on gfx950 miss the L2 and went to
+// the Infinity Cache / HBM for every copy (C3: k_snappy's FETCH was 11x its
+// compressed input).  PQ_FAR_AGENT (analysis) restores device scope.
+template <class T>
+__device__ __forceinline__ T far_ld(const T *p) {
+#ifdef PQ_FAR_AGENT
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  return *(const __attribute__((address_space(1))) T *)p;
+#endif
+}
+
 __device__ __forceinline__ void copy_literal(const uint8_t *s, uint8_t *dst, int64_t dpos, int64_t len, uint8_t *ring,
                                              int lane) {
   uint8_t *D = dst + dpos;
@@ -356,7 +373,7 @@ struct SnapLds {  // per wave
       uint4 tok[SB_TOK];        // {out_rel, len | literal << 31 | prefilled << 30, literal: window byte / copy: offset, 0}
       uint2 bmc[SB_OUT / 32];   // token-start bits, tokens starting in earlier words
     };
-    uint16_t jt[264];           // token chain: entry addresses of J_b over window positions 0..256
+    uint16_t jt[280];           // token chain: entry addresses of J_b over window positions 0..256 (jt_off)
   };
 };
 
@@ -455,10 +472,10 @@ __device__ __forceinline__ void lds_st64(uint32_t a, uint32_t lo, uint32_t hi) {
 }
 __device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) { *(PQ_LDS uint32_t *)(uintptr_t)a = v; }
 
-// Tag tables of k_snappy (one per workgroup, LDS): [tag] the stream bytes of
-// a short token (a literal's tag and payload, a copy's header; 255 for a long
-// literal's tag), [256 + tag] its output length (0: long literal) —
-// decode_other.go:27-86's cases as two lookups instead of a branch per case.
+// Tag table of k_snappy (one per workgroup, LDS), a u16 per tag: the stream
+// bytes of a short token (a literal's tag and payload, a copy's header; 255
+// for a long literal's tag) | its output length << 8 (0: long literal) —
+// decode_other.go:27-86's cases as one lookup instead of a branch per case.
 constexpr int SNAP_LUT = 512;
 __device__ __forceinline__ void snappy_lut_init(uint8_t *lut, int tag) {
   const uint32_t t = (uint32_t)tag & 3, x = (uint32_t)tag >> 2;
@@ -473,8 +490,26 @@ __device__ __forceinline__ void snappy_lut_init(uint8_t *lut, int tag) {
     need = t == 2 ? 3u : 5u;
     len = x + 1;
   }
-  lut[tag] = (uint8_t)need;
-  lut[256 + tag] = (uint8_t)len;
+  // one u16 a tag (stream bytes | output length << 8): one ds_read_u16 a
+  // token instead of two byte reads at independent random banks
+  *(uint16_t *)(lut + 2 * tag) = (uint16_t)(need | (len << 8));
+}
+
+// The chain table's byte offset of window position p: PQ_JT_PAD bytes after
+// every 64 positions.  Lane l's reads of a round land near position 4 l + c,
+// so lanes l and l + 16 of a 32-lane group hit one bank; a pad of 8 shifts
+// each 64-position block by two banks (the lanes' 8-byte stores stay 8-byte
+// aligned).  Measured (round 6, analysis variants): C3 3.218 ms unpadded vs
+// 3.255 padded, C5 16.14 vs 16.19 — the jump rounds are not bound by these
+// conflicts, so the default is no pad.
+#ifndef PQ_JT_PAD
+#define PQ_JT_PAD 0
+#endif
+__device__ __forceinline__ uint32_t jt_off(uint32_t p) { return 2 * p + PQ_JT_PAD * (p >> 6); }
+__device__ __forceinline__ uint32_t jt_pos(uint32_t off) {  // inverse of jt_off (off <= jt_off(256))
+  const uint32_t blk = (uint32_t)(off >= 128 + PQ_JT_PAD) + (uint32_t)(off >= 2 * (128 + PQ_JT_PAD)) +
+                       (uint32_t)(off >= 3 * (128 + PQ_JT_PAD)) + (uint32_t)(off >= 4 * (128 + PQ_JT_PAD));
+  return (off - PQ_JT_PAD * blk) >> 1;
 }
 
 // One batch starting at the short token at s.  Returns false on a corrupt
@@ -512,8 +547,8 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, uint32_t
   L.win[lane + 64] = g1;
   if (lane < 4) L.win[lane + 128] = g2;
   const uint32_t wb = lds_addr(L.win);  // window byte 0
-  const uint32_t tb = lds_addr(L.jt);   // chain table (u16): the entry of position i at tb + 2 i
-  const uint32_t stop = tb + 2 * 256;   // position 256: the chain's end (its entry points at itself)
+  const uint32_t tb = lds_addr(L.jt);      // chain table (u16): the entry of position i at tb + jt_off(i)
+  const uint32_t stop = tb + jt_off(256);  // position 256: the chain's end (its entry points at itself)
   // J_0 of this lane's positions 4 lane + j (the bytes of its window dword):
   // the entry address of the position after a token starting there.  Token
   // sizes SWAR over the 4 tags: a literal x + 2, copies 2 / 3 / 5 by a byte
@@ -524,8 +559,9 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, uint32_t
   const uint32_t need4 = ((x4 + 0x02020202u) & mlit) | (__builtin_amdgcn_perm(0u, 0x05030200u, t4) & ~mlit);
   uint32_t J[4];
 #pragma unroll
-  for (int j = 0; j < 4; j++) J[j] = tb + 2 * min(4 * (uint32_t)lane + j + ((need4 >> (8 * j)) & 0xffu), 256u);
-  lds_st64(tb + 8 * (uint32_t)lane, J[0] | (J[1] << 16), J[2] | (J[3] << 16));
+  for (int j = 0; j < 4; j++) J[j] = tb + jt_off(min(4 * (uint32_t)lane + j + ((need4 >> (8 * j)) & 0xffu), 256u));
+  const uint32_t jl = tb + jt_off(4 * (uint32_t)lane);  // this lane's four entries (8-byte aligned)
+  lds_st64(jl, J[0] | (J[1] << 16), J[2] | (J[3] << 16));
   if (lane == 0) lds_st16(stop, stop);
   SNAP_T(0);
   // 2. the token chain by pointer jumping, in place: J_b+1 = J_b o J_b (a
@@ -533,7 +569,7 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, uint32_t
   // run in order); lane m applies J_b for the set bits b of m starting at
   // sh, so it lands on the m-th token
   wave_lds_sync();
-  uint32_t P = tb + 2 * (uint32_t)sh;
+  uint32_t P = tb + jt_off((uint32_t)sh);
 #pragma unroll
   for (int b = 0; b < 6; b++) {
     const uint32_t hop = lds_u16(P);
@@ -543,7 +579,7 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, uint32_t
       for (int j = 0; j < 4; j++) n[j] = lds_u16(J[j]);
 #pragma unroll
       for (int j = 0; j < 4; j++) J[j] = n[j];
-      lds_st64(tb + 8 * (uint32_t)lane, n[0] | (n[1] << 16), n[2] | (n[3] << 16));
+      lds_st64(jl, n[0] | (n[1] << 16), n[2] | (n[3] << 16));
     }
     if ((lane >> b) & 1) P = hop;
     if (b < 5) wave_lds_sync();
@@ -553,10 +589,11 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, uint32_t
   // src, length <= remaining dst, 0 < offset <= d)
   const int64_t lim64 = (int64_t)sh + (slen - s) - 1;  // last position inside the block
   const uint32_t lim = lim64 < 255 ? (uint32_t)lim64 : 255u;
-  const uint32_t pos = (P - tb) >> 1;
+  const uint32_t pos = jt_pos(P - tb);
   const uint32_t pa = wb + pos;
   const uint32_t tag = lds_u8(pa);
-  const uint32_t need = lds_u8(lut + tag), len0 = lds_u8(lut + 256 + tag);
+  const uint32_t nl = lds_u16(lut + 2 * tag);
+  const uint32_t need = nl & 0xffu, len0 = nl >> 8;
   const uint32_t d0 = lds_u32(pa & ~3u), d1 = lds_u32((pa & ~3u) + 4);
   const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, pa & 3u), hi = __builtin_amdgcn_alignbyte(0u, d1, pa & 3u);
   const uint32_t t = tag & 3;
@@ -566,7 +603,7 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, uint32_t
   const uint32_t c4 = __builtin_amdgcn_alignbyte(hi, lo, 1u);   // tagCopy4
   // literal: window position of its bytes / copy: offset
   const uint32_t x = lit ? pos + 1 : t == 1 ? c1 : t == 2 ? c2 : c4;
-  const bool valid = P <= tb + 2 * lim && len0 != 0;
+  const bool valid = pos <= lim && len0 != 0;
   const int64_t rem64 = slen - s, room64 = dl - dpos;
   const int32_t rem = rem64 < 0x40000000 ? (int32_t)rem64 : 0x40000000;  // stream bytes from s
   const int32_t room = room64 < 0x40000000 ? (int32_t)room64 : 0x40000000;
@@ -649,14 +686,13 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, uint32_t
         // overlaps the steps between
         const uintptr_t b8 = fsrc & ~(uintptr_t)7;
         const uint64_t *qp = (const uint64_t *)b8;
-        fq0 = in_payload ? qp[0] : __hip_atomic_load(qp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fq0 = in_payload ? qp[0] : far_ld(qp);
         if ((int)(fsrc & 7) + (int)len > 8)
-          fq1 = in_payload ? qp[1] : __hip_atomic_load(qp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          fq1 = in_payload ? qp[1] : far_ld(qp + 1);
         fsh = (int)(fsrc & 7);
         fdefer = true;
       } else if (pre) {
-        // <= 64 source bytes: up to 9 aligned qwords; staged output read at
-        // device scope (bypasses a possibly stale L1 line)
+        // <= 64 source bytes: up to 9 aligned qwords of staged output (far_ld)
         const uintptr_t b8 = fsrc & ~(uintptr_t)7;
         const int sh8 = (int)(fsrc & 7);
         const int64_t o = dpos + out_rel;
@@ -664,7 +700,7 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, uint32_t
         for (int w = 0; w < 9; w++) {
           if (w * 8 >= sh8 + (int)len) break;
           const uint64_t *qp = (const uint64_t *)(b8 + 8 * (uintptr_t)w);
-          const uint64_t v = in_payload ? *qp : __hip_atomic_load(qp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint64_t v = in_payload ? *qp : far_ld(qp);
 #pragma unroll
           for (int bb = 0; bb < 8; bb++) {
             const int i2 = w * 8 + bb - sh8;
@@ -865,8 +901,7 @@ __device__ __forceinline__ bool snappy_batch(SnapLds &L, uint8_t *ring, uint32_t
               if (payload) {
                 b = *(const uint8_t *)from;
               } else {
-                const uint32_t word = __hip_atomic_load((const uint32_t *)(from & ~(uintptr_t)3), __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t word = far_ld((const uint32_t *)(from & ~(uintptr_t)3));
                 b = (uint8_t)(word >> ((from & 3) * 8));
               }
             }
@@ -921,7 +956,7 @@ template <int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PQ_SNAPPY_WPE))) void k_snappy(KArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t ring_all[SNAPPY_WAVES][RING];
   __shared__ SnapLds sl_all[SNAPPY_WAVES];
-  __shared__ uint8_t snap_lut[SNAP_LUT];
+  __shared__ __attribute__((aligned(4))) uint8_t snap_lut[SNAP_LUT];
   snappy_lut_init(snap_lut, (int)threadIdx.x);  // (256 threads: one tag each)
   __syncthreads();
   const int lane = lane_id();
@@ -3515,8 +3550,12 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
         wave_lds_sync();
       }
       int64_t acc = 0;
+      // a page split into k_decode<2> parts: the string bytes before every 256
+      // values, where a part's count starts (entry q: values [0, 256 q))
+      int64_t *spre = d.sp_base >= 0 && a.str_pre ? a.str_pre + d.sp_base : nullptr;
       for (int64_t k0 = 0; k0 < nn; k0 += 256) {
         const int cnt = (int)min<int64_t>(256, nn - k0);
+        if (spre && lane == 0) spre[k0 >> 8] = acc;
         uint32_t k4[4];
         e = keys.next4(cnt, k4);
         if (e) {
@@ -3540,6 +3579,7 @@ __device__ __forceinline__ void prepare_page(const KArgs &a, int gi, uint8_t *lb
           if (4 * lane + j < cnt) l += elds ? (int64_t)elen[k4[j]] : (int64_t)(a.dict_ent[dd.dict_base + k4[j]] & 0xffffffffu);
         acc += (int64_t)ufirst64((int64_t)shfl64((uint64_t)wave_incl_scan64(l), 63));
       }
+      if (spre && lane == 0) spre[(nn + 255) >> 8] = acc;
       sbytes = acc;
     } else if (dstr) {
       // byteArrayDeltaLengthDecoder.next (:111-123) and, for DELTA_BYTE_ARRAY,
@@ -4154,7 +4194,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   // k_levels' level bytes, the key stream is skipped to the part's first
   // value.  A part after the first that meets an error marks the page
   // ST_REDO, and the redo launch decodes it whole for the reference's status.
-  const bool part = (KIND == 3 && a.parts != nullptr) || KIND == 5;
+  // KIND 2 with a.parts: entries [e_lo, e_hi) of a flat dictionary-string
+  // page; the values before e_lo are counted from k_levels' level scratch,
+  // their string bytes taken from k_prepare's prefix table (PageDesc::sp_base)
+  const bool part = ((KIND == 3 || KIND == 2) && a.parts != nullptr) || KIND == 5;
   int page;
   int64_t e_lo = 0, e_hi = 0x7fffffffffffll;
   if (part) {
@@ -4164,7 +4207,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   } else {
     page = ufirst(a.list[gi]);
   }
-  if (KIND == 3 && a.redo) {
+  if ((KIND == 3 || KIND == 2) && a.redo) {
     if (page_status(a.status, page) != make_status(ST_REDO, 0)) return;
     if (lane == 0) __hip_atomic_store(&a.status[page], STATUS_OK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else if (page_status(a.status, page) != STATUS_OK) {
@@ -4279,7 +4322,50 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   int64_t e0 = 0, slot_run = 0, row_run = 0, nn_run = 0, str_run = pi.str_base;
   uint32_t err = E_OK, err_stage = 0;
   const int64_t e_end = part ? min<int64_t>(e_hi, (int64_t)n) : (int64_t)n;
-  if (part && e_lo > 0 && d.part0 >= 0) {
+  if (KIND == 2 && part && e_lo > 0) {
+    // (only dictionary pages with a level scratch and a prefix table are split)
+    if (d.sp_base < 0 || d.enc != ENC_RLE_DICT || !(d.lvl_bits || d.lvl_base >= 0)) {
+      set_status(a.status, page, ST_REDO, 0);
+      return;
+    }
+    int64_t cn = 0;  // values (def == max_def) among entries [0, e_lo)
+    if (d.lvl_bits) {
+      const uint32_t *lw = (const uint32_t *)(a.lvl + d.lvl_base);
+      const int64_t nw = e_lo >> 5;
+      for (int64_t w = lane; w < nw; w += 64) cn += __popc(lw[w]);
+      if (lane == 0 && (e_lo & 31)) cn += __popc(lw[nw] & ((1u << (e_lo & 31)) - 1u));
+    } else {
+      const uint8_t *ld = a.lvl + d.lvl_base;
+      for (int64_t b = lane; b < e_lo; b += 64) cn += (int)ld[b] == c.max_def;
+    }
+    nn_run = wave_sum32((int32_t)cn);
+    row_run = e_lo;
+    slot_run = e_lo;
+    e0 = e_lo;
+    // the string bytes of values [0, nn_run): the table's entry at the 256-value
+    // step below, then the keys of the step's first nn_run & 255 values
+    const int64_t q = nn_run & ~(int64_t)255;
+    if (keys.skip(q) != E_OK) {
+      set_status(a.status, page, ST_REDO, 0);
+      return;
+    }
+    int64_t sb = a.str_pre[d.sp_base + (q >> 8)];
+    const int rem = (int)(nn_run - q);
+    if (rem > 0) {
+      uint32_t k4[4];
+      if (keys.next4(rem, k4) != E_OK) {
+        set_status(a.status, page, ST_REDO, 0);
+        return;
+      }
+      int64_t l = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (4 * lane + j < rem && (int64_t)k4[j] < dict_n)
+          l += (int64_t)(uint32_t)(a.dict_ent[dict_base + k4[j]] & 0xffffffffu);
+      sb += wave_sum64(l);
+    }
+    str_run = pi.str_base + sb;
+  } else if (part && e_lo > 0 && d.part0 >= 0) {
     // rows (rep 0), slots (def >= rep_def) and values (def == max_def) before
     // the part: counted by k_levels
     row_run = ufirst(a.part_pre[4 * gi]);
@@ -5101,6 +5187,9 @@ __device__ void expand_direct(const KArgs &a, const ExPage &P, int page, int w, 
 // dealt so that the jobs of one column chunk (one dictionary) share an XCD's
 // L2 (host side).
 // ===========================================================================
+#ifndef PQ_NO_WINDOWED
+#define PQ_NO_WINDOWED 0  // 1 (analysis variant): jobs past the run window go to expand_direct as before
+#endif
 constexpr int EX_WAVE = EX_WAVE_VALUES;       // values per wave
 constexpr int EX_ROW = 256;                   // values per row (4 per lane)
 constexpr int EX_ROWS = EX_WAVE / EX_ROW;     // rows per wave
@@ -5146,6 +5235,137 @@ __device__ __forceinline__ T sload(const T *p) {
 #pragma unroll
   for (int i = 0; i < (int)(sizeof(T) / 16); i++) u.v[i] = q[i];
   return u.t;
+}
+
+// A staged job whose runs do not fit the 64-lane window (run-heavy key
+// streams: SURVEY.md §8(d) C2's run-heavy variant, ~128 runs a job), row by
+// row: before each row of EX_ROW values the window is moved so that the row's
+// first run is lane 0 (one load, only when the row's runs leave the window),
+// then each value takes its run among the runs starting inside the row
+// (wave-uniform, as the general rows of expand_job), its key from the staged
+// bytes or the run's RLE value, a range check, the gather and the store.  A
+// row holding more run starts than the window (runs of one or two values)
+// goes to expand_direct.  (Inlined: as a call its frame took k_expand_mix<4>
+// from 73 VGPRs to 101 and 544 bytes of scratch a lane.)
+template <int WIDTH, bool LD>
+__device__ __forceinline__ void expand_windowed(const KArgs &a, const TileJob &tj, const ExRec &rc,
+                                             const PQ_LDS uint32_t *kspan, int64_t lbase, const PQ_LDS uint32_t *sdict) {
+  const int lane = lane_id();
+  const int32_t v0 = rc.v0, lim = rc.lim;
+  const int bw = rc.bw;
+  const uint32_t mask = bw >= 32 ? 0xffffffffu : ((1u << bw) - 1);
+  const int32_t end_bit32 = (int32_t)(((int64_t)rc.val_len - 1) * 8);
+  const uint32_t dsh = (uint32_t)((uintptr_t)rc.dict & 3);
+  const __amdgpu_buffer_rsrc_t dra = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)((uintptr_t)rc.dict & ~(uintptr_t)3), (short)0, (int)(rc.dict_n * (uint32_t)WIDTH + 12), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ors =
+      __builtin_amdgcn_make_buffer_rsrc((void *)tj.out, (short)0, (int)((uint32_t)lim * (uint32_t)WIDTH), 0x00020000);
+  const bool out_al = ((uintptr_t)tj.out & 15) == 0;
+  RunWin W;
+  W.load(rc.runs, rc.nr, rc.first_run);
+  for (int32_t rl = v0; rl < lim; rl += EX_ROW) {
+    const int32_t rh = min(rl + EX_ROW, lim);
+    int32_t ri = max((int32_t)__popcll(ballot(W.start <= rl)) - 1, 0);
+    if ((int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, 63) < rh) {  // the row's runs leave the window
+      W.load(rc.runs, rc.nr, W.wb + ri);
+      ri = 0;
+    }
+    if ((int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, 63) < rh) {  // > 62 run starts in the row
+      ExPage P;
+      P.nr = rc.nr;
+      P.bw = rc.bw;
+      P.val_len = rc.val_len;
+      P.dict_n = rc.dict_n;
+      P.vals = rc.vals;
+      P.dict = rc.dict;
+      P.runs = rc.runs;
+      expand_direct(a, P, tj.page, WIDTH, tj.out, rl, rh, W.wb + ri);
+      continue;
+    }
+    const int32_t j0 = rl + 4 * lane;
+    int32_t sq[4];
+    uint32_t pq[4], fq[4];
+    {
+      const int32_t s0 = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, ri);
+      const uint32_t p0 = __builtin_amdgcn_readlane(W.prm, ri), f0 = __builtin_amdgcn_readlane(W.rle, ri);
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        sq[q] = s0;
+        pq[q] = p0;
+        fq[q] = f0;
+      }
+      for (int x = ri + 1; x < 64; x++) {
+        const int32_t ns = (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, x);
+        if (ns >= rh) break;
+        const uint32_t px = __builtin_amdgcn_readlane(W.prm, x), fx = __builtin_amdgcn_readlane(W.rle, x);
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+          if (j0 + q >= ns) {
+            sq[q] = ns;
+            pq[q] = px;
+            fq[q] = fx;
+          }
+      }
+    }
+    uint32_t key[4];
+    bool bad = false;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int32_t j = j0 + q;
+      const bool act = j < lim;
+      const uint32_t pr = pq[q], fr = fq[q];
+      const int32_t bb = (int32_t)pr * 8 + (j - sq[q]) * bw;  // stream bit of the key (pages < 256 MiB)
+      const uint32_t lb = (fr || !act) ? 0u : (uint32_t)(bb - (int32_t)lbase);
+      const PQ_LDS uint32_t *dw = kspan + (lb >> 5);
+      uint32_t kv = __builtin_amdgcn_alignbit(dw[1], dw[0], lb & 31) & mask;
+      const int32_t avail = end_bit32 - bb;  // zero-fill past the stream end (hybrid_decoder.go:133-141)
+      kv &= avail >= bw ? 0xffffffffu : avail <= 0 ? 0u : ((1u << avail) - 1);
+      kv = fr ? pr : kv;
+      bad |= act && kv >= rc.dict_n;
+      key[q] = act && kv < rc.dict_n ? kv : 0u;
+    }
+    if (ballot(bad)) {
+      set_status(a.status, tj.page, ST_VALUES, E_DICT);  // type_dict.go:51-53
+      return;
+    }
+    typedef typename std::conditional<WIDTH == 4, uint32_t, uint64_t>::type VT;
+    VT val[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      if (LD) {
+        val[q] = WIDTH == 4 ? (VT)sdict[key[q]] : (VT)((const PQ_LDS uint64_t *)sdict)[key[q]];
+      } else if (WIDTH == 4) {
+        const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(dra, key[q] * 4, 0, 0);
+        val[q] = (VT)__builtin_amdgcn_alignbyte(x.y, x.x, dsh);
+      } else {
+        const u32x3 x = __builtin_amdgcn_raw_buffer_load_b96(dra, key[q] * 8, 0, 0);
+        val[q] = (VT)(((uint64_t)__builtin_amdgcn_alignbyte(x.z, x.y, dsh) << 32) | __builtin_amdgcn_alignbyte(x.y, x.x, dsh));
+      }
+    }
+    const uint32_t off = (uint32_t)j0 * (uint32_t)WIDTH;
+    if (j0 + 4 <= lim && out_al) {
+      if (WIDTH == 4) {
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u32x4{(uint32_t)val[0], (uint32_t)val[1], (uint32_t)val[2], (uint32_t)val[3]}, ors, off, 0, 0);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{(uint32_t)val[0], (uint32_t)((uint64_t)val[0] >> 32), (uint32_t)val[1],
+                                                     (uint32_t)((uint64_t)val[1] >> 32)},
+                                               ors, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{(uint32_t)val[2], (uint32_t)((uint64_t)val[2] >> 32), (uint32_t)val[3],
+                                                     (uint32_t)((uint64_t)val[3] >> 32)},
+                                               ors, off + 16, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        if (j0 + q >= lim) continue;
+        if (WIDTH == 4) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)val[q], ors, off + 4 * q, 0, 0);
+        else
+          __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)val[q], (uint32_t)((uint64_t)val[q] >> 32)}, ors,
+                                                off + 8 * q, 0, 0);
+      }
+    }
+  }
 }
 
 // One job (EX_WAVE values of one page) by one wave.  kspan: this wave's
@@ -5199,6 +5419,12 @@ __device__ __forceinline__ void expand_job(const KArgs &a, const TileJob &tj, co
   const bool fits = staged && (int32_t)__builtin_amdgcn_readlane((uint32_t)W.start, 63) >= lim;
   STAMP(2);
   if (!fits) {
+    if (staged && !PQ_NO_WINDOWED) {  // more runs than the window holds: row by row, the window moved along
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the staged bytes (LDS-DMA)
+      expand_windowed<WIDTH, LD>(a, tj, rc, (const PQ_LDS uint32_t *)kspan, (int64_t)(A - (uintptr_t)ks) * 8,
+                                 (const PQ_LDS uint32_t *)sdict);
+      return;
+    }
     for (int32_t c = v0; c < lim; c += 512)
       expand_direct(a, P, page, w, tj.out, c, min(c + 512, lim), a.tile_info[tj.tf + (c - v0) / RUN_TILE].x);
     return;
@@ -6250,8 +6476,9 @@ struct pq_launch_args {
   const int32_t *walk, *seg_base;
   int64_t *segs;
   uint32_t *seg_flag;
-  const int32_t *parts;  // k_decode<3>: (page, first level, end level) triplets instead of `list`
-  int32_t redo;          // k_decode<3>: decode again (whole) the pages whose parts failed
+  const int32_t *parts;  // k_decode<3> / <2>: (page, first level, end level) triplets instead of `list`
+  int32_t redo;          // k_decode<3> / <2>: decode again (whole) the pages whose parts failed
+  int64_t *str_pre;      // k_prepare -> k_decode<2> parts: string bytes before every 256 values of a page
   const int64_t *hjobs;
   int32_t nhjobs;
   int32_t grid_cap;  // k_levels<-1>: at most this many workgroups (grid-stride loop)
@@ -6313,6 +6540,7 @@ static pq::KArgs to_k(const pq_launch_args *p) {
   k.lgroups = (const pq::LdsGroup *)p->lgroups;
   k.parts = p->parts;
   k.redo = p->redo;
+  k.str_pre = p->str_pre;
   k.part_tab = p->part_tab;
   k.part_pre = p->part_pre;
   k.hjobs = p->hjobs;

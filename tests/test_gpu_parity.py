@@ -565,6 +565,33 @@ def test_nullable_dictionary_strings_staged(maxlen):
                    "nullable dict strings maxlen %d v%s" % (maxlen, ver))
 
 
+@pytest.mark.parametrize("maxlen", [12, 200])
+def test_string_page_parts(maxlen):
+    """Flat nullable dictionary-string pages of >= 8,192 entries run as
+    k_decode<2> parts of ~4,096 entries on the column's 256-slot grid: each
+    part counts the values before it from k_levels' bitmap, takes their string
+    bytes from k_prepare's per-256-value prefix table and seeks the key stream
+    (HybS::skip).  Row groups of 23,457 rows put every page's first slot off
+    the grid; stretches with no nulls, with every entry null, and mixed put
+    part starts on null and non-null entries; V1 and V2, Snappy and not.
+    Every buffer bit-exact against the oracle (offsets, bytes, validity)."""
+    pa = pytest.importorskip("pyarrow")
+    rng = np.random.default_rng(71 + maxlen)
+    rows = 70001
+    lens = rng.integers(0, maxlen + 1, 900)
+    vocab = ["".join(chr(97 + int(c)) for c in rng.integers(0, 26, n)) for n in lens]
+    words = [vocab[i] for i in rng.integers(0, len(vocab), rows)]
+    mask = rng.random(rows) < 0.2
+    mask[9000:15000] = True    # every entry null
+    mask[30000:41000] = False  # no nulls
+    mask[50000:50300] = True
+    t = pa.table({"s": pa.array(words, mask=mask), "r": pa.array(words, mask=rng.random(rows) < 0.01)})
+    for ver in ("1.0", "2.0"):
+        for comp in ("snappy", "none"):
+            check_file(_pq_bytes(t, compression=comp, row_group_size=23457, data_page_version=ver),
+                       "string parts maxlen %d v%s %s" % (maxlen, ver, comp))
+
+
 def _c5_bytes(tmp_path, rows, rg_rows, **kw):
     import synth
     path = str(tmp_path / "c5_small.parquet")
