@@ -178,7 +178,10 @@ enum { PQG_BUF_VALUES = 0, PQG_BUF_VALIDITY = 1, PQG_BUF_LIST_OFFSETS = 2, PQG_B
        PQG_BUF_STR_OFFSETS = 4, PQG_BUF_DEF = 5, PQG_BUF_REP = 6 };
 
 /* batch flags */
-enum { PQG_BATCH_LEVELS = 1 /* also emit raw def/rep levels */ };
+enum {
+  PQG_BATCH_LEVELS = 1,       /* also emit raw def/rep levels */
+  PQG_BATCH_HOST_INFLATE = 2  /* inflate GZIP pages with zlib on the host while planning (default: k_inflate on the GPU) */
+};
 
 typedef struct {
   int64_t pages, data_pages, dict_pages, snappy_pages, host_inflated_pages;
@@ -194,6 +197,8 @@ typedef struct {
    * (including a counting pass's launch, not its device time) */
   double create_plan_ms, create_alloc_ms, create_upload_ms, create_tables_ms;
   double upload_gather_ms, upload_wait_ms;
+  int64_t gzip_device_pages;  /* GZIP pages inflated on the GPU (k_inflate) */
+  int64_t gzip_in_bytes;      /* their compressed bytes */
 } pqg_batch_stats;
 
 int pqg_batch_create(pqg_ctx *ctx, pqg_file *f, int rg_begin, int rg_end, const int *leaves, int nleaves, int flags,

@@ -19,7 +19,8 @@ enum : uint8_t { PAGE_V1 = 0, PAGE_V2 = 1, PAGE_DICT = 2 };
 // Where the uncompressed values section of a page comes from.
 enum : uint8_t { BODY_RAW = 0,        // uncompressed: body == payload in the input buffer
                  BODY_SNAPPY = 1,     // snappy-decoded on the GPU into staging
-                 BODY_HOST = 2 };     // inflated on the host (gzip / user codec), uploaded into staging
+                 BODY_HOST = 2,       // inflated on the host (gzip / user codec), uploaded into staging
+                 BODY_GZIP = 3 };     // gzip-inflated on the GPU into staging (k_inflate, pq_inflate.hip)
 
 // Error "stages" in the reference's order of evaluation.  The reference reads
 // and initialises ALL pages of a chunk (phase 1, readPages chunk_reader.go:206)
@@ -135,6 +136,16 @@ struct SwRes {     // per page, k_sw_link -> k_prepare / k_dict_prepare / k_sw_e
   int32_t pad;
 };
 // k_reset: a device buffer zeroed at the start of every decode
+// k_inflate's arguments (pq_inflate.hip): the gzip pages, one wave each.
+struct InflateArgs {
+  const uint8_t *in;
+  uint8_t *stage;
+  const PageDesc *pages;
+  uint32_t *status;
+  const int32_t *list;
+  int32_t n;
+};
+
 struct ZeroRange {
   uint32_t *ptr;
   uint64_t words;

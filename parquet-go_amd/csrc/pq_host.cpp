@@ -99,6 +99,7 @@ struct pq_launch_args {
   int32_t n_sw_items, n_sw_pages, sw_page0;
 };
 int pq_launch(int which, const pq_launch_args *p, hipStream_t s);
+int pq_launch_inflate(const pq::InflateArgs *a, hipStream_t s);  // pq_inflate.hip
 extern int pq_launch_fail_which, pq_launch_fail_err;
 static constexpr int64_t kSnapSeg = 65536;  // pq_kernels.hip SNAP_SEG
 }
@@ -753,6 +754,8 @@ struct pqg_batch {
   std::vector<PageDesc> pages;
   std::vector<uint32_t> status0;  // host-side initial status per page
   std::vector<int32_t> snappy_list, dict_list, data_list;
+  std::vector<int32_t> gzip_list;  // gzip pages inflated by k_inflate (BODY_GZIP)
+  int32_t gz_off = 0;              // their position in d_lists
   // Snappy segments: pages longer than kSnapSeg are decoded by one wave per
   // 64 KiB segment (k_snappy_walk finds the segment starts)
   std::vector<int32_t> seg_base;      // per Snappy-list position (+1): first segment
@@ -778,6 +781,7 @@ struct pqg_batch {
   bool any_count = false;
   std::vector<ChunkError> chunk_errors;
   int64_t input_bytes = 0, staged_bytes = 0, h2d_bytes = 0, host_inflated = 0, dict_entries = 0;
+  int64_t gzip_in_bytes = 0;  // compressed bytes of the BODY_GZIP pages (k_inflate's input)
   int64_t literal_pages = 0;  // Snappy pages that are one literal, read in place (no k_snappy work)
   // Snappy pages that are only literals (snappy_literal_train): copied by
   // k_copy from the plan, (stream offset in d_in, offset in d_stage, length,
@@ -1654,7 +1658,7 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
       if (st == STATUS_OK) st = make_status(stage, (uint32_t)code);
     };
     const int64_t avail = (int64_t)f->len - w.payload;
-    bool needs_device_codec = false;
+    bool needs_device_codec = false, gz_dev = false;
     std::vector<int64_t> train;
     int64_t comp = 0, body = 0, lsize = 0;
     if (h.type == 2) {
@@ -1740,6 +1744,15 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
         }
       } else if (builtin && C.codec == PQG_CODEC_UNCOMPRESSED) {
         if (comp != body) fail(ST_DECOMPRESS, PQG_ERR_SIZE);
+      } else if (builtin && C.codec == PQG_CODEC_GZIP && !(B->flags & PQG_BATCH_HOST_INFLATE)) {
+        // gzip on the GPU: the member is uploaded as stored and k_inflate
+        // writes the body into staging (zlib's outcome, pq_inflate.hip)
+        d.body_src = BODY_GZIP;
+        d.body = (uint64_t)stage_off;
+        stage_off += ((body + 15) & ~15) + 16;
+        B->staged_bytes += body;
+        B->gzip_in_bytes += comp;
+        gz_dev = true;
       } else {
         // host codec (gzip / user-registered): inflate now, upload into staging
         std::vector<uint8_t> out((size_t)body + 1);
@@ -1770,6 +1783,7 @@ static int plan_chunk(pqg_batch *B, HostBuf &in, std::vector<std::pair<uint64_t,
     int32_t my_index = (int32_t)B->pages.size();
     B->pages.push_back(d);
     B->status0.push_back(st);
+    if (gz_dev) B->gzip_list.push_back(my_index);
     if (d.kind == PAGE_DICT) {
       dict_idx = my_index;
       if (L.physical_type == T_BYTE_ARRAY) {
@@ -2542,6 +2556,8 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     lists.insert(lists.end(), B->general_list.begin(), B->general_list.end());
     lists.insert(lists.end(), B->dba_list.begin(), B->dba_list.end());
     lists.insert(lists.end(), B->pstr_items.begin(), B->pstr_items.end());
+    B->gz_off = (int32_t)lists.size();
+    lists.insert(lists.end(), B->gzip_list.begin(), B->gzip_list.end());
     // the small tables: one host image (256-byte aligned entries; the
     // zero-initialised ones are zeros in it) and one copy instead of a
     // synchronous copy or memset each (tens of µs apiece)
@@ -2971,6 +2987,12 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     e |= pq_launch(lv_id, &al, LN.side[2]);  // k_levels<-1>: every level page
     hipEventRecord(LN.join[2], LN.side[2]);
   }
+  if (!B->gzip_list.empty()) {
+    // gzip pages (k_inflate, a wave each) before everything that reads a
+    // body: the Snappy phase's dictionary preparation forks after this
+    InflateArgs ia{B->d_in, B->d_stage, B->d_pages, a.status, B->d_lists + B->gz_off, (int32_t)B->gzip_list.size()};
+    if (pq_launch_inflate(&ia, s)) e |= 1;
+  }
   a.list = B->d_lists;
   a.nlist = ns;
   a.sitems = B->d_sitems;
@@ -3377,6 +3399,8 @@ int pqg_batch_stats_get(const pqg_batch *B, pqg_batch_stats *out, size_t size) {
   for (const PageDesc &pd : B->pages) o->dict_pages += pd.kind == PAGE_DICT;
   o->snappy_pages = (int64_t)B->snappy_list.size();
   o->host_inflated_pages = B->host_inflated;
+  o->gzip_device_pages = (int64_t)B->gzip_list.size();
+  o->gzip_in_bytes = B->gzip_in_bytes;
   o->staged_bytes = B->staged_bytes;
   o->h2d_bytes = B->h2d_bytes;
   o->create_plan_ms = B->create_ms[0];

@@ -48,6 +48,7 @@ ABI_VERSION = 2
 
 BUF_VALUES, BUF_VALIDITY, BUF_LIST_OFFSETS, BUF_LIST_VALIDITY, BUF_STR_OFFSETS, BUF_DEF, BUF_REP = range(7)
 BATCH_LEVELS = 1
+BATCH_HOST_INFLATE = 2
 
 # every symbol include/pqgpu.h declares (checked by tests/test_capi_symbols.py)
 EXPORTS = [
@@ -95,7 +96,8 @@ class BatchStats(ctypes.Structure):
                                               "host_inflated_pages", "input_bytes", "staged_bytes",
                                               "output_bytes", "h2d_bytes", "snappy_in_bytes", "dict_bytes")] + \
         [(n, ctypes.c_double) for n in ("create_plan_ms", "create_alloc_ms", "create_upload_ms", "create_tables_ms",
-                                        "upload_gather_ms", "upload_wait_ms")]
+                                        "upload_gather_ms", "upload_wait_ms")] + \
+        [(n, ctypes.c_int64) for n in ("gzip_device_pages", "gzip_in_bytes")]
 
 
 DECOMPRESS_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t,
