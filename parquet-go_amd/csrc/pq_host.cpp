@@ -2556,6 +2556,12 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     lists.insert(lists.end(), B->general_list.begin(), B->general_list.end());
     lists.insert(lists.end(), B->dba_list.begin(), B->dba_list.end());
     lists.insert(lists.end(), B->pstr_items.begin(), B->pstr_items.end());
+    // k_inflate: longest bodies first (a page is one wave's serial decode,
+    // so the launch ends with its longest page; started first, it overlaps
+    // the rest — c5gz's ~1 MiB l_comment pages came last in column order)
+    std::stable_sort(B->gzip_list.begin(), B->gzip_list.end(), [&](int32_t x, int32_t y) {
+      return B->pages[(size_t)x].body_len > B->pages[(size_t)y].body_len;
+    });
     B->gz_off = (int32_t)lists.size();
     lists.insert(lists.end(), B->gzip_list.begin(), B->gzip_list.end());
     // the small tables: one host image (256-byte aligned entries; the
@@ -2922,6 +2928,10 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   // pages, level / length scratch, job records and scanned bases it left are
   // this decode's (same epoch), so only the bitmaps are zeroed and the decode
   // phase runs
+  // launches are checked with hipGetLastError: drop an error an earlier API
+  // call left behind (e.g. a query's hipErrorNotReady), which is not this
+  // decode's
+  (void)hipGetLastError();
   const bool resume = !upto_scan && B->counted;
   B->counted = upto_scan;
   a.epoch = resume ? B->epoch : ++B->epoch;

@@ -100,7 +100,9 @@ struct Canon {
 // code-length code zlib's entry then reads as length 0, as here).  Returns
 // false for a rejected set.  Whole wave; LDS only.
 template <int K, int ROOT>
-__device__ bool build_table(const uint8_t *lens, int n, uint32_t *tab, uint16_t *sorted, Canon &cv) {
+__device__ __forceinline__ bool build_table(const uint8_t *lens, int n, uint32_t *tab, uint16_t *sorted, Canon &cv) {
+  // (per-length values live in VGPR lanes, lane l for length l, and the
+  // loops over lengths are not unrolled: the decoder's state stays in SGPRs)
   const int lane = lane_id();
   constexpr int ROWS = K == K_LENS ? 5 : 1;  // n <= 288, 32, 19
   uint32_t Lr[ROWS];
@@ -109,79 +111,68 @@ __device__ bool build_table(const uint8_t *lens, int n, uint32_t *tab, uint16_t 
     const int s = lane + 64 * r;
     Lr[r] = s < n ? (uint32_t)lens[s] : 0u;
   }
-  uint32_t cnt[16];
-  cnt[0] = 0;
-#pragma unroll
+  uint32_t cntv = 0;
+  int mx = 0;
+#pragma unroll 1
   for (int l = 1; l < 16; l++) {
     uint32_t c = 0;
 #pragma unroll
     for (int r = 0; r < ROWS; r++) c += (uint32_t)__builtin_popcountll(ballot(Lr[r] == (uint32_t)l));
-    cnt[l] = c;
+    c = ufirst(c);
+    if (c) mx = l;
+    if (lane == l) cntv = c;
   }
-  int mx = 0;
-#pragma unroll
-  for (int l = 1; l < 16; l++)
-    if (cnt[l]) mx = l;
   constexpr int NT = 1 << ROOT;
+  cv.cnt = 0;
+  cv.first = 0;
+  cv.offs = 0;
   if (mx == 0) {
     const uint32_t e = K == K_CODES ? ent(Y_SYM, 0, 1, 0) : ent(Y_BAD, 0, 1, 0);
     for (int j = lane; j < NT; j += 64) tab[j] = e;
-    cv.cnt = 0;
-    cv.first = 0;
-    cv.offs = 0;
     __syncthreads();
     return true;
   }
   int left = 1;
-#pragma unroll
+  uint32_t code = 0, o = 0, prevc = 0;
+#pragma unroll 1
   for (int l = 1; l < 16; l++) {
-    left <<= 1;
-    left -= (int)cnt[l];
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cntv, l);
+    left = (left << 1) - (int)c;
     if (left < 0) return false;  // over-subscribed
+    code = (code + prevc) << 1;
+    if (lane == l) {
+      cv.first = code;
+      cv.offs = o;
+    }
+    o += c;
+    prevc = c;
   }
   if (left > 0 && (K == K_CODES || mx != 1)) return false;  // incomplete
-  uint32_t first[16], offs[16], base[16];
-  {
-    uint32_t code = 0, o = 0;
-#pragma unroll
-    for (int l = 1; l < 16; l++) {
-      code = (code + cnt[l - 1]) << 1;
-      first[l] = code;
-      offs[l] = o;
-      o += cnt[l];
-      base[l] = 0;
-    }
-  }
-  cv.cnt = 0;
-  cv.first = 0;
-  cv.offs = 0;
-#pragma unroll
-  for (int l = 1; l < 16; l++)
-    if (lane == l) {
-      cv.cnt = cnt[l];
-      cv.first = first[l];
-      cv.offs = offs[l];
-    }
+  cv.cnt = cntv;
   if (left > 0) {  // the one unused 1-bit code: invalid, 1 bit
     for (int j = lane; j < NT; j += 64) tab[j] = ent(Y_BAD, 0, 1, 0);
   }
+  uint32_t basev = 0;  // lane l: symbols of length l ranked so far
 #pragma unroll
   for (int r = 0; r < ROWS; r++) {
     const uint32_t L = Lr[r];
     const uint32_t s = (uint32_t)(lane + 64 * r);
-    uint32_t code = 0;
-#pragma unroll
+    uint32_t scode = 0;
+#pragma unroll 1
     for (int l = 1; l < 16; l++) {
       const uint64_t m = ballot(L == (uint32_t)l);
-      if (L == (uint32_t)l) {
-        const uint32_t rank = base[l] + (uint32_t)rank_in(m);
-        code = first[l] + rank;
-        sorted[offs[l] + rank] = (uint16_t)s;
+      if (m) {
+        const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)basev, l);
+        if (L == (uint32_t)l) {
+          const uint32_t rank = base + (uint32_t)rank_in(m);
+          scode = (uint32_t)__builtin_amdgcn_readlane((int)cv.first, l) + rank;
+          sorted[(uint32_t)__builtin_amdgcn_readlane((int)cv.offs, l) + rank] = (uint16_t)s;
+        }
+        if (lane == l) basev = base + (uint32_t)__builtin_popcountll(m);
       }
-      base[l] += (uint32_t)__builtin_popcountll(m);
     }
     if (L != 0) {
-      const uint32_t rev = __builtin_bitreverse32(code) >> (32 - L);
+      const uint32_t rev = __builtin_bitreverse32(scode) >> (32 - L);
       if (L <= (uint32_t)ROOT) {
         const uint32_t e = sym_entry<K>(s, L);
         for (uint32_t j = rev; j < (uint32_t)NT; j += 1u << L) tab[j] = e;
@@ -200,6 +191,7 @@ __device__ bool build_table(const uint8_t *lens, int n, uint32_t *tab, uint16_t 
 template <int K, int ROOT>
 __device__ __forceinline__ uint32_t slow_decode(uint64_t bb, const uint16_t *sorted, const Canon &cv) {
   uint32_t code = __builtin_bitreverse32((uint32_t)bb & ((1u << ROOT) - 1)) >> (32 - ROOT);
+#pragma unroll 1
   for (int L = ROOT + 1; L < 16; L++) {
     code = (code << 1) | (uint32_t)((bb >> (L - 1)) & 1u);
     const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cv.cnt, L);
@@ -246,42 +238,100 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
   return v;
 }
 
-// The page's compressed bytes through two 256-byte register windows (4 bytes
-// a lane): the next window is loaded when the decoder enters the current one,
-// so a refill is two v_readlane, never a load wait.  Offsets are relative to
-// p0, the page start rounded down to 4 bytes; windows may read up to 512
-// bytes past the page (the input buffer's 4 KiB readable slack covers the end).
-struct GzIn {
+// The page's compressed bytes through 256-byte register windows (4 bytes a
+// lane; window k = bytes [256 k, 256 k + 256) from p0, the page start rounded
+// down to 4 bytes): c holds the current window, x the next, and p the one
+// after is in flight — entering a window moves x and p down (p was issued a
+// whole window earlier, so the move's wait is normally already met) and
+// issues the next load.  Windows may read up to 768 bytes past the page: the
+// input buffer's 4 KiB readable slack covers the end.
+//
+// The bit reader on top (RFC 1951 3.1.1: bits from the least significant
+// end) keeps 33..64 bits in bb; a refill inside the current window is two
+// v_readlane and a 64-bit funnel shift.  All of it is wave-uniform (SGPRs).
+struct Bits {
   const uint32_t *p0;
-  int64_t wb;  // window base (multiple of 256)
-  uint32_t w0, w1;
-  __device__ __forceinline__ void at(int64_t base) {
-    wb = base;
-    w0 = p0[(wb >> 2) + lane_id()];
-    w1 = p0[(wb >> 2) + 64 + lane_id()];
+  int s0, n;        // page start's offset in its aligned word; compressed length
+  int kc, base;     // current window, its first byte (256 kc)
+  uint32_t c, x, p;
+  uint64_t bb = 0;  // bits not yet consumed (zeros above nb)
+  int nb = 0;
+  int ip = 0;       // next stream byte not yet in bb
+  __device__ __forceinline__ uint32_t load(int k) { return p0[k * 64 + lane_id()]; }
+  __device__ __forceinline__ void at(int k) {
+    kc = k;
+    base = k << 8;
+    c = load(k);
+    x = load(k + 1);
+    p = load(k + 2);
   }
-  __device__ __forceinline__ uint32_t u32(int64_t o) {  // bytes [o, o + 4), o >= 0
-    int64_t d = o - wb;
-    if (d >= 256) {
-      if (d < 512) {
-        wb += 256;
-        w0 = w1;
-        w1 = p0[(wb >> 2) + 64 + lane_id()];
+  __device__ __forceinline__ uint32_t u32_far(int pos) {  // any pos (window moves)
+    const int k = pos >> 8;
+    if (k != kc) {
+      if (k == kc + 1) {
+        c = x;
+        x = p;
+        p = load(k + 2);
+        kc = k;
+        base = k << 8;
       } else {
-        at(o & ~(int64_t)255);
+        at(k);
       }
-      d = o - wb;
-    } else if (d < 0) {
-      at(o & ~(int64_t)255);
-      d = o - wb;
     }
-    const int i = (int)(d >> 2), sh = (int)(d & 3) * 8;
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)w0, i);
-    const uint32_t hi = i < 63 ? (uint32_t)__builtin_amdgcn_readlane((int)w0, i + 1)
-                               : (uint32_t)__builtin_amdgcn_readlane((int)w1, 0);
-    return sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
+    const int w = (pos - base) >> 2;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)c, w);
+    const uint32_t hi = w < 63 ? (uint32_t)__builtin_amdgcn_readlane((int)c, w + 1)
+                               : (uint32_t)__builtin_amdgcn_readlane((int)x, 0);
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> ((pos & 3) * 8));
   }
+  __device__ __forceinline__ uint32_t u32(int pos) {  // bytes [pos, pos + 4) from p0
+    const uint32_t rel = (uint32_t)(pos - base);
+    if (rel < 252u) {
+      const int w = (int)(rel >> 2);
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)c, w);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)c, w + 1);
+      return (uint32_t)((((uint64_t)hi << 32) | lo) >> ((pos & 3) * 8));
+    }
+    return u32_far(pos);
+  }
+  __device__ __forceinline__ void refill() {
+    if (nb <= 32) {
+      if (ip + 4 <= n) {
+        bb |= (uint64_t)u32(ip + s0) << nb;
+        ip += 4;
+        nb += 32;
+      } else {
+        while (ip < n && nb <= 56) {
+          bb |= (uint64_t)(u32(ip + s0) & 0xffu) << nb;
+          ip++;
+          nb += 8;
+        }
+      }
+    }
+  }
+  __device__ __forceinline__ uint32_t take(int k) {  // k <= nb, k <= 32
+    const uint32_t v = (uint32_t)bb & (uint32_t)((1ull << k) - 1);
+    bb >>= k;
+    nb -= k;
+    return v;
+  }
+  __device__ __forceinline__ uint32_t byte_at(int i) { return u32(i + s0) & 0xffu; }
 };
+
+// [f, f + 1024) from the ring to staging, and its CRC-32 folded into crc
+__device__ __forceinline__ void flush(const uint8_t *ring, uint8_t *dst, int lane, int &f, uint32_t &crc,
+                                      uint32_t x_lane, uint32_t x_flush) {
+  const uint4 v = *(const uint4 *)&ring[(f + lane * 16) & (GZ_RING - 1)];
+  *(uint4 *)(dst + f + lane * 16) = v;
+  uint32_t c = 0xffffffffu;
+  c = crc_bytes(c, v.x, 4);
+  c = crc_bytes(c, v.y, 4);
+  c = crc_bytes(c, v.z, 4);
+  c = crc_bytes(c, v.w, 4);
+  const uint32_t part = wave_xor(multmodp(x_lane, ~c));
+  crc = multmodp(x_flush, crc) ^ ufirst(part);
+  f += GZ_FLUSH;
+}
 
 // Fixed Huffman code lengths (RFC 1951 3.2.6): literal/length 0-143: 8,
 // 144-255: 9, 256-279: 7, 280-287: 8; distance 0-31: 5.
@@ -299,133 +349,109 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs a) {
   const int page = (int)ufirst((uint32_t)a.list[blockIdx.x]);
   const PageDesc d = a.pages[page];
   if (ufirst(__atomic_load_n(&a.status[page], __ATOMIC_RELAXED)) < make_status(ST_DECOMPRESS, 0)) return;
-  const int64_t lsize = d.kind == PAGE_V2 ? (int64_t)d.v2_rep_len + d.v2_def_len : 0;
-  const uint8_t *src = a.in + d.src + lsize;
-  const int64_t n = d.comp_len;
-  uint8_t *dst = a.stage + d.body;
-  const int64_t cap = d.body_len;
-  const int64_t s0 = (int64_t)((uintptr_t)src & 3);
-  GzIn in;
-  in.p0 = (const uint32_t *)(src - s0);
-  in.at(0);
-  // bit reader (RFC 1951 3.1.1: bits from the least significant end)
-  uint64_t bb = 0;
-  int nb = 0;
-  int64_t ip = 0;  // next stream byte not yet in bb
-  auto refill = [&]() {
-    if (nb <= 32) {
-      if (ip + 4 <= n) {
-        bb |= (uint64_t)in.u32(ip + s0) << nb;
-        ip += 4;
-        nb += 32;
-      } else {
-        while (ip < n && nb <= 56) {
-          bb |= (uint64_t)(in.u32(ip + s0) & 0xffu) << nb;
-          ip++;
-          nb += 8;
-        }
-      }
-    }
-  };
-  auto take = [&](int k) -> uint32_t {  // k <= nb, k <= 32
-    const uint32_t v = (uint32_t)bb & (uint32_t)((1ull << k) - 1);
-    bb >>= k;
-    nb -= k;
-    return v;
-  };
-  auto byte_at = [&](int64_t i) -> uint32_t { return in.u32(i + s0) & 0xffu; };
+  // (every field read into SGPRs: a uniform value left in a VGPR drags the
+  // whole decoder's scalar state into VALU code)
+  const int64_t lsize = ufirst(d.kind) == PAGE_V2 ? (int64_t)(int32_t)ufirst((uint32_t)d.v2_rep_len) +
+                                                         (int64_t)(int32_t)ufirst((uint32_t)d.v2_def_len)
+                                                   : 0;
+  const uint8_t *src = a.in + (uint64_t)ufirst64((int64_t)d.src) + lsize;
+  const int n = (int32_t)ufirst((uint32_t)d.comp_len);
+  uint8_t *dst = a.stage + (uint64_t)ufirst64((int64_t)d.body);
+  const int cap = (int32_t)ufirst((uint32_t)d.body_len);
+  const int s0 = (int)((uintptr_t)src & 3);
+  Bits R;
+  R.p0 = (const uint32_t *)(src - s0);
+  R.s0 = s0;
+  R.n = n;
+  R.at(0);
 
   uint32_t err = 0;
   // ---- gzip header (RFC 1952 2.3.1; zlib inflate.c HEAD .. HCRC) ----
-  int64_t p = 0;
+  int p = 0;
   uint32_t flg = 0;
   do {
     if (n < 2) { err = E_SIZE; break; }
-    if (byte_at(0) != 0x1f || byte_at(1) != 0x8b) { err = E_CODEC; break; }
+    if (R.byte_at(0) != 0x1f || R.byte_at(1) != 0x8b) { err = E_CODEC; break; }
     if (n < 4) { err = E_SIZE; break; }
-    if (byte_at(2) != 8) { err = E_CODEC; break; }
-    flg = byte_at(3);
+    if (R.byte_at(2) != 8) { err = E_CODEC; break; }
+    flg = R.byte_at(3);
     if (flg & 0xe0) { err = E_CODEC; break; }
     p = 10;  // MTIME, XFL, OS
     if (n < p) { err = E_SIZE; break; }
     if (flg & 4) {  // FEXTRA
       if (n < p + 2) { err = E_SIZE; break; }
-      const int64_t xlen = (int64_t)(byte_at(p) | byte_at(p + 1) << 8);
+      const int xlen = (int)(R.byte_at(p) | R.byte_at(p + 1) << 8);
       p += 2 + xlen;
       if (n < p) { err = E_SIZE; break; }
     }
-    for (uint32_t f = 8; f <= 16 && !err; f <<= 1) {  // FNAME, FCOMMENT: zero-terminated
-      if (!(flg & f)) continue;
+    for (uint32_t fl = 8; fl <= 16 && !err; fl <<= 1) {  // FNAME, FCOMMENT: zero-terminated
+      if (!(flg & fl)) continue;
       for (;;) {
         if (p >= n) { err = E_SIZE; break; }
-        if (byte_at(p++) == 0) break;
+        if (R.byte_at(p++) == 0) break;
       }
     }
     if (err) break;
     if (flg & 2) {  // FHCRC: low 16 bits of the CRC-32 of the header bytes so far
       if (n < p + 2) { err = E_SIZE; break; }
       uint32_t c = 0xffffffffu;
-      for (int64_t i = 0; i < p; i++) c = crc_bytes(c, byte_at(i), 1);
+      for (int i = 0; i < p; i++) c = crc_bytes(c, R.byte_at(i), 1);
       c = ~c;
-      if ((c & 0xffffu) != (byte_at(p) | byte_at(p + 1) << 8)) { err = E_CODEC; break; }
+      if ((c & 0xffffu) != (R.byte_at(p) | R.byte_at(p + 1) << 8)) { err = E_CODEC; break; }
       p += 2;
     }
   } while (0);
-  ip = p;
+  R.ip = p;
 
   // CRC shift of this lane's 16 bytes inside a 1 KiB flush, and of a flush
   const uint32_t x_lane = x8n((uint32_t)(16 * (63 - lane)));
   const uint32_t x_flush = x8n(GZ_FLUSH);
   uint32_t crc = 0;  // CRC-32 of the flushed bytes
-  int64_t o = 0, f = 0;
-  auto flush = [&]() {  // [f, f + 1024) from the ring to staging
-    const uint4 v = *(const uint4 *)&S.ring[(f + lane * 16) & (GZ_RING - 1)];
-    *(uint4 *)(dst + f + lane * 16) = v;
-    uint32_t c = 0xffffffffu;
-    c = crc_bytes(c, v.x, 4);
-    c = crc_bytes(c, v.y, 4);
-    c = crc_bytes(c, v.z, 4);
-    c = crc_bytes(c, v.w, 4);
-    const uint32_t part = wave_xor(multmodp(x_lane, ~c));
-    crc = multmodp(x_flush, crc) ^ ufirst(part);
-    f += GZ_FLUSH;
+  int o = 0, f = 0;
+  // literals not yet in the ring: lane i holds the byte of position o - q + i
+  uint32_t lbuf = 0;
+  int q = 0;
+  auto put_lits = [&]() {
+    if (lane < q) S.ring[(o - q + lane) & (GZ_RING - 1)] = (uint8_t)lbuf;
+    q = 0;
   };
 
   bool last = false;
-  int tabs = 0;  // tables in LDS: 0 none, 1 fixed, 2 dynamic
+  int tabs = 0;  // tables built: 0 none, 1 fixed, 2 dynamic
   Canon lcv{0, 0, 0}, dcv{0, 0, 0};
+  // the root tables in VGPRs (entry i: lane i & 63 of register i >> 6): a
+  // lookup is s_set_gpr_idx + v_readlane, no LDS round trip
+  uint32_t ltv[1 << (GZ_LB - 6)], dtv[1 << (GZ_DB - 6)];
   while (!err && !last) {
     // ---- block header (RFC 1951 3.2.3) ----
-    refill();
-    if (nb < 3) { err = E_SIZE; break; }
-    last = take(1) != 0;
-    const uint32_t type = take(2);
+    R.refill();
+    if (R.nb < 3) { err = E_SIZE; break; }
+    last = R.take(1) != 0;
+    const uint32_t type = R.take(2);
     if (type == 3) { err = E_CODEC; break; }
     if (type == 0) {  // stored (3.2.4)
-      take(nb & 7);
-      refill();
-      if (nb < 32) { err = E_SIZE; break; }
-      const uint32_t w = take(32);
+      R.take(R.nb & 7);
+      R.refill();
+      if (R.nb < 32) { err = E_SIZE; break; }
+      const uint32_t w = R.take(32);
       if ((w & 0xffffu) != ((w >> 16) ^ 0xffffu)) { err = E_CODEC; break; }
-      int64_t len = w & 0xffffu;
-      ip -= nb >> 3;  // unread the whole bytes still in the bit buffer
-      bb = 0;
-      nb = 0;
+      int len = (int)(w & 0xffffu);
+      R.ip -= R.nb >> 3;  // unread the whole bytes still in the bit buffer
+      R.bb = 0;
+      R.nb = 0;
       if (len == 0) continue;
-      if (o >= cap || ip >= n) { err = E_SIZE; break; }
-      const bool fits = ip + len <= n && o + len <= cap;
-      if (!fits) { err = E_SIZE; break; }  // (zlib copies what fits, then Z_BUF_ERROR)
+      if (R.ip + len > n || o + len > cap) { err = E_SIZE; break; }  // (zlib copies what fits, then Z_BUF_ERROR)
       while (len > 0) {
-        const int64_t k = len < GZ_FLUSH ? len : GZ_FLUSH;
+        const int k = len < GZ_FLUSH ? len : GZ_FLUSH;
 #pragma unroll
-        for (int q = 0; q < 16; q++) {
-          const int64_t j = (int64_t)lane * 16 + q;
-          if (j < k) S.ring[(o + j) & (GZ_RING - 1)] = src[ip + j];
+        for (int t = 0; t < 16; t++) {
+          const int j = lane * 16 + t;
+          if (j < k) S.ring[(o + j) & (GZ_RING - 1)] = src[R.ip + j];
         }
         o += k;
-        ip += k;
+        R.ip += k;
         len -= k;
-        while (o - f >= GZ_FLUSH) flush();
+        while (o - f >= GZ_FLUSH) flush(S.ring, dst, lane, f, crc, x_lane, x_flush);
       }
       continue;
     }
@@ -434,20 +460,24 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs a) {
         fixed_lens(S.lens);
         build_table<K_LENS, GZ_LB>(S.lens, 288, S.lt, S.lsorted, lcv);
         build_table<K_DISTS, GZ_DB>(S.lens + 288, 32, S.dt, S.dsorted, dcv);
+#pragma unroll
+        for (int j = 0; j < (1 << (GZ_LB - 6)); j++) ltv[j] = S.lt[j * 64 + lane];
+#pragma unroll
+        for (int j = 0; j < (1 << (GZ_DB - 6)); j++) dtv[j] = S.dt[j * 64 + lane];
         tabs = 1;
       }
     } else {  // dynamic codes (3.2.7)
       tabs = 2;
-      refill();
-      if (nb < 14) { err = E_SIZE; break; }
-      const int nlen = (int)take(5) + 257, ndist = (int)take(5) + 1, ncode = (int)take(4) + 4;
+      R.refill();
+      if (R.nb < 14) { err = E_SIZE; break; }
+      const int nlen = (int)R.take(5) + 257, ndist = (int)R.take(5) + 1, ncode = (int)R.take(4) + 4;
       if (nlen > 286 || ndist > 30) { err = E_CODEC; break; }
       // the code-length code's lengths, in the order of 3.2.7
       uint32_t cl = 0;  // length of order position `lane` (lanes 0..18)
       for (int i = 0; i < ncode; i++) {
-        refill();
-        if (nb < 3) { err = E_SIZE; break; }
-        const uint32_t v = take(3);
+        R.refill();
+        if (R.nb < 3) { err = E_SIZE; break; }
+        const uint32_t v = R.take(3);
         if (lane == i) cl = v;
       }
       if (err) break;
@@ -480,24 +510,24 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs a) {
       uint32_t prev = 0;
       __syncthreads();
       while (have < total) {
-        refill();
-        const uint32_t e = ufirst(S.dt[(uint32_t)bb & 127u]);
+        R.refill();
+        const uint32_t e = ufirst(S.dt[(uint32_t)R.bb & 127u]);
         const int L = (int)e_bits(e);
-        if (L > nb) { err = E_SIZE; break; }
+        if (L > R.nb) { err = E_SIZE; break; }
         const uint32_t sym = e_val(e);
         if (sym < 16) {
-          take(L);
+          R.take(L);
           if (lane == 0) S.lens[have] = (uint8_t)sym;
           have++;
           prev = sym;
           continue;
         }
         const int xb = sym == 16 ? 2 : sym == 17 ? 3 : 7;
-        if (L + xb > nb) { err = E_SIZE; break; }
-        take(L);
+        if (L + xb > R.nb) { err = E_SIZE; break; }
+        R.take(L);
         if (sym == 16 && have == 0) { err = E_CODEC; break; }
         const uint32_t v = sym == 16 ? prev : 0u;
-        const int rep = (sym == 16 ? 3 : sym == 17 ? 3 : 11) + (int)take(xb);
+        const int rep = (sym == 16 ? 3 : sym == 17 ? 3 : 11) + (int)R.take(xb);
         if (have + rep > total) { err = E_CODEC; break; }
         for (int j = lane; j < rep; j += 64) S.lens[have + j] = (uint8_t)v;
         have += rep;
@@ -508,82 +538,115 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs a) {
       if (ufirst(S.lens[256]) == 0) { err = E_CODEC; break; }  // no end-of-block code
       if (!build_table<K_LENS, GZ_LB>(S.lens, nlen, S.lt, S.lsorted, lcv)) { err = E_CODEC; break; }
       if (!build_table<K_DISTS, GZ_DB>(S.lens + nlen, ndist, S.dt, S.dsorted, dcv)) { err = E_CODEC; break; }
+#pragma unroll
+      for (int j = 0; j < (1 << (GZ_LB - 6)); j++) ltv[j] = S.lt[j * 64 + lane];
+#pragma unroll
+      for (int j = 0; j < (1 << (GZ_DB - 6)); j++) dtv[j] = S.dt[j * 64 + lane];
     }
     // ---- Huffman-coded data (3.2.5; zlib LEN .. MATCH) ----
     for (;;) {
-      refill();
-      uint32_t e = ufirst(S.lt[(uint32_t)bb & ((1u << GZ_LB) - 1)]);
-      if (e_kind(e) == Y_SLOW) e = slow_decode<K_LENS, GZ_LB>(bb, S.lsorted, lcv);
+      // literals in a tight loop (one exit, no stores: a literal goes to its
+      // lane of lbuf); anything else — a length or end-of-block code, a code
+      // past the root table, missing bits, a full output, a full lbuf, a
+      // flush due — leaves it, undecoded, for the general path below
+      // (e >> 16 is a literal's code length, and >= 256 for any other
+      // kind, so one compare against nb catches both; lim folds the output
+      // limit, a full lbuf and a flush due into one bound on o)
+      uint32_t e;
+      {
+        const int lim = (int)ufirst((uint32_t)min(cap, min(f + GZ_FLUSH, o - q + 64)));
+        for (;;) {
+          R.refill();
+          const uint32_t li = (uint32_t)R.bb & ((1u << GZ_LB) - 1);
+          e = (uint32_t)__builtin_amdgcn_readlane((int)ltv[li >> 6], (int)(li & 63));
+          const int L = (int)(e >> 16);
+          if (L > R.nb || o >= lim) break;
+          R.bb >>= L;
+          R.nb -= L;
+          lbuf = lane == q ? (e & 0xffu) : lbuf;
+          q++;
+          o++;
+        }
+      }
+      if (q == 64 || o - f >= GZ_FLUSH) {
+        put_lits();
+        if (o - f >= GZ_FLUSH) flush(S.ring, dst, lane, f, crc, x_lane, x_flush);
+        continue;
+      }
+      if (e_kind(e) == Y_SLOW) e = slow_decode<K_LENS, GZ_LB>(R.bb, S.lsorted, lcv);
       const int L = (int)e_bits(e);
-      if (L > nb) { err = E_SIZE; break; }
-      take(L);
+      if (L > R.nb) { err = E_SIZE; break; }
+      R.take(L);
       const uint32_t kind = e_kind(e);
-      if (kind == Y_LIT) {
+      if (kind == Y_LIT) {  // (q < 64 and no flush due here: the tight loop handled those)
         if (o >= cap) { err = E_SIZE; break; }
-        if (lane == 0) S.ring[o & (GZ_RING - 1)] = (uint8_t)e_val(e);
+        lbuf = lane == q ? e_val(e) : lbuf;
+        q++;
         o++;
-        if (o - f >= GZ_FLUSH) flush();
         continue;
       }
       if (kind == Y_EOB) break;
       if (kind != Y_SYM) { err = E_CODEC; break; }  // 286 / 287, an unused code
       const int lx = (int)e_extra(e);
-      if (lx > nb) { err = E_SIZE; break; }
-      const int64_t len = (int64_t)e_val(e) + take(lx);
-      refill();
-      uint32_t g = ufirst(S.dt[(uint32_t)bb & ((1u << GZ_DB) - 1)]);
-      if (e_kind(g) == Y_SLOW) g = slow_decode<K_DISTS, GZ_DB>(bb, S.dsorted, dcv);
+      if (lx > R.nb) { err = E_SIZE; break; }
+      const int len = (int)e_val(e) + (int)R.take(lx);
+      R.refill();
+      const uint32_t di = (uint32_t)R.bb & ((1u << GZ_DB) - 1);
+      uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)dtv[di >> 6], (int)(di & 63));
+      if (e_kind(g) == Y_SLOW) g = slow_decode<K_DISTS, GZ_DB>(R.bb, S.dsorted, dcv);
       const int dL = (int)e_bits(g);
-      if (dL > nb) { err = E_SIZE; break; }
-      take(dL);
+      if (dL > R.nb) { err = E_SIZE; break; }
+      R.take(dL);
       if (e_kind(g) != Y_SYM) { err = E_CODEC; break; }  // 30 / 31, an unused code
       const int dx = (int)e_extra(g);
-      if (dx > nb) { err = E_SIZE; break; }
-      const int64_t dist = (int64_t)e_val(g) + take(dx);
-      if (o >= cap) { err = E_SIZE; break; }            // MATCH: no room left
-      if (dist > o) { err = E_CODEC; break; }     // too far back
-      if (o + len > cap) { err = E_SIZE; break; }       // partial copy, then no room
+      if (dx > R.nb) { err = E_SIZE; break; }
+      const int dist = (int)e_val(g) + (int)R.take(dx);
+      if (o >= cap) { err = E_SIZE; break; }        // MATCH: no room left
+      if (dist > o) { err = E_CODEC; break; }       // too far back
+      if (o + len > cap) { err = E_SIZE; break; }   // partial copy, then no room
+      put_lits();
       // the copy, 64 bytes a step: sources [o - dist, o) (periodic when dist < len)
-      for (int64_t k0 = 0; k0 < len; k0 += 64) {
-        const int64_t k = k0 + lane;
+      for (int k0 = 0; k0 < len; k0 += 64) {
+        const int k = k0 + lane;
         if (k < len) {
-          const int64_t sp = o - dist + (dist >= len ? k : (int64_t)((uint32_t)k % (uint32_t)dist));
+          const int sp = o - dist + (dist >= len ? k : (int)((uint32_t)k % (uint32_t)dist));
           const uint8_t b = S.ring[sp & (GZ_RING - 1)];
           S.ring[(o + k) & (GZ_RING - 1)] = b;
         }
       }
       o += len;
-      if (o - f >= GZ_FLUSH) flush();
+      if (o - f >= GZ_FLUSH) flush(S.ring, dst, lane, f, crc, x_lane, x_flush);
     }
+    put_lits();
   }
   if (!err) {
     // the last partial flush and the CRC of the whole output
-    const int64_t r = o - f;  // < 1024
-    const int64_t j0 = f + (int64_t)lane * 16;
-    const int64_t k = r - (int64_t)lane * 16 > 16 ? 16 : (r - (int64_t)lane * 16 > 0 ? r - (int64_t)lane * 16 : 0);
+    const int r = o - f;  // < 1024
+    const int j0 = f + lane * 16;
+    const int k = r - lane * 16 > 16 ? 16 : (r - lane * 16 > 0 ? r - lane * 16 : 0);
     uint32_t c = 0xffffffffu;
-    for (int64_t q = 0; q < k; q++) {
-      const uint8_t b = S.ring[(j0 + q) & (GZ_RING - 1)];
-      dst[j0 + q] = b;
+    for (int t = 0; t < k; t++) {
+      const uint8_t b = S.ring[(j0 + t) & (GZ_RING - 1)];
+      dst[j0 + t] = b;
       c = crc_bytes(c, b, 1);
     }
-    const int64_t after = r - (int64_t)lane * 16 - k;  // bytes after this lane's piece
+    const int after = r - lane * 16 - k;  // bytes after this lane's piece
     const uint32_t mine = k > 0 ? multmodp(x8n((uint32_t)(after > 0 ? after : 0)), ~c) : 0u;
     crc = multmodp(x8n((uint32_t)r), crc) ^ ufirst(wave_xor(mine));
     // trailer (RFC 1952 2.3.1: CRC32, ISIZE; zlib CHECK, LENGTH)
-    take(nb & 7);
-    ip -= nb >> 3;
-    bb = 0;
-    nb = 0;
-    if (ip + 4 > n) {
+    R.take(R.nb & 7);
+    R.ip -= R.nb >> 3;
+    R.bb = 0;
+    R.nb = 0;
+    if (R.ip + 4 > n) {
       err = E_SIZE;
     } else {
-      const uint32_t want = in.u32(ip + s0);
+      const uint32_t want = R.u32(R.ip + s0);
       if (want != crc) {
         err = E_CODEC;
-      } else if (ip + 8 > n) {
+      } else if (R.ip + 8 > n) {
         err = E_SIZE;
-      } else if (in.u32(ip + 4 + s0) != (uint32_t)o) {
+      } else if (R.u32(R.ip + 4 + s0) != (uint32_t)o) {
         err = E_CODEC;
       } else if (o != cap) {
         err = E_SIZE;  // newBlockReader's size check (compress.go:116-118)
@@ -596,8 +659,14 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs a) {
 }  // namespace
 }  // namespace pq
 
+extern "C" int pq_launch_fail_which, pq_launch_fail_err;  // pq_kernels.hip
+
 extern "C" int pq_launch_inflate(const pq::InflateArgs *a, hipStream_t s) {
   if (a->n <= 0) return 0;
   hipLaunchKernelGGL(pq::k_inflate, dim3((unsigned)a->n), dim3(64), 0, s, *a);
-  return hipGetLastError() == hipSuccess ? 0 : 1;
+  const hipError_t e = hipGetLastError();
+  if (e == hipSuccess) return 0;
+  pq_launch_fail_which = 40;  // (launch id of k_inflate in error messages)
+  pq_launch_fail_err = (int)e;
+  return 17;
 }

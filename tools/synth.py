@@ -11,6 +11,7 @@ analysis tools import this; the decoder never does.
   c3  DELTA_BINARY_PACKED INT64 ts + optional DOUBLE, V2, Snappy    (configs[2])
   c4  LIST<INT32> + dictionary STRING with rep/def levels, V1       (configs[3])
   c5  TPC-H lineitem-shaped, 16 columns, Snappy, V1                 (configs[4])
+  c5gz    C5's columns under GZIP (the k_inflate measurement, tools/gzip_ab.py)
 """
 import os
 import sys
@@ -26,6 +27,7 @@ DEFAULTS = {
     "c3": (100_000_000, 1 << 20),
     "c4": (20_000_000, 1 << 20),
     "c5": (45_300_000, 1_415_625),
+    "c5gz": (5_662_500, 707_813),
 }
 
 DESCR = {
@@ -36,9 +38,11 @@ DESCR = {
     "c3": "C3: DELTA_BINARY_PACKED INT64 ts + optional DOUBLE (10%% nulls), V2, Snappy, %d rows, %d-row row groups",
     "c4": "C4: LIST<INT32> (maxD 3, maxR 1) + dictionary STRING (10%% nulls), V1, Snappy, %d rows, %d-row row groups",
     "c5": "C5: TPC-H lineitem-shaped 16 columns, Snappy, V1, %d rows, %d-row row groups (one GPU's 32 of 256 RGs)",
+    "c5gz": "C5 under GZIP (level 6): TPC-H lineitem-shaped 16 columns, V1, %d rows, %d-row row groups",
 }
 
-DTYPE = {"c1": "int64", "c2": "int32", "c2runs": "int32", "c3": "int64+f64 bits", "c4": "int32+bytes", "c5": "int64/int32/f64 bits/bytes"}
+DTYPE = {"c1": "int64", "c2": "int32", "c2runs": "int32", "c3": "int64+f64 bits", "c4": "int32+bytes", "c5": "int64/int32/f64 bits/bytes",
+         "c5gz": "int64/int32/f64 bits/bytes"}
 
 
 def _write(path, schema, gen, rows, rg_rows, **kw):
@@ -183,5 +187,9 @@ def make(cfg, path, rows, rg_rows, fixed_bw=0, **writer_kw):
         kw = dict(compression="snappy", data_page_version="1.0")
         kw.update(writer_kw)
         _write(path, schema, gen, rows, rg_rows, **kw)
+    elif cfg == "c5gz":
+        kw = dict(compression="gzip", compression_level=6)
+        kw.update(writer_kw)
+        make("c5", path, rows, rg_rows, **kw)
     else:
         raise ValueError("unknown config %r" % cfg)
