@@ -44,6 +44,18 @@ constexpr int GZ_FLUSH = 1024;
 constexpr uint32_t CRC_POLY = 0xEDB88320u;
 constexpr uint32_t E_CODEC = 5;  // PQG_ERR_CODEC (include/pqgpu.h)
 
+// Diagnostic build (-DPQ_GZ_STAMPS, tools/gzip_rate.py with PQGPU_LIB): the
+// first page's s_memtime cycles per phase and event counts, printed by lane 0.
+#ifdef PQ_GZ_STAMPS
+#define GZ_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define GZ_ADD(i, t) gz_acc[i] += __builtin_amdgcn_s_memtime() - (t)
+#define GZ_CNT(i) gz_cnt[i]++
+#else
+#define GZ_T(v)
+#define GZ_ADD(i, t)
+#define GZ_CNT(i)
+#endif
+
 enum : uint32_t { Y_LIT = 0, Y_SYM = 1, Y_EOB = 2, Y_BAD = 3, Y_SLOW = 4 };
 // table entry: value [0,16) | code bits [16,20) | extra bits [20,24) | kind [24,27)
 __device__ __forceinline__ uint32_t ent(uint32_t kind, uint32_t val, uint32_t bits, uint32_t extra) {
@@ -404,6 +416,10 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs a) {
   R.ip = p;
 
   // CRC shift of this lane's 16 bytes inside a 1 KiB flush, and of a flush
+#ifdef PQ_GZ_STAMPS
+  uint64_t gz_acc[6] = {0, 0, 0, 0, 0, 0}, gz_cnt[6] = {0, 0, 0, 0, 0, 0};
+  const uint64_t gz_t0 = __builtin_amdgcn_s_memtime();
+#endif
   const uint32_t x_lane = x8n((uint32_t)(16 * (63 - lane)));
   const uint32_t x_flush = x8n(GZ_FLUSH);
   uint32_t crc = 0;  // CRC-32 of the flushed bytes
@@ -467,6 +483,8 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs a) {
         tabs = 1;
       }
     } else {  // dynamic codes (3.2.7)
+      GZ_T(gz_tb);
+      GZ_CNT(0);
       tabs = 2;
       R.refill();
       if (R.nb < 14) { err = E_SIZE; break; }
@@ -542,6 +560,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs a) {
       for (int j = 0; j < (1 << (GZ_LB - 6)); j++) ltv[j] = S.lt[j * 64 + lane];
 #pragma unroll
       for (int j = 0; j < (1 << (GZ_DB - 6)); j++) dtv[j] = S.dt[j * 64 + lane];
+      GZ_ADD(0, gz_tb);
     }
     // ---- Huffman-coded data (3.2.5; zlib LEN .. MATCH) ----
     for (;;) {
@@ -555,7 +574,9 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs a) {
       uint32_t e;
       {
         const int lim = (int)ufirst((uint32_t)min(cap, min(f + GZ_FLUSH, o - q + 64)));
+        GZ_T(gz_tl);
         for (;;) {
+          GZ_CNT(1);
           R.refill();
           const uint32_t li = (uint32_t)R.bb & ((1u << GZ_LB) - 1);
           e = (uint32_t)__builtin_amdgcn_readlane((int)ltv[li >> 6], (int)(li & 63));
@@ -567,12 +588,18 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs a) {
           q++;
           o++;
         }
+        GZ_ADD(1, gz_tl);
       }
       if (q == 64 || o - f >= GZ_FLUSH) {
+        GZ_T(gz_fl);
+        GZ_CNT(2);
         put_lits();
         if (o - f >= GZ_FLUSH) flush(S.ring, dst, lane, f, crc, x_lane, x_flush);
+        GZ_ADD(2, gz_fl);
         continue;
       }
+      GZ_T(gz_gp);
+      GZ_CNT(3);
       if (e_kind(e) == Y_SLOW) e = slow_decode<K_LENS, GZ_LB>(R.bb, S.lsorted, lcv);
       const int L = (int)e_bits(e);
       if (L > R.nb) { err = E_SIZE; break; }
@@ -587,6 +614,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs a) {
       }
       if (kind == Y_EOB) break;
       if (kind != Y_SYM) { err = E_CODEC; break; }  // 286 / 287, an unused code
+      GZ_CNT(4);
       const int lx = (int)e_extra(e);
       if (lx > R.nb) { err = E_SIZE; break; }
       const int len = (int)e_val(e) + (int)R.take(lx);
@@ -616,6 +644,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs a) {
       }
       o += len;
       if (o - f >= GZ_FLUSH) flush(S.ring, dst, lane, f, crc, x_lane, x_flush);
+      GZ_ADD(3, gz_gp);
     }
     put_lits();
   }
@@ -654,6 +683,14 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs a) {
     }
   }
   if (err && lane == 0) atomicMin(&a.status[page], make_status(ST_DECOMPRESS, err));
+#ifdef PQ_GZ_STAMPS
+  if (blockIdx.x == 0 && lane == 0)
+    printf("GZSTAMP out %d in %d total %llu tables %llu/%llu litloop %llu/%llu flush %llu/%llu general %llu/%llu copies %llu\n",
+           o, n, (unsigned long long)(__builtin_amdgcn_s_memtime() - gz_t0), (unsigned long long)gz_acc[0],
+           (unsigned long long)gz_cnt[0], (unsigned long long)gz_acc[1], (unsigned long long)gz_cnt[1],
+           (unsigned long long)gz_acc[2], (unsigned long long)gz_cnt[2], (unsigned long long)gz_acc[3],
+           (unsigned long long)gz_cnt[3], (unsigned long long)gz_cnt[4]);
+#endif
 }
 
 }  // namespace
