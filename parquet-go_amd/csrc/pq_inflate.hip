@@ -587,6 +587,17 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs a) {
           lbuf = lane == q ? (e & 0xffu) : lbuf;
           q++;
           o++;
+          // a second literal without the refill check (the exits are only
+          // taken at the top, after a refill)
+          const uint32_t li2 = (uint32_t)R.bb & ((1u << GZ_LB) - 1);
+          const uint32_t e2 = (uint32_t)__builtin_amdgcn_readlane((int)ltv[li2 >> 6], (int)(li2 & 63));
+          const int L2 = (int)(e2 >> 16);
+          if (L2 > R.nb || o >= lim) continue;
+          R.bb >>= L2;
+          R.nb -= L2;
+          lbuf = lane == q ? (e2 & 0xffu) : lbuf;
+          q++;
+          o++;
         }
         GZ_ADD(1, gz_tl);
       }
@@ -634,12 +645,18 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs a) {
       if (o + len > cap) { err = E_SIZE; break; }   // partial copy, then no room
       put_lits();
       // the copy, 64 bytes a step: sources [o - dist, o) (periodic when dist < len)
-      for (int k0 = 0; k0 < len; k0 += 64) {
-        const int k = k0 + lane;
-        if (k < len) {
-          const int sp = o - dist + (dist >= len ? k : (int)((uint32_t)k % (uint32_t)dist));
-          const uint8_t b = S.ring[sp & (GZ_RING - 1)];
-          S.ring[(o + k) & (GZ_RING - 1)] = b;
+      if (dist >= len) {
+        for (int k0 = 0; k0 < len; k0 += 64) {
+          const int k = k0 + lane;
+          if (k < len) S.ring[(o + k) & (GZ_RING - 1)] = S.ring[(o - dist + k) & (GZ_RING - 1)];
+        }
+      } else {
+        for (int k0 = 0; k0 < len; k0 += 64) {
+          const int k = k0 + lane;
+          if (k < len) {
+            const int sp = o - dist + (int)((uint32_t)k % (uint32_t)dist);
+            S.ring[(o + k) & (GZ_RING - 1)] = S.ring[sp & (GZ_RING - 1)];
+          }
         }
       }
       o += len;
