@@ -316,6 +316,40 @@ def pmc_traffic(args):
     return res or None
 
 
+def gather_classes(args, rg0, rg1, decode_ms):
+    """C2 only: the decode phase split by dictionary-index bit-width class,
+    from the per-width rates tools/bw_sweep.sh measured (tools/gather_classes.json;
+    single-width files, same kernel) and this shard's rows per width (row
+    group i has bit width 1 + i % 20, tools/synth.py).  Names the share of the
+    phase the L2-bound widths take, beside the gather ceilings."""
+    ref = json.load(open(os.path.join(ROOT, "tools", "gather_classes.json")))
+    rates = {int(k): v for k, v in ref["by_bit_width"].items()}
+    known = sorted(rates)
+
+    def rate(bw):
+        if bw in rates:
+            return rates[bw]
+        lo = max(k for k in known if k < bw)
+        hi = min(k for k in known if k > bw)
+        return rates[lo] + (rates[hi] - rates[lo]) * (bw - lo) / (hi - lo)
+    rows = {}
+    for i in range(rg0, rg1):
+        bw = 1 + i % 20
+        rows[bw] = rows.get(bw, 0) + min(args.rg_rows, args.rows * max(1, args.gpus) - i * args.rg_rows)
+    ms = {bw: n / (rate(bw) * 1e9) * 1e3 for bw, n in rows.items()}
+    total = sum(ms.values())
+    out = {"unit": "Gval/s", "source": ref["source"], "ceilings": ref["ceilings"], "classes": {}}
+    for name, bws in ref["classes"].items():
+        n = sum(rows.get(b, 0) for b in bws)
+        t = sum(ms.get(b, 0.0) for b in bws)
+        if n:
+            out["classes"][name] = {"rows": n, "Gval_per_s": round(n / (t * 1e-3) / 1e9, 1),
+                                    "predicted_ms": round(t, 4), "time_share": round(t / total, 3)}
+    out["predicted_decode_ms"] = round(total, 4)
+    out["measured_decode_ms"] = round(decode_ms, 4)
+    return out
+
+
 def segment_times(reader, rg0, rg1, decodes=6):
     """Every pipeline phase timed with HIP events (PQG_SEGMENT_TIMES=1) on a
     second batch of the same shard, outside the timed loop (each event adds a
@@ -794,6 +828,11 @@ def main():
                             "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                             "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
                             "pipeline_frac": round((in_b + out_b) / per_step / 1e9 / HBM_PEAK_GBPS, 4)}
+        if args.config == "c2" and not args.bw and "k_decode+k_expand" in seg:
+            try:
+                line["roofline"]["gather_classes"] = gather_classes(args, rg0, rg1, seg["k_decode+k_expand"])
+            except Exception as e:  # (analysis figure only)
+                line["roofline"]["gather_classes"] = {"error": str(e)}
         trace = None if args.no_prof or args.no_pmc else kernel_trace(args)
         if trace:
             line["config"]["kernel_trace_us_per_step"] = {
