@@ -8,6 +8,7 @@
 // of page payload goes to HBM in one hipMemcpyAsync per batch; decompression
 // (Snappy) and all decoding run in pq_kernels.hip.
 #include <chrono>
+#include <ctype.h>
 #include <errno.h>
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
@@ -18,6 +19,8 @@
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
+#include <pthread.h>
+#include <sched.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -505,8 +508,47 @@ bool codec_builtin(int codec, bool *registered) {
 // (memcpy from the file mapping) is split into parts run by the pool and the
 // calling thread together, so the copy into pinned memory keeps up with the
 // PCIe DMA (one thread copies at about half the DMA rate).
+// The GPU's NUMA node (its PCI device's numa_node in sysfs) and the CPUs of
+// that node this process may run on: the pinned upload ring is allocated and
+// first touched there, and the gather threads run there, so the H2D DMA
+// reads memory on the GPU's own socket (the box of round 6: GPU on node 1 of
+// 2, the process allowed on all 256 CPUs of both; tools/numa_probe.py).
+// PQG_NO_NUMA=1 (analysis) leaves placement to the scheduler.
+static bool gpu_node_cpus(int device, cpu_set_t *out) {
+  char bdf[64] = {0};
+  if (hipDeviceGetPCIBusId(bdf, (int)sizeof(bdf), device) != hipSuccess) return false;
+  for (char *q = bdf; *q; q++) *q = (char)tolower((unsigned char)*q);
+  char path[256];
+  snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bdf);
+  FILE *f = fopen(path, "r");
+  int node = -1;
+  if (!f) return false;
+  if (fscanf(f, "%d", &node) != 1) node = -1;
+  fclose(f);
+  if (node < 0) return false;
+  snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
+  f = fopen(path, "r");
+  if (!f) return false;
+  char list[4096] = {0};
+  const bool ok = fgets(list, sizeof(list), f) != nullptr;
+  fclose(f);
+  if (!ok) return false;
+  cpu_set_t allowed;
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return false;
+  CPU_ZERO(out);
+  for (char *tok = strtok(list, ",\n"); tok; tok = strtok(nullptr, ",\n")) {
+    int a = -1, b = -1;
+    if (sscanf(tok, "%d-%d", &a, &b) < 2) b = a;
+    for (int c = a; c >= 0 && c <= b && c < CPU_SETSIZE; c++)
+      if (CPU_ISSET(c, &allowed)) CPU_SET(c, out);
+  }
+  return CPU_COUNT(out) > 0;
+}
+
 struct GatherPool {
   std::vector<std::thread> th;
+  cpu_set_t cpus;          // where the threads run (when `bind`)
+  bool bind = false;
   std::mutex mu;
   std::condition_variable go, done_cv;
   std::function<void(int)> job;
@@ -516,6 +558,7 @@ struct GatherPool {
   void start(int n) {
     for (int i = 0; i < n; i++)
       th.emplace_back([this] {
+        if (bind) pthread_setaffinity_np(pthread_self(), sizeof(cpus), &cpus);
         uint64_t seen = 0;
         std::unique_lock<std::mutex> lk(mu);
         for (;;) {
@@ -626,15 +669,27 @@ static int ring_upload(pqg_ctx *c, uint8_t *dst, const Layout &in, hipStream_t s
   const size_t n = in.n;
   std::lock_guard<std::mutex> lk(c->upload_mu);
   if (!c->pin[0]) {
+    // allocated and first touched by this thread moved to the GPU's node
+    static const bool numa_off = knob_flag("PQG_NO_NUMA");
+    cpu_set_t old;
+    bool moved = false;
+    if (!numa_off && gpu_node_cpus(c->device, &c->pool.cpus) &&
+        pthread_getaffinity_np(pthread_self(), sizeof(old), &old) == 0) {
+      c->pool.bind = true;
+      moved = pthread_setaffinity_np(pthread_self(), sizeof(c->pool.cpus), &c->pool.cpus) == 0;
+    }
     for (int i = 0; i < pqg_ctx::kRingBufs; i++) {
       if (hipHostMalloc(&c->pin[i], pqg_ctx::kRingBytes, hipHostMallocDefault) != hipSuccess ||
           hipEventCreateWithFlags(&c->pin_ev[i], hipEventDisableTiming) != hipSuccess) {
         c->pin[i] = nullptr;
+        if (moved) pthread_setaffinity_np(pthread_self(), sizeof(old), &old);
         for (const auto &r : in.ranges)  // pageable fallback
           if (r.len && hipMemcpy(dst + r.off, r.src, r.len, hipMemcpyHostToDevice) != hipSuccess) return 1;
         return 0;
       }
+      memset(c->pin[i], 0, pqg_ctx::kRingBytes);
     }
+    if (moved) pthread_setaffinity_np(pthread_self(), sizeof(old), &old);
   }
   if (!c->pool_started) {
     const char *e = getenv("PQG_UPLOAD_THREADS");
