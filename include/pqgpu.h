@@ -215,6 +215,20 @@ void *pqg_batch_stream(const pqg_batch *b);
 int pqg_batch_sync(pqg_batch *b);
 int pqg_batch_error_location(const pqg_batch *b, int *rg, int *leaf, int *page);
 int pqg_batch_column(const pqg_batch *b, int i, pqg_column_view *out);
+/* Columns with max_rep >= 2 (List<...List<T>>; the reference's ColumnStore
+ * keeps them as levels + values, data_store.go:158-203, schema.go:171-264):
+ * the list structure, built on the GPU from the levels (kept for such
+ * columns; pqg_column_view.def_levels / rep_levels).  level k = 1..max_rep:
+ * the level-k lists' int32 offsets (count + 1 entries) into the level-(k+1)
+ * lists — for k = max_rep into the leaf slots — and their validity bitmap
+ * (LSB first; non-null iff def >= the k-th repeated ancestor's def level - 1);
+ * level max_rep + 1: the leaf slots' validity (def == max_def: slot j holds the
+ * next dense value), offsets NULL.  Device pointers, valid until the next
+ * decode; *count from the last synced decode.  PQG_ERR_ARG for other columns
+ * or levels, PQG_ERR_UNSUPPORTED past 8 repetition levels. */
+int pqg_batch_column_nest(const pqg_batch *b, int i, int level, void **offsets, void **validity, int64_t *count);
+/* Copy one of them to host memory: what 0 = offsets, 1 = validity. */
+int pqg_batch_copy_nest(pqg_batch *b, int i, int level, int what, void *dst, size_t cap, size_t *nbytes);
 /* Copy one output buffer of selected column i to host memory. */
 int pqg_batch_copy(pqg_batch *b, int i, int buf_id, void *dst, size_t cap, size_t *nbytes);
 /* Fills min(size, sizeof(pqg_batch_stats)) bytes of *out (pass sizeof(*out));

@@ -136,6 +136,28 @@ struct SwRes {     // per page, k_sw_link -> k_prepare / k_dict_prepare / k_sw_e
   int32_t pad;
 };
 // k_reset: a device buffer zeroed at the start of every decode
+// k_nest_count / k_nest_write (pq_nest.hip): the list structure of a column
+// with max_rep >= 2 from its decoded levels.  Per level entry i, flag f_0 =
+// rep == 0 (a row: a level-1 list starts) and f_k = rep <= k && def >=
+// rdef[k] (an element of a level-k list, k = 1..max_rep; f_k also starts a
+// level-(k+1) list).  Level k's offsets: at the j-th f_(k-1) entry, the
+// number of f_k entries before it; its validity: def >= rdef[k] - 1.  The
+// leaf slots (f_max_rep entries): validity def == max_def.
+constexpr int NEST_MAXR = 8;
+constexpr int NEST_CH = 4096;  // level entries a block
+struct NestArgs {
+  const uint8_t *def, *rep;
+  int64_t n;
+  int32_t max_rep, max_def;
+  int32_t rdef[NEST_MAXR + 1];  // rdef[k]: def level of the k-th repeated ancestor
+  int32_t *sums;                // per block: counts of f_0 .. f_max_rep
+  int32_t *off;                 // level k's offsets at off + ostride * (k - 1)
+  uint32_t *val;                // level k's validity at val + vstride * (k - 1); the leaf slots' at k = max_rep + 1
+  int64_t ostride, vstride;
+  int64_t *cnt;                 // totals of f_0 .. f_max_rep
+  int32_t nblocks;
+};
+
 // k_inflate's arguments (pq_inflate.hip): the gzip pages, one wave each.
 struct InflateArgs {
   const uint8_t *in;

@@ -103,6 +103,7 @@ struct pq_launch_args {
 };
 int pq_launch(int which, const pq_launch_args *p, hipStream_t s);
 int pq_launch_inflate(const pq::InflateArgs *a, hipStream_t s);  // pq_inflate.hip
+int pq_launch_nest(const pq::NestArgs *a, hipStream_t s);        // pq_nest.hip
 extern int pq_launch_fail_which, pq_launch_fail_err;
 static constexpr int64_t kSnapSeg = 65536;  // pq_kernels.hip SNAP_SEG
 }
@@ -774,6 +775,7 @@ struct pqg_file {
   std::vector<SchemaElem> schema;
   std::vector<RowGroupMeta> rgs;
   std::vector<pqg_column_info> leaves;
+  std::vector<std::vector<int>> leaf_rdefs;  // per leaf: def level of each repeated ancestor, outermost first
   int64_t num_rows = 0;
   std::string err;
   ~pqg_file() {
@@ -798,6 +800,12 @@ struct ColumnPlan {
        *str_offsets = nullptr, *def_out = nullptr, *rep_out = nullptr;
   size_t values_bytes = 0, validity_bytes = 0, list_off_bytes = 0, list_val_bytes = 0, str_off_bytes = 0;
   int64_t slots = 0, rows = 0, str_bytes = 0;
+  // max_rep >= 2: every level's offsets / validity and the leaf slots'
+  // validity (k_nest_*, pq_nest.hip), from the emitted levels
+  std::vector<int> rdefs;  // def level of each repeated ancestor
+  void *nest_off = nullptr, *nest_val = nullptr, *nest_sums = nullptr, *nest_cnt = nullptr;
+  int64_t nest_ostride = 0, nest_vstride = 0;
+  int32_t nest_nblocks = 0;
 };
 
 struct pqg_batch {
@@ -1117,7 +1125,8 @@ int pqg_decompress_block(pqg_ctx *ctx, int codec, const uint8_t *src, size_t src
 // ---------------------------------------------------------------------------
 // file
 // ---------------------------------------------------------------------------
-static int walk_schema(pqg_file *f, size_t &idx, const std::string &prefix, int d, int r, int rep_def, int depth) {
+static int walk_schema(pqg_file *f, size_t &idx, const std::string &prefix, int d, int r, int rep_def, int depth,
+                       std::vector<int> rdefs = {}) {
   if (depth > 64 || idx >= f->schema.size()) return PQG_ERR_SCHEMA;
   const SchemaElem &e = f->schema[idx];
   if (e.name.empty() || !e.has_rep) return PQG_ERR_SCHEMA;  // schema.go:792-798
@@ -1125,6 +1134,7 @@ static int walk_schema(pqg_file *f, size_t &idx, const std::string &prefix, int 
   if (e.repetition == 2) {                                  // :804-806
     r++;
     rep_def = d;
+    rdefs.push_back(d);
   }
   std::string name = prefix.empty() ? e.name : prefix + "." + e.name;
   idx++;
@@ -1146,10 +1156,11 @@ static int walk_schema(pqg_file *f, size_t &idx, const std::string &prefix, int 
     L.unsigned_int = uns;
     L.value_width = value_width(e.type, e.type_length);
     f->leaves.push_back(L);
+    f->leaf_rdefs.push_back(rdefs);
     return 0;
   }
   for (int c = 0; c < e.num_children; c++) {
-    int rc = walk_schema(f, idx, name, d, r, rep_def, depth + 1);
+    int rc = walk_schema(f, idx, name, d, r, rep_def, depth + 1, rdefs);
     if (rc) return rc;
   }
   return 0;
@@ -2048,6 +2059,11 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     cp.flags = 0;
     if (cp.info.max_rep > 0 || cp.info.physical_type == T_BYTE_ARRAY) cp.flags |= COL_NEEDS_COUNT;
     if (flags & PQG_BATCH_LEVELS) cp.flags |= COL_EMIT_LEVELS;
+    // max_rep >= 2: the levels are kept (the nested offsets are built from them)
+    if (cp.info.max_rep >= 2) {
+      cp.flags |= COL_EMIT_LEVELS;
+      if ((size_t)l < f->leaf_rdefs.size()) cp.rdefs = f->leaf_rdefs[(size_t)l];
+    }
     cp.levels = 0;
     B->cols.push_back(cp);
   }
@@ -2856,6 +2872,16 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     c.str_offsets = (int64_t *)cp.str_offsets;
     c.def_out = (uint8_t *)cp.def_out;
     c.rep_out = (uint8_t *)cp.rep_out;
+    if (c.max_rep >= 2 && c.max_rep <= NEST_MAXR && (int)cp.rdefs.size() == c.max_rep) {
+      const int R = c.max_rep;
+      cp.nest_ostride = cp.levels + 1;
+      cp.nest_vstride = (cp.levels + 32) / 32;
+      cp.nest_nblocks = (int32_t)((cp.levels + NEST_CH - 1) / NEST_CH);
+      rc |= alloc_dev(&cp.nest_off, sizeof(int32_t) * (size_t)(R * cp.nest_ostride));
+      rc |= alloc_dev(&cp.nest_val, sizeof(uint32_t) * (size_t)((R + 1) * cp.nest_vstride));
+      rc |= alloc_dev(&cp.nest_sums, sizeof(int32_t) * (size_t)(R + 1) * (size_t)(cp.nest_nblocks + 1));
+      rc |= alloc_dev(&cp.nest_cnt, sizeof(int64_t) * (size_t)(R + 1));
+    }
   }
   if (rc) return PQG_ERR_DEVICE;
   if (!B->cols.empty())
@@ -3295,6 +3321,36 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     if (big && big_order == 2) hipStreamWaitEvent(s, LN.join[1], 0);
     if (B->ngen_flat > 0) hipStreamWaitEvent(s, LN.join[0], 0);
     if (B->ngen_nest > 0) hipStreamWaitEvent(s, LN.join[2], 0);
+    // nested (max_rep >= 2) columns: offsets and validity of every level
+    // from the levels k_decode emitted
+    if (!upto_scan) {
+      for (const ColumnPlan &cp : B->cols) {
+        if (!cp.nest_off) continue;
+        const int R = cp.info.max_rep;
+        hipMemsetAsync(cp.nest_val, 0, sizeof(uint32_t) * (size_t)((R + 1) * cp.nest_vstride), s);
+        if (cp.levels == 0) {
+          hipMemsetAsync(cp.nest_off, 0, sizeof(int32_t) * (size_t)(R * cp.nest_ostride), s);
+          hipMemsetAsync(cp.nest_cnt, 0, sizeof(int64_t) * (size_t)(R + 1), s);
+          continue;
+        }
+        NestArgs na;
+        memset(&na, 0, sizeof(na));
+        na.def = (const uint8_t *)cp.def_out;
+        na.rep = (const uint8_t *)cp.rep_out;
+        na.n = cp.levels;
+        na.max_rep = R;
+        na.max_def = cp.info.max_def;
+        for (int k = 1; k <= R; k++) na.rdef[k] = cp.rdefs[(size_t)k - 1];
+        na.sums = (int32_t *)cp.nest_sums;
+        na.off = (int32_t *)cp.nest_off;
+        na.val = (uint32_t *)cp.nest_val;
+        na.ostride = cp.nest_ostride;
+        na.vstride = cp.nest_vstride;
+        na.cnt = (int64_t *)cp.nest_cnt;
+        na.nblocks = cp.nest_nblocks;
+        if (pq_launch_nest(&na, s)) e |= 1;
+      }
+    }
     mark(true);
     a.list = B->d_lists + ns + nd;
     a.nlist = ndata;
@@ -3420,6 +3476,42 @@ int pqg_batch_column(const pqg_batch *B, int i, pqg_column_view *v) {
   return PQG_OK;
 }
 
+int pqg_batch_column_nest(const pqg_batch *B, int i, int level, void **offsets, void **validity, int64_t *count) {
+  if (!B || i < 0 || i >= (int)B->cols.size()) return PQG_ERR_ARG;
+  const ColumnPlan &cp = B->cols[(size_t)i];
+  const int R = cp.info.max_rep;
+  if (R < 2 || level < 1 || level > R + 1) return PQG_ERR_ARG;
+  if (!cp.nest_off) {
+    set_err("leaf %d: nested offsets need max_rep <= %d", cp.leaf, NEST_MAXR);
+    return PQG_ERR_UNSUPPORTED;
+  }
+  HIPCHK(hipSetDevice(B->ctx->device));
+  int64_t cnt[NEST_MAXR + 1];
+  HIPCHK(hipMemcpy(cnt, cp.nest_cnt, sizeof(int64_t) * (size_t)(R + 1), hipMemcpyDeviceToHost));
+  if (offsets) *offsets = level <= R ? (void *)((int32_t *)cp.nest_off + cp.nest_ostride * (level - 1)) : nullptr;
+  if (validity) *validity = (void *)((uint32_t *)cp.nest_val + cp.nest_vstride * (level - 1));
+  if (count) *count = cnt[level - 1];
+  return PQG_OK;
+}
+
+int pqg_batch_copy_nest(pqg_batch *B, int i, int level, int what, void *dst, size_t cap, size_t *nbytes) {
+  void *off = nullptr, *val = nullptr;
+  int64_t n = 0;
+  const int rc = pqg_batch_column_nest(B, i, level, &off, &val, &n);
+  if (rc) return rc;
+  const void *src = what == 0 ? off : val;
+  const size_t bytes = what == 0 ? (off ? sizeof(int32_t) * (size_t)(n + 1) : 0) : (size_t)((n + 7) / 8);
+  if (what != 0 && what != 1) return PQG_ERR_ARG;
+  if (nbytes) *nbytes = bytes;
+  if (!dst || !bytes) return PQG_OK;
+  if (cap < bytes) {
+    set_err("destination too small");
+    return PQG_ERR_ARG;
+  }
+  HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return PQG_OK;
+}
+
 int pqg_batch_copy(pqg_batch *B, int i, int buf, void *dst, size_t cap, size_t *nbytes) {
   if (!B || i < 0 || i >= (int)B->cols.size()) return PQG_ERR_ARG;
   HIPCHK(hipSetDevice(B->ctx->device));
@@ -3541,6 +3633,10 @@ void pqg_batch_destroy(pqg_batch *B) {
     free_dev(cp.str_offsets);
     free_dev(cp.def_out);
     free_dev(cp.rep_out);
+    free_dev(cp.nest_off);
+    free_dev(cp.nest_val);
+    free_dev(cp.nest_sums);
+    free_dev(cp.nest_cnt);
   }
   free_dev(B->d_in_alloc);
   free_dev(B->d_info);

@@ -59,7 +59,7 @@ EXPORTS = [
     "pqg_file_row_group_cost", "pqg_batch_stream",
     "pqg_file_column_count", "pqg_file_column_info", "pqg_file_find_column", "pqg_file_select_columns",
     "pqg_file_last_error", "pqg_batch_create", "pqg_batch_decode", "pqg_batch_sync",
-    "pqg_batch_error_location", "pqg_batch_row_groups", "pqg_batch_column", "pqg_batch_copy", "pqg_batch_stats_get",
+    "pqg_batch_error_location", "pqg_batch_row_groups", "pqg_batch_column", "pqg_batch_copy", "pqg_batch_column_nest", "pqg_batch_copy_nest", "pqg_batch_stats_get",
     "pqg_batch_kernel_times", "pqg_batch_set_timing", "pqg_batch_destroy",
     "pqg_stream_open", "pqg_stream_next", "pqg_stream_close", "pqg_file_open_many", "pqg_release_cache",
 ]
@@ -139,6 +139,8 @@ def lib():
                 "pqg_batch_row_groups": (i32, [vp, P(ctypes.c_int), P(ctypes.c_int)]),
                 "pqg_batch_column": (i32, [vp, i32, P(ColumnView)]),
                 "pqg_batch_copy": (i32, [vp, i32, i32, vp, sz, P(sz)]),
+                "pqg_batch_column_nest": (i32, [vp, i32, i32, P(vp), P(vp), P(ctypes.c_int64)]),
+                "pqg_batch_copy_nest": (i32, [vp, i32, i32, i32, vp, sz, P(sz)]),
                 "pqg_batch_stats_get": (i32, [vp, P(BatchStats), sz]),
                 "pqg_batch_kernel_times": (i32, [vp, P(ctypes.c_char_p), P(ctypes.c_float), i32]),
                 "pqg_batch_set_timing": (i32, [vp, i32]),
@@ -299,6 +301,31 @@ class Batch:
         out = np.empty(n.value, np.uint8)
         if n.value:
             _check(lib().pqg_batch_copy(self._h, i, buf, out.ctypes.data, n.value, ctypes.byref(n)))
+        return out
+
+    def nest(self, i):
+        """Selected column i with max_rep >= 2: the list structure
+        (pqg_batch_column_nest) as host arrays — for each repetition level k
+        = 1..max_rep {"offsets": int32[count + 1], "validity": uint8 bitmap,
+        "count": lists}, then the leaf slots {"validity", "count"}."""
+        out = []
+        k = 1
+        while True:
+            cnt = ctypes.c_int64()
+            rc = lib().pqg_batch_column_nest(self._h, i, k, None, None, ctypes.byref(cnt))
+            if rc == 1 and k > 1:  # PQG_ERR_ARG: past the leaf slots
+                break
+            _check(rc, "pqg_batch_column_nest")
+            lvl = {"count": cnt.value}
+            for what, name in ((0, "offsets"), (1, "validity")):
+                n = ctypes.c_size_t()
+                _check(lib().pqg_batch_copy_nest(self._h, i, k, what, None, 0, ctypes.byref(n)))
+                a = np.empty(n.value, np.uint8)
+                if n.value:
+                    _check(lib().pqg_batch_copy_nest(self._h, i, k, what, a.ctypes.data, n.value, ctypes.byref(n)))
+                lvl[name] = a.view(np.int32) if what == 0 else a
+            out.append(lvl)
+            k += 1
         return out
 
     def column(self, i):
