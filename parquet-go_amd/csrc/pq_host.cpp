@@ -3283,7 +3283,13 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     // (k_plain_str beside k_decode<2> on another side stream, and the tiled
     // expand beside both, were measured on C5: 24.50 vs 24.28 ms — the three
     // are throughput-bound and only slowed each other)
-    if (str_side) hipStreamWaitEvent(s, LN.join[1], 0);
+    // the tiled expand beside the string side stream, joined after it (round
+    // 6, C5: 16.12 / 16.11 -> 15.97 / 15.92 ms, C4 unchanged; with round 4's
+    // k_decode<2> for the dictionary strings it had been slower).
+    // PQG_EXPAND_AFTER_STR=1 (analysis): after the strings, as before
+    static const bool expand_after = knob_flag("PQG_EXPAND_AFTER_STR");
+    const bool late_str_join = str_side && !expand_after && B->dba_list.empty();
+    if (str_side && !late_str_join) hipStreamWaitEvent(s, LN.join[1], 0);
     if (!B->dba_list.empty()) {  // DELTA_BYTE_ARRAY value bytes (after k_decode's offsets)
       a.list = B->d_lists + ns + nd + ndata + ngen;
       a.nlist = (int32_t)B->dba_list.size();
@@ -3319,6 +3325,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     }
     if (big && big_order == 0) e |= pq_launch(22, &a, s);
     if (big && big_order == 2) hipStreamWaitEvent(s, LN.join[1], 0);
+    if (late_str_join) hipStreamWaitEvent(s, LN.join[1], 0);
     if (B->ngen_flat > 0) hipStreamWaitEvent(s, LN.join[0], 0);
     if (B->ngen_nest > 0) hipStreamWaitEvent(s, LN.join[2], 0);
     // nested (max_rep >= 2) columns: offsets and validity of every level
