@@ -3233,9 +3233,23 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
       e |= pq_launch(14, &a, LN.side[0]);  // k_decode<1>: flat fixed-width pages
       hipEventRecord(LN.join[0], LN.side[0]);
     }
+    // k_plain_str on side stream 0 (after k_decode<1>), beside the
+    // dictionary strings on side stream 1 instead of before them (round 6,
+    // C5: 15.98 / 15.92 -> 15.70 / 15.72 ms; round 4's k_decode<2> had
+    // needed the wave slots).  PQG_PSTR_SERIAL=1 (analysis): the old order
+    static const bool pstr_serial = knob_flag("PQG_PSTR_SERIAL");
+    const bool pstr0 = !pstr_serial && npstr > 0;
+    if (pstr0) {
+      if (B->ngen_flat == 0) hipStreamWaitEvent(LN.side[0], LN.fork, 0);
+      pq_launch_args ap = a;
+      ap.list = B->d_lists + ns + nd + ndata + ngen + (int32_t)B->dba_list.size();
+      ap.nlist = npstr;
+      e |= pq_launch(23, &ap, LN.side[0]);
+      hipEventRecord(LN.join[0], LN.side[0]);
+    }
     if (str_side) {
       hipStreamWaitEvent(LN.side[1], LN.fork, 0);
-      if (npstr > 0) {  // k_plain_str: flat required PLAIN string pages, items of PLAIN_STR_ITEM values
+      if (npstr > 0 && !pstr0) {  // k_plain_str: flat required PLAIN string pages, items of PLAIN_STR_ITEM values
         a.list = B->d_lists + ns + nd + ndata + ngen + (int32_t)B->dba_list.size();
         a.nlist = npstr;
         e |= pq_launch(23, &a, LN.side[1]);
@@ -3280,9 +3294,10 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     a.list = B->d_lists + ns + nd + ndata;
     a.nlist = ng0;
     e |= pq_launch(3, &a, s);  // k_decode<0>: lists of strings, booleans, level output
-    // (k_plain_str beside k_decode<2> on another side stream, and the tiled
-    // expand beside both, were measured on C5: 24.50 vs 24.28 ms — the three
-    // are throughput-bound and only slowed each other)
+    // (round 4: k_plain_str beside k_decode<2> on another side stream, and
+    // the tiled expand beside both, measured on C5 24.50 vs 24.28 ms — slower
+    // then; with k_decode<4> for the dictionary strings both pay, see above
+    // and below)
     // the tiled expand beside the string side stream, joined after it (round
     // 6, C5: 16.12 / 16.11 -> 15.97 / 15.92 ms, C4 unchanged; with round 4's
     // k_decode<2> for the dictionary strings it had been slower).
@@ -3326,7 +3341,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     if (big && big_order == 0) e |= pq_launch(22, &a, s);
     if (big && big_order == 2) hipStreamWaitEvent(s, LN.join[1], 0);
     if (late_str_join) hipStreamWaitEvent(s, LN.join[1], 0);
-    if (B->ngen_flat > 0) hipStreamWaitEvent(s, LN.join[0], 0);
+    if (B->ngen_flat > 0 || pstr0) hipStreamWaitEvent(s, LN.join[0], 0);
     if (B->ngen_nest > 0) hipStreamWaitEvent(s, LN.join[2], 0);
     // nested (max_rep >= 2) columns: offsets and validity of every level
     // from the levels k_decode emitted
