@@ -819,6 +819,9 @@ struct pqg_batch {
   std::vector<int32_t> snappy_list, dict_list, data_list;
   std::vector<int32_t> gzip_list;  // gzip pages inflated by k_inflate (BODY_GZIP)
   int32_t gz_off = 0;              // their position in d_lists
+  // k_prepare split around the region-parallel length walk: the data pages
+  // without a walk (beside it) and those with one (after it), in d_lists
+  int32_t prep_a_off = 0, prep_a_n = 0, prep_b_off = 0, prep_b_n = 0;
   // Snappy segments: pages longer than kSnapSeg are decoded by one wave per
   // 64 KiB segment (k_snappy_walk finds the segment starts)
   std::vector<int32_t> seg_base;      // per Snappy-list position (+1): first segment
@@ -2635,6 +2638,14 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     });
     B->gz_off = (int32_t)lists.size();
     lists.insert(lists.end(), B->gzip_list.begin(), B->gzip_list.end());
+    B->prep_a_off = (int32_t)lists.size();
+    for (int32_t pi : B->data_list)
+      if (B->pages[(size_t)pi].swalk < 0) lists.push_back(pi);
+    B->prep_a_n = (int32_t)lists.size() - B->prep_a_off;
+    B->prep_b_off = (int32_t)lists.size();
+    for (int32_t pi : B->data_list)
+      if (B->pages[(size_t)pi].swalk >= 0) lists.push_back(pi);
+    B->prep_b_n = (int32_t)lists.size() - B->prep_b_off;
     // the small tables: one host image (256-byte aligned entries; the
     // zero-initialised ones are zeros in it) and one copy instead of a
     // synchronous copy or memset each (tens of µs apiece)
@@ -3169,16 +3180,16 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   const bool lvl_now = B->lvl_bytes && !lvl_early;
   // long PLAIN string pages: the length walk region-parallel (after the
   // copies and k_levels' non-null counts; k_prepare reads the result)
-  auto sw_walk = [&]() {
+  auto sw_walk = [&](hipStream_t ws) {
     if ((int32_t)B->sw_pages.size() == B->sw_ndict) return;
     pq_launch_args w = a;
     w.sw_items = B->d_sw_items + 2 * (size_t)B->sw_dict_items;
     w.n_sw_items = (int32_t)(B->sw_items.size() / 2) - B->sw_dict_items;
     w.sw_page0 = B->sw_ndict;
     w.n_sw_pages = (int32_t)B->sw_pages.size() - B->sw_ndict;
-    e |= pq_launch(28, &w, s);  // k_sw_regions
-    e |= pq_launch(29, &w, s);  // k_sw_link
-    e |= pq_launch(30, &w, s);  // k_sw_emit
+    e |= pq_launch(28, &w, ws);  // k_sw_regions
+    e |= pq_launch(29, &w, ws);  // k_sw_link
+    e |= pq_launch(30, &w, ws);  // k_sw_emit
   };
   if (fused) {
     a.list = B->d_lists + ns + nd;
@@ -3191,7 +3202,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     }
     if (B->data_may_defer && !B->all_srec) {  // pages that waited on k_copy (or on the length walk)
       if (lvl_now) e |= pq_launch(lv_id + 2, &a, s);
-      sw_walk();
+      sw_walk(s);
       e |= pq_launch(11, &a, s);
     }
   } else {
@@ -3209,8 +3220,29 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     a.list = B->d_lists + ns + nd;
     a.nlist = ndata;
     if (lvl_now) e |= pq_launch(lv_id, &a, s);  // k_levels
-    sw_walk();
-    if (!B->all_srec) e |= pq_launch(2, &a, s);  // (+ the run walk of tiled RLE_DICTIONARY pages)
+    // the region-parallel length walk and k_prepare of the pages that read it
+    // on side stream 0, k_prepare of every other page beside them (round 6,
+    // C5: 15.46 / 15.48 -> 15.22 / 15.26 ms).  PQG_PREP_SERIAL=1 (analysis):
+    // one k_prepare launch after the walk, as before
+    static const bool prep_serial = knob_flag("PQG_PREP_SERIAL");
+    if (!prep_serial && !B->all_srec && B->prep_b_n > 0 && B->prep_a_n > 0 && !B->seg_times) {
+      hipEventRecord(LN.fork, s);
+      hipStreamWaitEvent(LN.side[0], LN.fork, 0);
+      sw_walk(LN.side[0]);
+      pq_launch_args pb = a;
+      pb.list = B->d_lists + B->prep_b_off;
+      pb.nlist = B->prep_b_n;
+      e |= pq_launch(2, &pb, LN.side[0]);  // k_prepare: pages with a length walk
+      hipEventRecord(LN.join[0], LN.side[0]);
+      pq_launch_args pa = a;
+      pa.list = B->d_lists + B->prep_a_off;
+      pa.nlist = B->prep_a_n;
+      e |= pq_launch(2, &pa, s);  // k_prepare: the other pages (+ the run walk of tiled pages)
+      hipStreamWaitEvent(s, LN.join[0], 0);
+    } else {
+      sw_walk(s);
+      if (!B->all_srec) e |= pq_launch(2, &a, s);  // (+ the run walk of tiled RLE_DICTIONARY pages)
+    }
   }
   mark(false);
   }  // !resume
