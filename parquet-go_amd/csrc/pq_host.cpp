@@ -822,6 +822,13 @@ struct pqg_batch {
   // k_prepare split around the region-parallel length walk: the data pages
   // without a walk (beside it) and those with one (after it), in d_lists
   int32_t prep_a_off = 0, prep_a_n = 0, prep_b_off = 0, prep_b_n = 0;
+  // level / prepare / scan chain split by column kind (round 6): the data
+  // pages of repeated columns (all of them k_decode<3> / <5> pages) on side
+  // stream 2 up to their decode, the other columns' on the context stream,
+  // in d_lists; column runs [c0, c1) of each kind for k_scan
+  bool rep_split = false;
+  int32_t rep_off = 0, rep_n = 0, flat_off = 0, flat_n = 0;
+  std::vector<std::pair<int32_t, int32_t>> rep_cruns, flat_cruns;
   // Snappy segments: pages longer than kSnapSeg are decoded by one wave per
   // 64 KiB segment (k_snappy_walk finds the segment starts)
   std::vector<int32_t> seg_base;      // per Snappy-list position (+1): first segment
@@ -2620,6 +2627,35 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
       }
     }
   }
+  // the chain split by column kind: only when every data page of a repeated
+  // column is a k_decode<3> / <5> page (nothing else on the context stream
+  // reads their levels, counts or scanned bases) and no data page has a
+  // region-parallel length walk (that k_prepare split stays as it is)
+  std::vector<int32_t> rep_pages, flat_pages;
+  {
+    std::vector<char> in_nest(npages, 0);
+    for (int32_t pg : B->general_nest) in_nest[(size_t)pg] = 1;
+    bool ok = B->lvl_bytes > 0;
+    for (int32_t pi : B->data_list) {
+      const PageDesc &pd = B->pages[(size_t)pi];
+      if (pd.swalk >= 0) ok = false;
+      if (B->cols[(size_t)pd.col].info.max_rep > 0) {
+        rep_pages.push_back(pi);
+        ok &= in_nest[(size_t)pi] != 0;
+      } else {
+        flat_pages.push_back(pi);
+      }
+    }
+    static const bool no_split = knob_flag("PQG_NO_REP_SPLIT");  // (analysis: one chain, as before)
+    B->rep_split = ok && !no_split && !rep_pages.empty() && !flat_pages.empty();
+    B->rep_cruns.clear();
+    B->flat_cruns.clear();
+    for (int32_t c = 0; c < (int32_t)B->cols.size(); c++) {
+      auto &runs = B->cols[(size_t)c].info.max_rep > 0 ? B->rep_cruns : B->flat_cruns;
+      if (!runs.empty() && runs.back().second == c) runs.back().second = c + 1;
+      else runs.push_back({c, c + 1});
+    }
+  }
   B->general_list.insert(B->general_list.end(), B->general_nest.begin(), B->general_nest.end());
   B->general_nest.clear();
   {
@@ -2646,6 +2682,12 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     for (int32_t pi : B->data_list)
       if (B->pages[(size_t)pi].swalk >= 0) lists.push_back(pi);
     B->prep_b_n = (int32_t)lists.size() - B->prep_b_off;
+    B->rep_off = (int32_t)lists.size();
+    lists.insert(lists.end(), rep_pages.begin(), rep_pages.end());
+    B->rep_n = (int32_t)rep_pages.size();
+    B->flat_off = (int32_t)lists.size();
+    lists.insert(lists.end(), flat_pages.begin(), flat_pages.end());
+    B->flat_n = (int32_t)flat_pages.size();
     // the small tables: one host image (256-byte aligned entries; the
     // zero-initialised ones are zeros in it) and one copy instead of a
     // synchronous copy or memset each (tens of µs apiece)
@@ -3069,6 +3111,19 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   // PQG_LEVELS_LATE=1 (analysis): k_levels back after the Snappy phase
   static const bool lvl_late_env = knob("PQG_LEVELS_LATE") != nullptr;
   const bool lvl_early = !resume && B->lvl_bytes > 0 && !B->lvl_late && !B->seg_times && !lvl_late_env;
+  // repeated columns' level / prepare / scan chain on side stream 2, beside
+  // the other columns' (B->rep_split; not with the fused prepare-copy launch
+  // or phase timing)
+  const bool rsplit = !resume && B->rep_split && B->lvl_bytes > 0 && !lvl_early && !B->seg_times &&
+                      !(nd == 0 && (B->max_jobs > 0 || !B->hjobs.empty()));
+  auto scan_runs = [&](const std::vector<std::pair<int32_t, int32_t>> &runs, hipStream_t st) {
+    for (const auto &r : runs) {
+      pq_launch_args sc = a;
+      sc.cols = B->d_cols + r.first;
+      sc.ncols = r.second - r.first;
+      e |= pq_launch(4, &sc, st);  // k_scan over the run's columns
+    }
+  };
   if (!resume) {
   mark(false);
   // (k_levels first on the context stream with k_snappy on the side stream
@@ -3219,13 +3274,31 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     mark(false);
     a.list = B->d_lists + ns + nd;
     a.nlist = ndata;
-    if (lvl_now) e |= pq_launch(lv_id, &a, s);  // k_levels
+    if (rsplit) {
+      // repeated columns' pages on side stream 2: k_levels (two waves a
+      // page), k_prepare, k_scan of their columns, then their k_decode<5> /
+      // <3> below, beside the other columns' chain on the context stream
+      hipEventRecord(LN.fork, s);
+      hipStreamWaitEvent(LN.side[2], LN.fork, 0);
+      pq_launch_args ar = a;
+      ar.list = B->d_lists + B->rep_off;
+      ar.nlist = B->rep_n;
+      e |= pq_launch(24, &ar, LN.side[2]);  // k_levels<-1, true>
+      e |= pq_launch(2, &ar, LN.side[2]);   // k_prepare
+      if (B->any_count) scan_runs(B->rep_cruns, LN.side[2]);
+      a.list = B->d_lists + B->flat_off;
+      a.nlist = B->flat_n;
+      e |= pq_launch(19, &a, s);  // k_levels<-1, false>: the other columns' pages
+      e |= pq_launch(2, &a, s);   // k_prepare
+    } else if (lvl_now) e |= pq_launch(lv_id, &a, s);  // k_levels
     // the region-parallel length walk and k_prepare of the pages that read it
     // on side stream 0, k_prepare of every other page beside them (round 6,
     // C5: 15.46 / 15.48 -> 15.22 / 15.26 ms).  PQG_PREP_SERIAL=1 (analysis):
     // one k_prepare launch after the walk, as before
     static const bool prep_serial = knob_flag("PQG_PREP_SERIAL");
-    if (!prep_serial && !B->all_srec && B->prep_b_n > 0 && B->prep_a_n > 0 && !B->seg_times) {
+    if (rsplit) {
+      // (k_prepare launched above, per chain)
+    } else if (!prep_serial && !B->all_srec && B->prep_b_n > 0 && B->prep_a_n > 0 && !B->seg_times) {
       hipEventRecord(LN.fork, s);
       hipStreamWaitEvent(LN.side[0], LN.fork, 0);
       sw_walk(LN.side[0]);
@@ -3248,7 +3321,15 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   }  // !resume
   // scans only feed lists / strings (rerun on resume: with the outputs now
   // allocated they also write the closing list / string offsets)
-  if (B->any_count) e |= pq_launch(4, &a, s);
+  if (rsplit) {
+    if (B->any_count) scan_runs(B->flat_cruns, s);
+    if (upto_scan) {  // the counting pass ends with both chains
+      hipEventRecord(LN.join[2], LN.side[2]);
+      hipStreamWaitEvent(s, LN.join[2], 0);
+    }
+  } else if (B->any_count) {
+    e |= pq_launch(4, &a, s);
+  }
   mark(true);
   if (!upto_scan) {
     // the three k_decode instances run side by side: <1> and <2> on side
@@ -3305,7 +3386,7 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
       hipEventRecord(LN.join[1], LN.side[1]);
     }
     if (B->ngen_nest > 0) {
-      hipStreamWaitEvent(LN.side[2], LN.fork, 0);
+      if (!rsplit) hipStreamWaitEvent(LN.side[2], LN.fork, 0);  // (split: side stream 2 carries its own chain)
       a.list = B->d_lists + ns + nd + ndata + ng0 + B->ngen_flat + B->ngen_str;
       a.nlist = B->ngen_nest;
       const int32_t nparts = (int32_t)(B->nest_parts.size() / 3);
