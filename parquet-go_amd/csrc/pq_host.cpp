@@ -829,6 +829,13 @@ struct pqg_batch {
   bool rep_split = false;
   int32_t rep_off = 0, rep_n = 0, flat_off = 0, flat_n = 0;
   std::vector<std::pair<int32_t, int32_t>> rep_cruns, flat_cruns;
+  // scan / decode split by length walk (see where it is planned): column runs
+  // with (w) and without (o) walked pages, and the walked columns'
+  // k_decode<4> pages (the last ngen_str4_w of that launch's list)
+  bool sw_split = false;
+  int32_t ngen_str4_w = 0;
+  std::vector<std::pair<int32_t, int32_t>> w_cruns, o_cruns;
+  std::vector<char> w_col;  // per column: it has a walked page
   // Snappy segments: pages longer than kSnapSeg are decoded by one wave per
   // 64 KiB segment (k_snappy_walk finds the segment starts)
   std::vector<int32_t> seg_base;      // per Snappy-list position (+1): first segment
@@ -2554,6 +2561,43 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
   B->ngen_flat = (int32_t)B->general_flat.size();
   B->general_list.insert(B->general_list.end(), B->general_flat.begin(), B->general_flat.end());
   B->general_flat.clear();
+  {
+    // the chain split by length walk (round 6): columns with a
+    // region-parallel length walk (C5's l_comment) are scanned and decoded on
+    // side stream 0 after the walk, the other columns' scan and decode start
+    // when their own k_prepare ends.  Only when every page of a walked column
+    // is a k_plain_str or k_decode<4> page and every k_plain_str page belongs
+    // to one; their k_decode<4> pages go last in that launch's list
+    std::vector<char> &wcol = B->w_col;
+    wcol.assign(B->cols.size(), 0);
+    std::vector<char> in_p(npages, 0), in_4(npages, 0);
+    bool any_w = false, any_o = false;
+    for (int32_t pi : B->data_list)
+      if (B->pages[(size_t)pi].swalk >= 0) wcol[(size_t)B->pages[(size_t)pi].col] = 1, any_w = true;
+    for (size_t i = 0; i < B->pstr_items.size(); i += 2) in_p[(size_t)B->pstr_items[i]] = 1;
+    for (int32_t pg : B->general_str4) in_4[(size_t)pg] = 1;
+    bool ok = any_w && B->general_nest.empty();
+    for (int32_t pi : B->data_list) {
+      const PageDesc &pd = B->pages[(size_t)pi];
+      if (wcol[(size_t)pd.col]) ok &= in_p[(size_t)pi] || in_4[(size_t)pi];
+      else any_o = true, ok &= !in_p[(size_t)pi];
+    }
+    static const bool no_split = knob_flag("PQG_NO_WALK_SPLIT");  // (analysis: one scan, as before)
+    B->sw_split = ok && any_o && !no_split;
+    B->ngen_str4_w = 0;
+    B->w_cruns.clear();
+    B->o_cruns.clear();
+    if (B->sw_split) {
+      std::stable_partition(B->general_str4.begin(), B->general_str4.end(),
+                            [&](int32_t pg) { return !wcol[(size_t)B->pages[(size_t)pg].col]; });
+      for (int32_t pg : B->general_str4) B->ngen_str4_w += wcol[(size_t)B->pages[(size_t)pg].col];
+      for (int32_t c = 0; c < (int32_t)B->cols.size(); c++) {
+        auto &runs = wcol[(size_t)c] ? B->w_cruns : B->o_cruns;
+        if (!runs.empty() && runs.back().second == c) runs.back().second = c + 1;
+        else runs.push_back({c, c + 1});
+      }
+    }
+  }
   B->ngen_str4 = (int32_t)B->general_str4.size();
   B->ngen_str = (int32_t)(B->general_str4.size() + B->general_str.size());
   {
@@ -2674,13 +2718,19 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     });
     B->gz_off = (int32_t)lists.size();
     lists.insert(lists.end(), B->gzip_list.begin(), B->gzip_list.end());
+    // (with the walk split, every page of a walked column is prepared after
+    // the walk: that chain's k_scan reads all of its columns' pages)
+    auto after_walk = [&](int32_t pi) {
+      const PageDesc &pd = B->pages[(size_t)pi];
+      return pd.swalk >= 0 || (B->sw_split && B->w_col[(size_t)pd.col]);
+    };
     B->prep_a_off = (int32_t)lists.size();
     for (int32_t pi : B->data_list)
-      if (B->pages[(size_t)pi].swalk < 0) lists.push_back(pi);
+      if (!after_walk(pi)) lists.push_back(pi);
     B->prep_a_n = (int32_t)lists.size() - B->prep_a_off;
     B->prep_b_off = (int32_t)lists.size();
     for (int32_t pi : B->data_list)
-      if (B->pages[(size_t)pi].swalk >= 0) lists.push_back(pi);
+      if (after_walk(pi)) lists.push_back(pi);
     B->prep_b_n = (int32_t)lists.size() - B->prep_b_off;
     B->rep_off = (int32_t)lists.size();
     lists.insert(lists.end(), rep_pages.begin(), rep_pages.end());
@@ -3116,6 +3166,11 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
   // or phase timing)
   const bool rsplit = !resume && B->rep_split && B->lvl_bytes > 0 && !lvl_early && !B->seg_times &&
                       !(nd == 0 && (B->max_jobs > 0 || !B->hjobs.empty()));
+  // walked columns' scan and decode on side stream 0 after the length walk,
+  // the other columns' from the end of their own k_prepare (B->sw_split)
+  static const bool prep_serial = knob_flag("PQG_PREP_SERIAL");
+  const bool wsplit = !resume && !rsplit && B->sw_split && !B->seg_times && !prep_serial && !B->all_srec &&
+                      B->prep_b_n > 0 && B->prep_a_n > 0 && !(nd == 0 && (B->max_jobs > 0 || !B->hjobs.empty()));
   auto scan_runs = [&](const std::vector<std::pair<int32_t, int32_t>> &runs, hipStream_t st) {
     for (const auto &r : runs) {
       pq_launch_args sc = a;
@@ -3295,7 +3350,6 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     // on side stream 0, k_prepare of every other page beside them (round 6,
     // C5: 15.46 / 15.48 -> 15.22 / 15.26 ms).  PQG_PREP_SERIAL=1 (analysis):
     // one k_prepare launch after the walk, as before
-    static const bool prep_serial = knob_flag("PQG_PREP_SERIAL");
     if (rsplit) {
       // (k_prepare launched above, per chain)
     } else if (!prep_serial && !B->all_srec && B->prep_b_n > 0 && B->prep_a_n > 0 && !B->seg_times) {
@@ -3306,12 +3360,13 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
       pb.list = B->d_lists + B->prep_b_off;
       pb.nlist = B->prep_b_n;
       e |= pq_launch(2, &pb, LN.side[0]);  // k_prepare: pages with a length walk
+      if (wsplit && B->any_count) scan_runs(B->w_cruns, LN.side[0]);  // k_scan: the walked columns
       hipEventRecord(LN.join[0], LN.side[0]);
       pq_launch_args pa = a;
       pa.list = B->d_lists + B->prep_a_off;
       pa.nlist = B->prep_a_n;
       e |= pq_launch(2, &pa, s);  // k_prepare: the other pages (+ the run walk of tiled pages)
-      hipStreamWaitEvent(s, LN.join[0], 0);
+      if (!wsplit) hipStreamWaitEvent(s, LN.join[0], 0);
     } else {
       sw_walk(s);
       if (!B->all_srec) e |= pq_launch(2, &a, s);  // (+ the run walk of tiled RLE_DICTIONARY pages)
@@ -3327,6 +3382,9 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
       hipEventRecord(LN.join[2], LN.side[2]);
       hipStreamWaitEvent(s, LN.join[2], 0);
     }
+  } else if (wsplit) {
+    if (B->any_count) scan_runs(B->o_cruns, s);  // (the walked columns': side stream 0, above)
+    if (upto_scan) hipStreamWaitEvent(s, LN.join[0], 0);
   } else if (B->any_count) {
     e |= pq_launch(4, &a, s);
   }
@@ -3339,6 +3397,19 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     const bool str_side = B->ngen_str > 0 || npstr > 0;
     const bool fork = B->ngen_flat > 0 || str_side || B->ngen_nest > 0;
     if (fork) hipEventRecord(LN.fork, s);
+    // the walked columns' k_decode<4> pages on side stream 2 once their scan
+    // (side stream 0) is done, not behind the other columns' <4> pages
+    const int32_t n4w = wsplit ? B->ngen_str4_w : 0;
+    if (n4w > 0) {
+      hipEventRecord(LN.join[2], LN.side[0]);
+      hipStreamWaitEvent(LN.side[2], LN.join[2], 0);
+      hipStreamWaitEvent(LN.side[2], LN.fork, 0);
+      pq_launch_args aw4 = a;
+      aw4.list = B->d_lists + ns + nd + ndata + ng0 + B->ngen_flat + (B->ngen_str4 - n4w);
+      aw4.nlist = n4w;
+      e |= pq_launch(31, &aw4, LN.side[2]);  // k_decode<4>: the walked columns' dictionary pages
+      hipEventRecord(LN.join[2], LN.side[2]);
+    }
     if (B->ngen_flat > 0) {
       hipStreamWaitEvent(LN.side[0], LN.fork, 0);
       a.list = B->d_lists + ns + nd + ndata + ng0;
@@ -3368,9 +3439,9 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
         e |= pq_launch(23, &a, LN.side[1]);
       }
       a.list = B->d_lists + ns + nd + ndata + ng0 + B->ngen_flat;
-      a.nlist = B->ngen_str4;
+      a.nlist = B->ngen_str4 - n4w;
       e |= pq_launch(31, &a, LN.side[1]);  // k_decode<4>: flat required dictionary strings
-      a.list += B->ngen_str4;
+      a.list = B->d_lists + ns + nd + ndata + ng0 + B->ngen_flat + B->ngen_str4;
       a.nlist = B->ngen_str - B->ngen_str4;
       if (B->str_split) {
         pq_launch_args ap = a;
@@ -3454,8 +3525,8 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     if (big && big_order == 0) e |= pq_launch(22, &a, s);
     if (big && big_order == 2) hipStreamWaitEvent(s, LN.join[1], 0);
     if (late_str_join) hipStreamWaitEvent(s, LN.join[1], 0);
-    if (B->ngen_flat > 0 || pstr0) hipStreamWaitEvent(s, LN.join[0], 0);
-    if (B->ngen_nest > 0) hipStreamWaitEvent(s, LN.join[2], 0);
+    if (B->ngen_flat > 0 || pstr0 || wsplit) hipStreamWaitEvent(s, LN.join[0], 0);
+    if (B->ngen_nest > 0 || n4w > 0) hipStreamWaitEvent(s, LN.join[2], 0);
     // nested (max_rep >= 2) columns: offsets and validity of every level
     // from the levels k_decode emitted
     if (!upto_scan) {
