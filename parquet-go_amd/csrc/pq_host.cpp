@@ -822,6 +822,7 @@ struct pqg_batch {
   // k_prepare split around the region-parallel length walk: the data pages
   // without a walk (beside it) and those with one (after it), in d_lists
   int32_t prep_a_off = 0, prep_a_n = 0, prep_b_off = 0, prep_b_n = 0;
+  int32_t prep_bw = 0;  // the first prep_bw of the after-walk list: walked columns' pages without a walk
   // level / prepare / scan chain split by column kind (round 6): the data
   // pages of repeated columns (all of them k_decode<3> / <5> pages) on side
   // stream 2 up to their decode, the other columns' on the context stream,
@@ -1008,9 +1009,22 @@ int pqg_ctx_create(int device, pqg_ctx **out) {
     set_err("hipStreamCreate failed");
     return PQG_ERR_DEVICE;
   }
+  // side stream 0 at the device's greatest priority: it carries the chain
+  // that ends a C5 step (the length walk, the walked columns' scan and
+  // k_plain_str), and the dispatcher then favours its waves over the other
+  // columns' decode (C5 14.72 / 14.74 -> 14.56 / 14.48 ms; C2, C3, C4
+  // unchanged: profiles/r06/evidence/side_prio_*.txt).  PQG_SIDE_PRIO
+  // (analysis): three digits, side streams 0..2, '0' default priority, '1'
+  // the greatest, '2' the least
+  int prio_lo = 0, prio_hi = 0;
+  hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  const char *sp = knob("PQG_SIDE_PRIO") ? knob("PQG_SIDE_PRIO") : "100";
   for (int i = 0; i < 3; i++) {
-    if (hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming) != hipSuccess) {
+    const char m = sp && (int)strlen(sp) > i ? sp[i] : '0';
+    const hipError_t se = m == '0' ? hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking)
+                                   : hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking,
+                                                                 m == '1' ? prio_hi : prio_lo);
+    if (se != hipSuccess || hipEventCreateWithFlags(&c->join[i], hipEventDisableTiming) != hipSuccess) {
       set_err("hipStreamCreate failed");
       return PQG_ERR_DEVICE;
     }
@@ -2729,8 +2743,13 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
       if (!after_walk(pi)) lists.push_back(pi);
     B->prep_a_n = (int32_t)lists.size() - B->prep_a_off;
     B->prep_b_off = (int32_t)lists.size();
+    // (the walked columns' pages without a walk first: with the walk split
+    // they are prepared beside the walk, on side stream 2)
     for (int32_t pi : B->data_list)
-      if (after_walk(pi)) lists.push_back(pi);
+      if (after_walk(pi) && B->pages[(size_t)pi].swalk < 0) lists.push_back(pi);
+    B->prep_bw = (int32_t)lists.size() - B->prep_b_off;
+    for (int32_t pi : B->data_list)
+      if (after_walk(pi) && B->pages[(size_t)pi].swalk >= 0) lists.push_back(pi);
     B->prep_b_n = (int32_t)lists.size() - B->prep_b_off;
     B->rep_off = (int32_t)lists.size();
     lists.insert(lists.end(), rep_pages.begin(), rep_pages.end());
@@ -3355,11 +3374,23 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
     } else if (!prep_serial && !B->all_srec && B->prep_b_n > 0 && B->prep_a_n > 0 && !B->seg_times) {
       hipEventRecord(LN.fork, s);
       hipStreamWaitEvent(LN.side[0], LN.fork, 0);
-      sw_walk(LN.side[0]);
       pq_launch_args pb = a;
       pb.list = B->d_lists + B->prep_b_off;
       pb.nlist = B->prep_b_n;
+      if (wsplit && B->prep_bw > 0) {
+        // the walked columns' other pages (C5: l_comment's dictionary pages,
+        // 0.7 ms) prepared beside the walk on side stream 2
+        hipStreamWaitEvent(LN.side[2], LN.fork, 0);
+        pq_launch_args pw = pb;
+        pw.nlist = B->prep_bw;
+        e |= pq_launch(2, &pw, LN.side[2]);
+        hipEventRecord(LN.join[2], LN.side[2]);
+        pb.list += B->prep_bw;
+        pb.nlist -= B->prep_bw;
+      }
+      sw_walk(LN.side[0]);
       e |= pq_launch(2, &pb, LN.side[0]);  // k_prepare: pages with a length walk
+      if (wsplit && B->prep_bw > 0) hipStreamWaitEvent(LN.side[0], LN.join[2], 0);
       if (wsplit && B->any_count) scan_runs(B->w_cruns, LN.side[0]);  // k_scan: the walked columns
       hipEventRecord(LN.join[0], LN.side[0]);
       pq_launch_args pa = a;
