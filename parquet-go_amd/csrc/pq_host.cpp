@@ -889,6 +889,9 @@ struct pqg_batch {
   int64_t str_pre_entries = 0;     // prefix-table entries of the split pages (PageDesc::sp_base)
   bool str_split = false;          // some k_decode<2> page is split
   int32_t *d_str_parts = nullptr;
+  std::vector<int32_t> str4w_parts;  // walked columns' k_decode<4> waves: (page, first value, end value)
+  bool str4w_split = false;          // some of those pages is split
+  int32_t *d_str4w_parts = nullptr;
   int64_t *d_str_pre = nullptr;
   int32_t *d_part_pre = nullptr;  // per part: counts before it (k_levels -> k_decode<3>)
   void *d_jobs = nullptr;        // deferred long-literal copy jobs (k_snappy -> k_copy)
@@ -2648,6 +2651,39 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
       }
     }
   }
+  {
+    // the walked columns' k_decode<4> pages (walk split: C5's l_comment
+    // dictionary pages, ~20,000 values and a ~1 MiB dictionary each, the
+    // step's last 64 waves) in parts as k_decode<2>'s above: a part's values
+    // before it are its first entry (required column), their string bytes
+    // from k_prepare's prefix table.  PQG_NO_STR4_PARTS (analysis): whole pages
+    B->str4w_parts.clear();
+    B->str4w_split = false;
+    static const bool no_p4 = knob_flag("PQG_NO_STR4_PARTS");
+    static const int64_t spart4 = knob("PQG_STR_PART") ? atoll(knob("PQG_STR_PART")) : STR_PART;
+    const size_t n4 = B->general_str4.size();
+    for (size_t i = n4 - (size_t)B->ngen_str4_w; i < n4; i++) {
+      const int32_t pg = B->general_str4[i];
+      PageDesc &pd = B->pages[(size_t)pg];
+      const int64_t n = std::max(pd.num_values, 0);
+      pd.sp_base = -1;
+      const bool can = !no_p4 && spart4 > 0 && pd.enc == ENC_RLE_DICT && pd.dict >= 0 &&
+                       B->cols[(size_t)pd.col].info.max_def == 0 && n >= 2 * spart4;
+      if (!can) {
+        B->str4w_parts.insert(B->str4w_parts.end(), {pg, 0, (int32_t)n});
+        continue;
+      }
+      pd.sp_base = B->str_pre_entries;
+      B->str_pre_entries += n / 256 + 2;
+      B->str4w_split = true;
+      for (int64_t lo = 0; lo < n;) {
+        int64_t hi = ((pd.level_base + lo + spart4 + 255) & ~(int64_t)255) - pd.level_base;
+        if (n - hi < spart4 / 2) hi = n;
+        B->str4w_parts.insert(B->str4w_parts.end(), {pg, (int32_t)lo, (int32_t)hi});
+        lo = hi;
+      }
+    }
+  }
   B->general_list.insert(B->general_list.end(), B->general_str4.begin(), B->general_str4.end());
   B->general_list.insert(B->general_list.end(), B->general_str.begin(), B->general_str.end());
   B->general_str4.clear();
@@ -2777,6 +2813,7 @@ static int batch_init(pqg_batch *B, pqg_ctx *ctx, pqg_file *f, int rg_begin, int
     tab.put((void **)&B->d_part_pre, nullptr, sizeof(int32_t) * 4 * (B->nest_parts.size() / 3 + 1));
     tab.put((void **)&B->d_str_parts, B->str_parts.data(), sizeof(int32_t) * B->str_parts.size());
     tab.put((void **)&B->d_str_pre, nullptr, sizeof(int64_t) * (size_t)(B->str_pre_entries + 1));
+    tab.put((void **)&B->d_str4w_parts, B->str4w_parts.data(), sizeof(int32_t) * B->str4w_parts.size());
     tab.put((void **)&B->d_lgroups, B->lgroups.data(), sizeof(LdsGroup) * (B->lgroups.size() + 1));
     tab.put((void **)&B->d_page_jobs, pj.data(), sizeof(int32_t) * pj.size());
     tab.put((void **)&B->d_sitems, B->snap_items.data(), 4 * B->snap_items.size());
@@ -3438,7 +3475,17 @@ static int launch_all(pqg_batch *B, bool upto_scan, bool timed) {
       pq_launch_args aw4 = a;
       aw4.list = B->d_lists + ns + nd + ndata + ng0 + B->ngen_flat + (B->ngen_str4 - n4w);
       aw4.nlist = n4w;
-      e |= pq_launch(31, &aw4, LN.side[2]);  // k_decode<4>: the walked columns' dictionary pages
+      if (B->str4w_split) {
+        pq_launch_args ap = aw4;
+        ap.parts = B->d_str4w_parts;
+        ap.nlist = (int32_t)(B->str4w_parts.size() / 3);
+        e |= pq_launch(31, &ap, LN.side[2]);  // k_decode<4>: the walked columns' dictionary pages, in parts
+        ap = aw4;
+        ap.redo = 1;
+        e |= pq_launch(31, &ap, LN.side[2]);  // k_decode<4>: pages whose later parts failed, whole
+      } else {
+        e |= pq_launch(31, &aw4, LN.side[2]);  // k_decode<4>: the walked columns' dictionary pages
+      }
       hipEventRecord(LN.join[2], LN.side[2]);
     }
     if (B->ngen_flat > 0) {

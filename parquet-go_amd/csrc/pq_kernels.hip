@@ -4197,7 +4197,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   // KIND 2 with a.parts: entries [e_lo, e_hi) of a flat dictionary-string
   // page; the values before e_lo are counted from k_levels' level scratch,
   // their string bytes taken from k_prepare's prefix table (PageDesc::sp_base)
-  const bool part = ((KIND == 3 || KIND == 2) && a.parts != nullptr) || KIND == 5;
+  // KIND 4 with a.parts: as KIND 2's, for a required column (the values
+  // before e_lo are e_lo; the walked columns' dictionary pages, C5)
+  const bool part = ((KIND == 3 || KIND == 2 || KIND == 4) && a.parts != nullptr) || KIND == 5;
   int page;
   int64_t e_lo = 0, e_hi = 0x7fffffffffffll;
   if (part) {
@@ -4207,7 +4209,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   } else {
     page = ufirst(a.list[gi]);
   }
-  if ((KIND == 3 || KIND == 2) && a.redo) {
+  if ((KIND == 3 || KIND == 2 || KIND == 4) && a.redo) {
     if (page_status(a.status, page) != make_status(ST_REDO, 0)) return;
     if (lane == 0) __hip_atomic_store(&a.status[page], STATUS_OK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else if (page_status(a.status, page) != STATUS_OK) {
@@ -4322,14 +4324,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == 1 ?
   int64_t e0 = 0, slot_run = 0, row_run = 0, nn_run = 0, str_run = pi.str_base;
   uint32_t err = E_OK, err_stage = 0;
   const int64_t e_end = part ? min<int64_t>(e_hi, (int64_t)n) : (int64_t)n;
-  if (KIND == 2 && part && e_lo > 0) {
-    // (only dictionary pages with a level scratch and a prefix table are split)
-    if (d.sp_base < 0 || d.enc != ENC_RLE_DICT || !(d.lvl_bits || d.lvl_base >= 0)) {
+  if ((KIND == 2 || KIND == 4) && part && e_lo > 0) {
+    // (only dictionary pages with a prefix table and, nullable, a level
+    // scratch are split)
+    if (d.sp_base < 0 || d.enc != ENC_RLE_DICT || (KIND == 2 && !(d.lvl_bits || d.lvl_base >= 0)) ||
+        (KIND == 4 && c.max_def != 0)) {
       set_status(a.status, page, ST_REDO, 0);
       return;
     }
     int64_t cn = 0;  // values (def == max_def) among entries [0, e_lo)
-    if (d.lvl_bits) {
+    if (KIND == 4) {
+      cn = lane == 0 ? e_lo : 0;  // required: every entry is a value
+    } else if (d.lvl_bits) {
       const uint32_t *lw = (const uint32_t *)(a.lvl + d.lvl_base);
       const int64_t nw = e_lo >> 5;
       for (int64_t w = lane; w < nw; w += 64) cn += __popc(lw[w]);

@@ -634,6 +634,56 @@ def test_c5_lineitem_large_string_dictionary(tmp_path):
         del os.environ["PQG_SNAPPY_SEG_MIN"]
 
 
+def _walked_dict_column_bytes(compression):
+    """A required string column whose first 30,000 rows (a 100-word vocabulary)
+    are RLE_DICTIONARY pages (bit width 7) of 20,000 / 10,000 values; 16
+    5,000-byte strings then overflow the 64 KiB dictionary limit (116 entries:
+    keys 116-127 are out of range), and 40-byte strings after them are PLAIN
+    pages of 20,000 values (880 KB: region-parallel length walk); beside a
+    required INT64 column."""
+    rng = np.random.default_rng(43)
+    letters = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz", np.uint8)
+    word = lambda n: bytes(letters[rng.integers(0, 26, n)]).decode()
+    vocab = [word(12) for _ in range(100)]
+    rows = 90000
+    w = [vocab[i] for i in rng.integers(0, 100, 30000)] + [word(5000) for _ in range(16)]
+    w += [word(40) for _ in range(rows - len(w))]
+    t = _req_table({"x": rng.integers(-2**40, 2**40, rows, dtype=np.int64), "w": w})
+    return _pq_bytes(t, compression=compression, row_group_size=rows, dictionary_pagesize_limit=64 << 10,
+                     data_page_size=1 << 20, write_batch_size=16)
+
+
+def test_walked_column_dictionary_parts_corrupted():
+    """Walk split (pq_host.cpp: a column with region-parallel-walked PLAIN
+    pages is scanned and decoded after the walk, on side streams 0 / 2): that
+    column's dictionary pages go to k_decode<4> in parts of ~2,048 values.
+    Snappy and uncompressed, then seeded corruptions of the first dictionary
+    page's key stream past its first part — a later part's error sends the
+    page to the whole-page redo launch — against the oracle's outcome
+    (type_dict.go:44-53, hybrid_decoder.go:82-166)."""
+    pq = pytest.importorskip("pyarrow.parquet")
+    check_file(_walked_dict_column_bytes("snappy"), "walked dict column, snappy")
+    base = _walked_dict_column_bytes("none")
+    check_file(base, "walked dict column")
+    cc = pq.ParquetFile(io.BytesIO(base)).metadata.row_group(0).column(1)
+    lo = cc.dictionary_page_offset if cc.has_dictionary_page else cc.data_page_offset
+    assert cc.data_page_offset > lo  # (the dictionary page, then the key streams)
+    rng = np.random.default_rng(41)
+    outcomes = set()
+    for trial in range(10):
+        data = bytearray(base)
+        for _ in range(2):
+            p = cc.data_page_offset + int(rng.integers(4000, 16000))
+            data[p] = 0xff if trial % 2 == 0 else data[p] ^ int(rng.integers(1, 256))  # 0xff: a key of 127
+        check_file(bytes(data), "corrupt %d" % trial)
+        try:
+            oracle.File(bytes(data)).decode(1)
+            outcomes.add(0)
+        except oracle.OracleError as e:
+            outcomes.add(e.code)
+    assert len(outcomes - {0}) >= 1, outcomes  # some corruption is an error the redo launch reports
+
+
 @pytest.mark.parametrize("per,depth,ramp", [(1, 2, False), (2, 1, False), (3, 3, False), (4, 3, True)])
 def test_stream_slices_match_oracle(tmp_path, per, depth, ramp):
     """pqg_stream: row-group slices planned and uploaded by the host worker
