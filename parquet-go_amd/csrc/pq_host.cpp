@@ -1012,16 +1012,17 @@ int pqg_ctx_create(int device, pqg_ctx **out) {
     set_err("hipStreamCreate failed");
     return PQG_ERR_DEVICE;
   }
-  // side stream 0 at the device's greatest priority: it carries the chain
-  // that ends a C5 step (the length walk, the walked columns' scan and
-  // k_plain_str), and the dispatcher then favours its waves over the other
-  // columns' decode (C5 14.72 / 14.74 -> 14.56 / 14.48 ms; C2, C3, C4
-  // unchanged: profiles/r06/evidence/side_prio_*.txt).  PQG_SIDE_PRIO
-  // (analysis): three digits, side streams 0..2, '0' default priority, '1'
-  // the greatest, '2' the least
+  // PQG_SIDE_PRIO (analysis): three digits, side streams 0..2, '0' default
+  // priority, '1' the greatest, '2' the least.  Side stream 0 at the
+  // greatest priority gave C5 14.72 / 14.74 -> 14.56 / 14.48 ms but C1 0.0321
+  // -> 0.0330 ms (C2, C3, C4 unchanged); a separate greatest-priority stream
+  // for the walk-split batches alone cost C4 2.38 -> 2.87 ms and C5 0.7 ms
+  // (not understood; probably the streams' hardware-queue mapping, 4 queues
+  // a process on the box), so every side stream
+  // keeps the default priority (profiles/r06/evidence/side_prio_*.txt)
   int prio_lo = 0, prio_hi = 0;
   hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  const char *sp = knob("PQG_SIDE_PRIO") ? knob("PQG_SIDE_PRIO") : "100";
+  const char *sp = knob("PQG_SIDE_PRIO") ? knob("PQG_SIDE_PRIO") : "000";
   for (int i = 0; i < 3; i++) {
     const char m = sp && (int)strlen(sp) > i ? sp[i] : '0';
     const hipError_t se = m == '0' ? hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking)
